@@ -1,0 +1,188 @@
+"""Benchmark of the fused validate-and-count hot path (K1: BF.EXISTS +
+valid-gated PFADD) -- BASELINE.json's metric on its configs[1] (C2).
+
+One step = one K1 launch over one resident batch of synthetic swipes (C2: 1M
+swipes, 7-digit ids from a 100k-student population, 10 % invalid, 50
+lecture-day HLL keys, Bloom RESERVE 0.01 / 100k preloaded).  Inputs are
+generated on the GPU and resident in HBM before timing; each step consumes a
+distinct batch of the stream.  N>1: one process per GPU (torchrun), each rank
+runs its own stream over its own key shard with the Bloom replicated
+(no data-path collective; weak scaling).
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "swipes/sec (fused BF.EXISTS+PFADD) at 1/2/4/8 GPUs; % of HBM peak"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--batch", type=int, default=0, help="swipes per step (default: config)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--probe-batch", type=int, default=0)
+    ap.add_argument("--variant", type=int, default=-1, help="-1 auto, 0 global Bloom, 1 LDS Bloom")
+    ap.add_argument("--max-batches", type=int, default=64)
+    return ap.parse_args()
+
+
+def cpu_baseline(engine, pkg, w, p, b0, seconds):
+    """Oracle (C restatement of Redis/RedisBloom, 1 thread) running the
+    processor loop attendance_processor.py:100-137 (BF.EXISTS then PFADD) on
+    the same batch, repeated for ~`seconds`."""
+    import numpy as np
+    import __graft_entry__ as ge
+    orc = ge.load_oracle()
+    mbatch = engine.members_batch(p, 0, w.n_members)
+    mb, mo, _ = mbatch.to_host()
+    mbatch.free()
+    chain = orc.Chain(w.bf_capacity, w.bf_error)
+    chain.madd_packed(mb, mo)
+    buf, offs, slot = b0.to_host()
+    slot = slot.astype(np.uint32)
+    regs = np.zeros((int(slot.max()) + 1, 16384), np.uint8)
+    n, passes = len(offs) - 1, 0
+    t0 = time.perf_counter()
+    while True:
+        orc.process_swipes(chain, regs, slot, buf, offs)
+        passes += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n * passes / dt, "unit": "swipes/s", "cores": 1, "kind": "port",
+            "sample": f"{passes} passes over the first {n}-swipe batch (C oracle, "
+                      f"orc_process_swipes, 1 thread, {dt:.1f}s)"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import SketchEngine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    w = synthetic.WORKLOADS[args.config]
+    n = args.batch or w.n_swipes
+    engine = SketchEngine(local)
+    # a dedicated (non-null) stream shared by libsketch and the timing events
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    engine.set_stream(stream.cuda_stream)
+    if args.probe_batch:
+        engine.set_option("probe_batch", args.probe_batch)
+    if args.variant >= 0:
+        engine.set_option("variant", args.variant)
+
+    # Bloom preload (replicated on every rank), HLL key shard of this rank
+    engine.reserve(0, w.bf_error, w.bf_capacity)
+    p = engine.gen_params(w)
+    t0 = time.perf_counter()
+    engine.preload(0, p, w.n_members)
+    preload_s = time.perf_counter() - t0
+    engine.hll_reserve(w.n_keys)
+
+    nb = max(1, min(args.max_batches, args.steps + args.warmup))
+    batches = [engine.swipe_batch(p, (rank * nb + j) * n, n) for j in range(nb)]
+    probes, nvalid = engine.swipes_stats(0, batches[0])
+    width = len(str(w.id_hi - 1))
+
+    def step(j):
+        engine.swipes_async(0, batches[j % nb])
+
+    for j in range(args.warmup):
+        step(j)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for j in range(args.steps):
+        ev[j][0].record(stream)
+        step(args.warmup + j)
+        ev[j][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = world * n * args.steps / elapsed
+    # algorithmic bytes per launch: S_io per swipe (id bytes +
+    # u32 offset + u32 slot + u8 answer), one 64-B sector per RedisBloom probe
+    # (sequential count, measured), one 64-B sector read + write per PFADD
+    s_io = width + 4 + 4 + 1
+    alg_bytes = n * s_io + 64 * probes + 128 * nvalid
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "swipes/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (device counter-based generator, seed %d)" % w.seed,
+        "config": {"workload": w.name, "swipes_per_step": n, "students": w.n_members,
+                   "hll_keys_per_gpu": w.n_keys, "invalid_frac": w.invalid_frac,
+                   "bloom": {"error": w.bf_error, "capacity": w.bf_capacity},
+                   "id_bytes": width, "parallelism": f"dp{world} (key-sharded, Bloom replicated)",
+                   "k1_variant": "lds-bloom" if engine.variant(0) else "global-bloom",
+                   "probe_batch": args.probe_batch or 1},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "k_swipes", "kernel_ms": kern_ms,
+                     "alg_bytes_per_swipe": alg_bytes / n,
+                     "probes_per_swipe": probes / n, "valid_frac": nvalid / n},
+        "preload_s": preload_s,
+    }
+    if rank == 0 and not args.no_cpu and args.cpu_seconds > 0:
+        line["cpu_baseline"] = cpu_baseline(engine, pkg, w, p, batches[0], args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    for b in batches:
+        b.free()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,196 @@
+/*
+ * sketch.h -- C-ABI of libsketch, the MI355X (gfx950) sketch engine for the
+ * attendance validate-and-count hot path.
+ *
+ * The reference (devarshpatel1506/Real-Time-Student-Attendance-System) reaches
+ * this path through a redis-py client object (attendance_processor.py:37-41,
+ * data_generator.py:45-49).  Each entry point below replaces one family of the
+ * RESP round trips that client makes; the Python facade
+ * (real-time-student-attendance-system_amd/client.py) keeps the redis-py call
+ * surface and binds these symbols through ctypes (INTEGRATION.md shows the
+ * binding).
+ *
+ * Conventions
+ *   - return 0 (SKE_OK) or a negative SKE_E* code; no exception crosses the ABI;
+ *     ske_strerror() maps a code to the Redis / RedisBloom error text.
+ *   - the caller owns every input / output buffer.  `mem` says where the
+ *     buffers live: SKE_MEM_HOST (pageable host memory, staged through the
+ *     context's device buffers) or SKE_MEM_DEVICE (HIP device pointers, e.g.
+ *     torch-ROCm data_ptr(), used in place on the context stream).
+ *   - packed items: `bytes` + `offs[n+1]` (u32 byte offsets, offs[0] may be
+ *     non-zero).  Device byte buffers must stay readable up to the next 8-byte
+ *     boundary after bytes+offs[n] (any hipMalloc / torch allocation is).
+ *   - a context is single-threaded and stream-ordered; every call returns
+ *     after its work on the context stream completed, except ske_swipes_async.
+ *   - filters are addressed by a caller-chosen id `fid` < SKE_MAX_FILTERS, HLL
+ *     keys by a caller-chosen register-slab slot.  The facade maps Redis key
+ *     names to fids / slots.
+ */
+#ifndef SKETCH_H
+#define SKETCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SKE_OK 0
+#define SKE_EINVAL -1        /* bad argument */
+#define SKE_ENOMEM -2        /* device or host allocation failed */
+#define SKE_EHIP -3          /* HIP runtime error (see ske_last_hip_error) */
+#define SKE_ENOFILTER -4     /* fid not reserved */
+#define SKE_EEXISTS -5       /* BF.RESERVE on an existing key: "ERR item exists" */
+#define SKE_EFULL -6         /* non-scaling filter full */
+#define SKE_ERANGE -7        /* HLL slot outside the reserved slab */
+#define SKE_EBADRATE -8      /* "ERR (0 < error rate range < 1)" */
+#define SKE_EBADCAP -9       /* "ERR (capacity should be larger than 0)" */
+#define SKE_EBADEXP -10      /* "ERR expansion should be greater or equal to 1" */
+#define SKE_EBADHLL -11      /* corrupted HLL string on import */
+#define SKE_ETOOLONG -12     /* item longer than the supported maximum */
+
+#define SKE_MEM_HOST 0
+#define SKE_MEM_DEVICE 1
+
+#define SKE_MAX_FILTERS 4096
+#define SKE_MAX_LINKS 48
+#define SKE_HLL_REGISTERS 16384
+#define SKE_HLL_DENSE_BYTES 12288
+
+typedef struct ske_ctx ske_ctx;
+
+typedef struct {
+    uint64_t capacity;      /* sum of link entries   (BF.INFO Capacity) */
+    uint64_t size_bytes;    /* bytes of all bit arrays + headers (BF.INFO Size) */
+    uint32_t nfilters;      /* links in the chain    (BF.INFO Number of filters) */
+    uint32_t expansion;     /* growth factor         (BF.INFO Expansion rate) */
+    uint64_t inserted;      /* items added           (BF.INFO Number of items inserted) */
+    int32_t nonscaling;
+    int32_t pad_;
+} ske_bf_info_t;
+
+typedef struct {
+    uint64_t entries;  /* bloom->entries */
+    uint64_t bytes;    /* bloom->bytes */
+    uint64_t bits;     /* bloom->bits (modulus of the probe sequence) */
+    uint64_t size;     /* SBLink.size (items added to this link) */
+    double error;      /* bloom->error */
+    double bpe;        /* bloom->bpe */
+    int32_t hashes;    /* bloom->hashes (k) */
+    int32_t pad_;
+} ske_bf_link_t;
+
+/* Synthetic swipe stream (counter-based, device-side).  See DESIGN.md
+ * "Synthetic workload" for the exact definition; tests restate it in numpy. */
+typedef struct {
+    uint64_t seed;
+    uint64_t id_lo, id_hi;        /* IDs in [id_lo, id_hi), all with the same digit count */
+    uint64_t n_members;           /* valid population: first n_members of the permutation */
+    uint64_t perm_mul, perm_add;  /* member(i) = id_lo + (perm_mul*i + perm_add) mod R */
+    uint64_t perm_mul_inv;        /* perm_mul^-1 mod R (R = id_hi - id_lo < 2^32) */
+    uint32_t invalid_thresh;      /* P(invalid) * 2^32 */
+    uint32_t near_thresh;         /* P(near-collision | invalid) * 2^32 */
+    uint32_t n_keys;              /* HLL keys of this stream: slot_base + [0, n_keys) */
+    uint32_t slot_base;
+    const uint32_t *key_cdf;      /* optional device table (n_keys u32 CDF * 2^32); NULL = uniform */
+} ske_gen_params_t;
+
+/* ---- context ---- */
+int ske_open(int device, ske_ctx **out);
+int ske_close(ske_ctx *ctx);
+const char *ske_strerror(int code);
+const char *ske_last_hip_error(ske_ctx *ctx);
+int ske_set_stream(ske_ctx *ctx, void *hip_stream); /* NULL = the context's own stream */
+int ske_sync(ske_ctx *ctx);
+int ske_device_alloc(ske_ctx *ctx, uint64_t bytes, void **out); /* device scratch for callers */
+int ske_device_free(ske_ctx *ctx, void *p);
+int ske_memcpy(ske_ctx *ctx, void *dst, const void *src, uint64_t bytes, int kind); /* 0 H2D 1 D2H 2 D2D */
+
+/* ---- Bloom (RedisBloom SBChain) ----
+ * BF.RESERVE key error_rate capacity [EXPANSION e] [NONSCALING]
+ *   replaces: execute_command('BF.RESERVE', ...) attendance_processor.py:83-88
+ *   (also the implicit auto-create of BF.ADD: data_generator.py:59-63). */
+int ske_bf_reserve(ske_ctx *ctx, uint32_t fid, double error_rate, uint64_t capacity,
+                   uint32_t expansion, int nonscaling);
+int ske_bf_exists_key(ske_ctx *ctx, uint32_t fid); /* 1 if reserved, 0 if not */
+int ske_bf_free(ske_ctx *ctx, uint32_t fid);
+/* BF.MADD key item...  (BF.ADD = n 1), sequential RedisBloom semantics:
+ *   out[i] = 1 added, 0 already present, -2 non-scaling filter full.
+ *   replaces: execute_command('BF.ADD', BLOOM_FILTER_KEY, id) data_generator.py:59-63 */
+int ske_bf_madd(ske_ctx *ctx, uint32_t fid, const uint8_t *bytes, const uint32_t *offs,
+                uint64_t n, int8_t *out_or_null, int mem);
+/* BF.MEXISTS key item...  (BF.EXISTS = n 1); a missing key answers 0s.
+ *   replaces: execute_command('BF.EXISTS', BLOOM_FILTER_KEY, student_id)
+ *   attendance_processor.py:109-113 and the probe at :78 */
+int ske_bf_mexists(ske_ctx *ctx, uint32_t fid, const uint8_t *bytes, const uint32_t *offs,
+                   uint64_t n, uint8_t *out, int mem);
+/* BF.INFO / BF.DEBUG and BF.SCANDUMP-style raw bit arrays */
+int ske_bf_info(ske_ctx *ctx, uint32_t fid, ske_bf_info_t *out);
+int ske_bf_link_info(ske_ctx *ctx, uint32_t fid, uint32_t link, ske_bf_link_t *out);
+int ske_bf_export_link(ske_ctx *ctx, uint32_t fid, uint32_t link, uint8_t *out, uint64_t cap);
+int ske_bf_import_link(ske_ctx *ctx, uint32_t fid, uint32_t link, const uint8_t *in,
+                       uint64_t nbytes);
+
+/* ---- HyperLogLog register slab (Redis p=14, one byte per register) ---- */
+int ske_hll_reserve(ske_ctx *ctx, uint32_t nslots);  /* grow the slab to >= nslots keys */
+uint32_t ske_hll_capacity(ske_ctx *ctx);
+int ske_hll_clear(ske_ctx *ctx, uint32_t slot);      /* new / deleted key: zero registers */
+/* PFADD key element...  for many (key, element) pairs at once.
+ *   changed_or_null: per-element "this element raised a register" in the
+ *   given order (sequential Redis semantics); the facade folds it per call.
+ *   replaces: redis_client.pfadd(hll_key, student_id) attendance_processor.py:127-129 */
+int ske_hll_pfadd(ske_ctx *ctx, const uint32_t *slot, const uint8_t *bytes,
+                  const uint32_t *offs, uint64_t n, uint8_t *changed_or_null, int mem);
+/* PFCOUNT key [key ...] (union), one answer.  attendance_processor.py:152 */
+int ske_hll_pfcount(ske_ctx *ctx, const uint32_t *slots, uint32_t nkeys, uint64_t *out);
+/* PFCOUNT of each key separately (rankings, attendance_analysis.py:87-97 as
+ * README.md:179 describes); group form: union over slots[goffs[g]..goffs[g+1]). */
+int ske_hll_pfcount_each(ske_ctx *ctx, const uint32_t *slots, uint32_t nkeys, uint64_t *out,
+                         int mem);
+int ske_hll_pfcount_groups(ske_ctx *ctx, const uint32_t *slots, const uint32_t *goffs,
+                           uint32_t ngroups, uint64_t *out, int mem);
+/* PFMERGE dst src...  (dst's own registers take part, as in Redis) */
+int ske_hll_pfmerge(ske_ctx *ctx, uint32_t dst, const uint32_t *srcs, uint32_t n);
+int ske_hll_histogram(ske_ctx *ctx, uint32_t slot, uint32_t *out64);
+int ske_hll_export_raw(ske_ctx *ctx, uint32_t slot, uint8_t *out16384);
+int ske_hll_export_dense(ske_ctx *ctx, uint32_t slot, uint8_t *out12288);
+int ske_hll_import_raw(ske_ctx *ctx, uint32_t slot, const uint8_t *regs16384);
+/* raw device pointer of the slab (slot s at + s*16384), for RCCL max-reduce */
+int ske_hll_slab(ske_ctx *ctx, void **dev_ptr, uint64_t *bytes);
+/* dst_dev[g*16384 ..] = register max over slots[goffs[g]..goffs[g+1]) (K3 into an
+ * external device buffer, e.g. a torch tensor that RCCL then max-reduces);
+ * an empty group yields zeros.  slots / goffs are host arrays. */
+int ske_hll_merge_groups_dev(ske_ctx *ctx, const uint32_t *slots, const uint32_t *goffs,
+                             uint32_t ngroups, uint8_t *dst_dev);
+/* estimator only: PFCOUNT of raw register arrays already on the device */
+int ske_hll_count_raw_dev(ske_ctx *ctx, const uint8_t *regs_dev, uint32_t nkeys, uint64_t *out);
+
+/* ---- the fused hot path (K1) ----
+ * For every swipe i: v = BF.EXISTS fid id_i; if v: PFADD slot_i id_i.
+ *   replaces the per-event pair attendance_processor.py:109-113 + :127-129.
+ * out_valid (may be NULL) receives v per swipe. */
+int ske_swipes(ske_ctx *ctx, uint32_t fid, const uint32_t *slot, const uint8_t *bytes,
+               const uint32_t *offs, uint64_t n, uint8_t *out_valid, int mem);
+/* device-pointer form that only enqueues (no sync); for the benchmark */
+int ske_swipes_async(ske_ctx *ctx, uint32_t fid, const uint32_t *slot, const uint8_t *bytes,
+                     const uint32_t *offs, uint64_t n, uint8_t *out_valid);
+/* probe statistics of the same swipes (untimed): Bloom bit tests performed
+ * and valid count, to price the algorithmic bytes of the roofline. */
+int ske_swipes_stats(ske_ctx *ctx, uint32_t fid, const uint8_t *bytes, const uint32_t *offs,
+                     uint64_t n, uint64_t *probes, uint64_t *nvalid);
+/* which K1 variant the current chain selects: 1 = LDS-staged Bloom, 0 = global */
+int ske_swipes_variant(ske_ctx *ctx, uint32_t fid);
+int ske_set_option(ske_ctx *ctx, const char *name, int64_t value);
+
+/* ---- synthetic stream (device buffers) ---- */
+int ske_gen_members(ske_ctx *ctx, const ske_gen_params_t *p, uint64_t start, uint64_t n,
+                    uint8_t *bytes_dev, uint32_t *offs_dev);
+int ske_gen_swipes(ske_ctx *ctx, const ske_gen_params_t *p, uint64_t start, uint64_t n,
+                   uint8_t *bytes_dev, uint32_t *offs_dev, uint32_t *slot_dev);
+int ske_gen_id_width(const ske_gen_params_t *p); /* digits per ID */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

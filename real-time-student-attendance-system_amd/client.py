@@ -1,0 +1,739 @@
+"""SketchClient -- the redis-py call surface of the reference's hot path,
+executed on MI355X through libsketch.
+
+The reference builds one ``redis.Redis(host, port, decode_responses=True)``
+client per process (attendance_processor.py:37-41, data_generator.py:45-49)
+and uses exactly these calls on the validate-and-count path:
+
+=====================================================  ====================================
+reference call (file:line)                             here
+=====================================================  ====================================
+``execute_command('BF.EXISTS', key, id)`` (ap.py:109)  ``execute_command`` -> ske_bf_mexists
+``execute_command('BF.RESERVE', key, err, cap)`` (:83) ``execute_command`` -> ske_bf_reserve
+``execute_command('BF.ADD', key, id)`` (dg.py:59)      ``execute_command`` -> ske_bf_madd
+``pfadd(hll_key, student_id)`` (ap.py:129)             ``pfadd`` -> ske_hll_pfadd
+``pfcount(hll_key)`` (ap.py:152)                       ``pfcount`` -> ske_hll_pfcount
+=====================================================  ====================================
+
+plus the north-star surface: ``bf().reserve/add/madd/exists/mexists/info``,
+``pfmerge``, ``pipeline()`` and the batched ``swipes()`` (the fused K1 kernel:
+BF.EXISTS then valid-gated PFADD for a whole batch of events).
+
+Semantics kept from Redis / RedisBloom / redis-py:
+  * argument encoding as redis-py (``encoding.encode``);
+  * ``BF.EXISTS``/``BF.MEXISTS`` on a missing key answer 0 (so the
+    reference's probe at attendance_processor.py:78 never raises and its
+    ``BF.RESERVE`` branch never runs -- reproduced, not "fixed");
+  * ``BF.ADD``/``BF.MADD`` auto-create a chain (error 0.01, capacity 100,
+    expansion 2); ``BF.RESERVE`` on an existing key -> ``ERR item exists``;
+  * ``PFADD key`` with no elements creates the key and replies 1;
+    ``PFCOUNT`` of missing keys -> 0; keys of the other type -> WRONGTYPE.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import (BfInfo, BfLink, Context, SketchLibError, SKE_MEM_DEVICE, SKE_MEM_HOST,
+                   HLL_DENSE_BYTES, HLL_REGISTERS)
+from .encoding import encode, pack
+from .exceptions import DataError, ResponseError, WRONGTYPE
+
+BF_TYPE_NAME = "MBbloom--"  # RedisBloom's module type name (TYPE reply)
+_DEFAULT_ERROR = 0.01       # rebloom.c BFDefaultErrorRate
+_DEFAULT_CAPACITY = 100     # rebloom.c BFDefaultInitCapacity
+_DEFAULT_EXPANSION = 2      # rebloom.c BFDefaultExpansion
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _err(e: SketchLibError) -> ResponseError:
+    return ResponseError(str(e))
+
+
+class KeySpace:
+    """Key name -> device object (Bloom fid or HLL register-slab slot)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self.kind: dict[bytes, str] = {}
+        self.fid: dict[bytes, int] = {}
+        self.slot: dict[bytes, int] = {}
+        self._free_fids = list(range(_lib.SKE_MAX_FILTERS - 1, -1, -1))
+        self._free_slots: list[int] = []
+        self._next_slot = 0
+
+    def type_of(self, key: bytes) -> str | None:
+        return self.kind.get(key)
+
+    def expect(self, key: bytes, kind: str) -> bool:
+        """True if the key exists with this kind, False if missing; raises
+        WRONGTYPE if it holds the other kind."""
+        k = self.kind.get(key)
+        if k is None:
+            return False
+        if k != kind:
+            raise ResponseError(WRONGTYPE)
+        return True
+
+    def new_fid(self, key: bytes) -> int:
+        if not self._free_fids:
+            raise ResponseError("ERR too many Bloom filters on this device")
+        f = self._free_fids.pop()
+        self.kind[key] = "bf"
+        self.fid[key] = f
+        return f
+
+    def new_slot(self, key: bytes) -> int:
+        if self._free_slots:
+            s = self._free_slots.pop()
+        else:
+            s = self._next_slot
+            self._next_slot += 1
+            if s >= self.ctx.lib.ske_hll_capacity(self.ctx.ptr):
+                self.ctx.call("ske_hll_reserve", s + 1)
+        self.kind[key] = "hll"
+        self.slot[key] = s
+        return s
+
+    def drop(self, key: bytes) -> bool:
+        k = self.kind.pop(key, None)
+        if k == "bf":
+            f = self.fid.pop(key)
+            self.ctx.call("ske_bf_free", f)
+            self._free_fids.append(f)
+        elif k == "hll":
+            s = self.slot.pop(key)
+            self.ctx.call("ske_hll_clear", s)  # a reused slot starts empty
+            self._free_slots.append(s)
+        return k is not None
+
+    def release_unused_slot(self, key: bytes) -> None:
+        """Undo new_slot() for a key that no command ended up creating (its
+        registers were never written)."""
+        s = self.slot.pop(key)
+        del self.kind[key]
+        self._free_slots.append(s)
+
+
+class SketchClient:
+    """Drop-in for ``redis.Redis`` on the reference's Bloom + HLL calls."""
+
+    def __init__(self, host: str = "localhost", port: int = 6379, db: int = 0,
+                 decode_responses: bool = False, device: int = 0,
+                 context: Context | None = None, **_ignored):
+        self.ctx = context if context is not None else Context(device)
+        self.decode_responses = decode_responses
+        self.keys = KeySpace(self.ctx)
+        self.host, self.port, self.db = host, port, db
+
+    # ------------------------------------------------------------ helpers
+    def _ok(self):
+        return "OK" if self.decode_responses else b"OK"
+
+    def _s(self, text: str):
+        return text if self.decode_responses else text.encode()
+
+    def close(self) -> None:
+        pass  # the device context lives as long as the client object
+
+    def ping(self) -> bool:
+        return True
+
+    # ------------------------------------------------------------ generic keys
+    def delete(self, *names) -> int:
+        return sum(self.keys.drop(encode(n)) for n in names)
+
+    def exists(self, *names) -> int:
+        return sum(encode(n) in self.keys.kind for n in names)
+
+    def type(self, name):
+        k = self.keys.type_of(encode(name))
+        return self._s({"bf": BF_TYPE_NAME, "hll": "string", None: "none"}[k])
+
+    def flushall(self, *_a, **_k) -> bool:
+        for key in list(self.keys.kind):
+            self.keys.drop(key)
+        return True
+
+    flushdb = flushall
+
+    # ------------------------------------------------------------ Bloom
+    def _bf_reserve(self, key: bytes, error_rate, capacity, expansion=None, nonscaling=False):
+        try:
+            err = float(error_rate)
+        except (TypeError, ValueError):
+            raise ResponseError("ERR bad error rate")
+        try:
+            cap = int(capacity)
+        except (TypeError, ValueError):
+            raise ResponseError("ERR bad capacity")
+        if not (0 < err < 1):
+            raise ResponseError("ERR (0 < error rate range < 1)")
+        if cap <= 0:
+            raise ResponseError("ERR (capacity should be larger than 0)")
+        exp = _DEFAULT_EXPANSION if expansion is None else int(expansion)
+        if exp < 1 and not nonscaling:
+            raise ResponseError("ERR expansion should be greater or equal to 1")
+        if key in self.keys.kind:
+            if self.keys.kind[key] != "bf":
+                raise ResponseError(WRONGTYPE)
+            raise ResponseError("ERR item exists")
+        f = self.keys.new_fid(key)
+        try:
+            self.ctx.call("ske_bf_reserve", f, err, cap, exp, 1 if nonscaling else 0)
+        except SketchLibError as e:
+            self.keys.kind.pop(key, None)
+            self.keys.fid.pop(key, None)
+            self.keys._free_fids.append(f)
+            raise _err(e)
+        return self._ok()
+
+    def _bf_fid_for_add(self, key: bytes) -> int:
+        if self.keys.expect(key, "bf"):
+            return self.keys.fid[key]
+        f = self.keys.new_fid(key)
+        # rebloom.c: BF.ADD / BF.MADD on a missing key create a default chain
+        self.ctx.call("ske_bf_reserve", f, _DEFAULT_ERROR, _DEFAULT_CAPACITY, _DEFAULT_EXPANSION, 0)
+        return f
+
+    def bf_madd_packed(self, key, buf: np.ndarray, offs: np.ndarray) -> np.ndarray:
+        """BF.MADD over a packed batch; returns int8 replies (1 / 0 / -2 full)."""
+        key = encode(key)
+        f = self._bf_fid_for_add(key)
+        n = len(offs) - 1
+        out = np.zeros(n, np.int8)
+        if n:
+            self.ctx.call("ske_bf_madd", f, _ptr(buf), _ptr(offs), n, _ptr(out), SKE_MEM_HOST)
+        return out
+
+    def bf_mexists_packed(self, key, buf: np.ndarray, offs: np.ndarray) -> np.ndarray:
+        """BF.MEXISTS over a packed batch; missing key -> zeros."""
+        key = encode(key)
+        n = len(offs) - 1
+        out = np.zeros(n, np.uint8)
+        if not self.keys.expect(key, "bf") or n == 0:
+            return out
+        self.ctx.call("ske_bf_mexists", self.keys.fid[key], _ptr(buf), _ptr(offs), n, _ptr(out),
+                      SKE_MEM_HOST)
+        return out
+
+    def _bf_madd_reply(self, key: bytes, items: Sequence) -> list:
+        buf, offs = pack(items)
+        res = self.bf_madd_packed(key, buf, offs)
+        return [ResponseError("ERR non scaling filter is full") if r == -2 else int(r) for r in res]
+
+    def bf_info(self, key) -> dict:
+        key = encode(key)
+        if not self.keys.expect(key, "bf"):
+            raise ResponseError("ERR not found")
+        info = BfInfo()
+        self.ctx.call("ske_bf_info", self.keys.fid[key], C.byref(info))
+        return {"Capacity": info.capacity, "Size": info.size_bytes,
+                "Number of filters": info.nfilters, "Number of items inserted": info.inserted,
+                "Expansion rate": None if info.nonscaling else info.expansion}
+
+    def bf_links(self, key) -> list[dict]:
+        """BF.DEBUG-like view: one dict per link (bloom_init geometry)."""
+        key = encode(key)
+        if not self.keys.expect(key, "bf"):
+            raise ResponseError("ERR not found")
+        f = self.keys.fid[key]
+        info = BfInfo()
+        self.ctx.call("ske_bf_info", f, C.byref(info))
+        out = []
+        for i in range(info.nfilters):
+            L = BfLink()
+            self.ctx.call("ske_bf_link_info", f, i, C.byref(L))
+            out.append(dict(entries=L.entries, bytes=L.bytes, bits=L.bits, size=L.size,
+                            error=L.error, bpe=L.bpe, hashes=L.hashes))
+        return out
+
+    def bf_link_bits(self, key, link: int) -> np.ndarray:
+        """Raw bit array of one link (BF.SCANDUMP data chunk layout)."""
+        key = encode(key)
+        if not self.keys.expect(key, "bf"):
+            raise ResponseError("ERR not found")
+        links = self.bf_links(key)
+        out = np.zeros(links[link]["bytes"], np.uint8)
+        self.ctx.call("ske_bf_export_link", self.keys.fid[key], link, _ptr(out), out.size)
+        return out
+
+    def bf(self) -> "BloomCommands":
+        return BloomCommands(self)
+
+    # ------------------------------------------------------------ HLL
+    def _hll_slots_for_add(self, keys: Sequence[bytes]):
+        """slot per key, creating missing keys; returns (slots, created_flags)."""
+        slots, created = [], []
+        for k in keys:
+            if self.keys.expect(k, "hll"):
+                slots.append(self.keys.slot[k])
+                created.append(False)
+            else:
+                slots.append(self.keys.new_slot(k))
+                created.append(True)
+        return slots, created
+
+    def pfadd_calls(self, calls: Sequence[tuple]) -> list[int]:
+        """Several PFADD calls executed as one device batch with Redis's
+        sequential replies: call c replies 1 if it created its key or any of
+        its elements raised a register given all elements before it."""
+        keys = [encode(c[0]) for c in calls]
+        for k in keys:  # type check before any side effect
+            self.keys.expect(k, "hll")
+        created = []
+        slots = []
+        seen_new = set()
+        for k in keys:
+            if k in self.keys.slot:
+                slots.append(self.keys.slot[k])
+                created.append(False)
+            else:
+                slots.append(self.keys.new_slot(k))
+                created.append(k not in seen_new)
+                seen_new.add(k)
+        elems, owner = [], []
+        for ci, c in enumerate(calls):
+            for v in c[1:]:
+                elems.append(v)
+                owner.append(ci)
+        replies = [1 if cr else 0 for cr in created]
+        if elems:
+            buf, offs = pack(elems)
+            slot_arr = np.asarray([slots[o] for o in owner], dtype=np.uint32)
+            changed = np.zeros(len(elems), np.uint8)
+            self.ctx.call("ske_hll_pfadd", _ptr(slot_arr), _ptr(buf), _ptr(offs), len(elems),
+                          _ptr(changed), SKE_MEM_HOST)
+            any_changed = np.zeros(len(calls), np.uint8)
+            np.maximum.at(any_changed, np.asarray(owner, dtype=np.int64), changed)
+            replies = [1 if (replies[i] or any_changed[i]) else 0 for i in range(len(calls))]
+        return replies
+
+    def pfadd(self, name, *values) -> int:
+        return self.pfadd_calls([(name, *values)])[0]
+
+    def pfadd_packed(self, slots: np.ndarray, buf: np.ndarray, offs: np.ndarray,
+                     changed: bool = False) -> np.ndarray | None:
+        """PFADD of (slot, element) pairs already resolved to slots."""
+        n = len(offs) - 1
+        slots = np.ascontiguousarray(slots, dtype=np.uint32)
+        out = np.zeros(n, np.uint8) if changed else None
+        if n:
+            self.ctx.call("ske_hll_pfadd", _ptr(slots), _ptr(buf), _ptr(offs), n, _ptr(out),
+                          SKE_MEM_HOST)
+        return out
+
+    def _count_slots(self, names) -> list[int]:
+        slots = []
+        for n in names:
+            k = encode(n)
+            if self.keys.expect(k, "hll"):
+                slots.append(self.keys.slot[k])
+        return slots
+
+    def pfcount(self, *sources) -> int:
+        if not sources:
+            raise ResponseError("ERR wrong number of arguments for 'pfcount' command")
+        slots = self._count_slots(sources)
+        if not slots:
+            return 0
+        arr = np.asarray(slots, dtype=np.uint32)
+        out = np.zeros(1, np.uint64)
+        self.ctx.call("ske_hll_pfcount", _ptr(arr), len(slots), _ptr(out))
+        return int(out[0])
+
+    def pfcount_each(self, keys: Sequence) -> np.ndarray:
+        """PFCOUNT of every key separately, one device launch (K2)."""
+        slots = []
+        present = []
+        for n in keys:
+            k = encode(n)
+            ok = self.keys.expect(k, "hll")
+            present.append(ok)
+            slots.append(self.keys.slot[k] if ok else 0)
+        out = np.zeros(len(slots), np.uint64)
+        idx = np.flatnonzero(present)
+        if idx.size:
+            arr = np.asarray([slots[i] for i in idx], dtype=np.uint32)
+            sub = np.zeros(idx.size, np.uint64)
+            self.ctx.call("ske_hll_pfcount_each", _ptr(arr), arr.size, _ptr(sub), SKE_MEM_HOST)
+            out[idx] = sub
+        return out
+
+    def pfcount_groups(self, groups: Sequence[Sequence]) -> np.ndarray:
+        """PFCOUNT(k1 k2 ...) for many key groups in one launch (unions)."""
+        slots, goffs = [], [0]
+        for g in groups:
+            slots.extend(self._count_slots(g))
+            goffs.append(len(slots))
+        out = np.zeros(len(groups), np.uint64)
+        if groups:
+            s = np.asarray(slots if slots else [0], dtype=np.uint32)
+            go = np.asarray(goffs, dtype=np.uint32)
+            self.ctx.call("ske_hll_pfcount_groups", _ptr(s), _ptr(go), len(groups), _ptr(out),
+                          SKE_MEM_HOST)
+        return out
+
+    def pfmerge(self, dest, *sources) -> bool:
+        d = encode(dest)
+        src = [encode(s) for s in sources]
+        for k in src:
+            self.keys.expect(k, "hll")
+        if not self.keys.expect(d, "hll"):
+            self.keys.new_slot(d)
+        slots = np.asarray([self.keys.slot[k] for k in src if k in self.keys.slot], dtype=np.uint32)
+        self.ctx.call("ske_hll_pfmerge", self.keys.slot[d], _ptr(slots), slots.size)
+        return True
+
+    def hll_registers(self, name) -> np.ndarray:
+        """Raw registers (Redis HLL_RAW view, one byte per register)."""
+        k = encode(name)
+        out = np.zeros(HLL_REGISTERS, np.uint8)
+        if self.keys.expect(k, "hll"):
+            self.ctx.call("ske_hll_export_raw", self.keys.slot[k], _ptr(out))
+        return out
+
+    def hll_dense(self, name) -> bytes:
+        """The 12288-byte HLL_DENSE register payload of the key."""
+        k = encode(name)
+        if not self.keys.expect(k, "hll"):
+            raise ResponseError("ERR no such key")
+        out = np.zeros(HLL_DENSE_BYTES, np.uint8)
+        self.ctx.call("ske_hll_export_dense", self.keys.slot[k], _ptr(out))
+        return out.tobytes()
+
+    def hll_load_registers(self, name, regs: np.ndarray) -> None:
+        k = encode(name)
+        if not self.keys.expect(k, "hll"):
+            self.keys.new_slot(k)
+        r = np.ascontiguousarray(regs, dtype=np.uint8)
+        if r.shape != (HLL_REGISTERS,):
+            raise DataError("expected 16384 registers")
+        self.ctx.call("ske_hll_import_raw", self.keys.slot[k], _ptr(r))
+
+    def key_slot(self, name, create: bool = True) -> int:
+        """Slot of an HLL key (creating it when asked) for batched calls."""
+        k = encode(name)
+        if self.keys.expect(k, "hll"):
+            return self.keys.slot[k]
+        if not create:
+            raise ResponseError("ERR no such key")
+        return self.keys.new_slot(k)
+
+    # ------------------------------------------------------------ fused hot path
+    def swipes(self, bf_key, hll_keys, items=None, *, packed=None) -> np.ndarray:
+        """Batched attendance_processor.py:109-129: for every event
+        ``valid = BF.EXISTS bf_key id``; if valid ``PFADD hll_key id``.
+
+        ``hll_keys``: one key for the whole batch or one key per item.
+        ``items``: ids (encoded as redis-py does) or ``packed=(buf, offs)``.
+        Returns the per-event validity (bool array).  HLL keys that receive
+        no valid event are not created, exactly as in the per-event loop."""
+        if packed is None:
+            buf, offs = pack(items)
+        else:
+            buf, offs = packed
+            buf = np.ascontiguousarray(buf, np.uint8)
+            offs = np.ascontiguousarray(offs, np.uint32)
+        n = len(offs) - 1
+        bkey = encode(bf_key)
+        has_bf = self.keys.expect(bkey, "bf")
+        if n == 0:
+            return np.zeros(0, bool)
+        if isinstance(hll_keys, (str, bytes, int, float)):
+            key_list = [encode(hll_keys)]
+            slot_idx = np.zeros(n, np.int64)
+        else:
+            hk = [encode(k) for k in hll_keys]
+            if len(hk) != n:
+                raise DataError("hll_keys must be one key or one key per item")
+            uniq = {}
+            slot_idx = np.fromiter((uniq.setdefault(k, len(uniq)) for k in hk), np.int64, count=n)
+            key_list = list(uniq)
+        for k in key_list:
+            self.keys.expect(k, "hll")
+        tentative = [k for k in key_list if k not in self.keys.slot]
+        key_slots = np.asarray([self.keys.slot[k] if k in self.keys.slot else self.keys.new_slot(k)
+                                for k in key_list], dtype=np.uint32)
+        slots = key_slots[slot_idx]
+        valid = np.zeros(n, np.uint8)
+        if has_bf:
+            self.ctx.call("ske_swipes", self.keys.fid[bkey], _ptr(slots), _ptr(buf), _ptr(offs), n,
+                          _ptr(valid), SKE_MEM_HOST)
+        if tentative:
+            hit = np.zeros(len(key_list), bool)
+            hit[np.unique(slot_idx[valid.astype(bool)])] = True
+            for k in tentative:
+                if not hit[key_list.index(k)]:
+                    self.keys.release_unused_slot(k)
+        return valid.astype(bool)
+
+    def swipes_slots(self, bf_key, slots: np.ndarray, buf: np.ndarray, offs: np.ndarray) -> np.ndarray:
+        """``swipes`` with keys already resolved to slots (see ``key_slot``)."""
+        n = len(offs) - 1
+        valid = np.zeros(n, np.uint8)
+        bkey = encode(bf_key)
+        if n and self.keys.expect(bkey, "bf"):
+            s = np.ascontiguousarray(slots, dtype=np.uint32)
+            self.ctx.call("ske_swipes", self.keys.fid[bkey], _ptr(s), _ptr(buf), _ptr(offs), n,
+                          _ptr(valid), SKE_MEM_HOST)
+        return valid.astype(bool)
+
+    # ------------------------------------------------------------ command dispatch
+    def execute_command(self, *args, **options):
+        if not args:
+            raise ResponseError("ERR empty command")
+        name = args[0].decode() if isinstance(args[0], bytes) else str(args[0])
+        cmd = name.upper()
+        a = args[1:]
+
+        def need(lo, hi=None):
+            if len(a) < lo or (hi is not None and len(a) > hi):
+                raise ResponseError(f"ERR wrong number of arguments for '{name.lower()}' command")
+
+        if cmd == "BF.RESERVE":
+            need(3)
+            exp, nonscaling = None, False
+            rest = list(a[3:])
+            while rest:
+                opt = rest.pop(0)
+                opt = (opt.decode() if isinstance(opt, bytes) else str(opt)).upper()
+                if opt == "EXPANSION" and rest:
+                    exp = rest.pop(0)
+                elif opt == "NONSCALING":
+                    nonscaling = True
+                else:
+                    raise ResponseError("ERR syntax error")
+            return self._bf_reserve(encode(a[0]), a[1], a[2], exp, nonscaling)
+        if cmd == "BF.ADD":
+            need(2, 2)
+            r = self._bf_madd_reply(encode(a[0]), [a[1]])[0]
+            if isinstance(r, ResponseError):
+                raise r
+            return r
+        if cmd == "BF.MADD":
+            need(2)
+            return self._bf_madd_reply(encode(a[0]), a[1:])
+        if cmd in ("BF.EXISTS", "BF.MEXISTS"):
+            need(2, 2 if cmd == "BF.EXISTS" else None)
+            buf, offs = pack(a[1:])
+            r = [int(x) for x in self.bf_mexists_packed(a[0], buf, offs)]
+            return r[0] if cmd == "BF.EXISTS" else r
+        if cmd == "BF.INFO":
+            need(1, 1)
+            info = self.bf_info(a[0])
+            flat = []
+            for k, v in info.items():
+                flat += [self._s(k), v]
+            return flat
+        if cmd == "BF.CARD":
+            need(1, 1)
+            k = encode(a[0])
+            return self.bf_info(k)["Number of items inserted"] if self.keys.expect(k, "bf") else 0
+        if cmd == "PFADD":
+            need(1)
+            return self.pfadd(*a)
+        if cmd == "PFCOUNT":
+            need(1)
+            return self.pfcount(*a)
+        if cmd == "PFMERGE":
+            need(1)
+            self.pfmerge(*a)
+            return self._ok()
+        if cmd in ("DEL", "UNLINK"):
+            need(1)
+            return self.delete(*a)
+        if cmd == "EXISTS":
+            need(1)
+            return self.exists(*a)
+        if cmd == "TYPE":
+            need(1, 1)
+            return self.type(a[0])
+        if cmd in ("FLUSHALL", "FLUSHDB"):
+            self.flushall()
+            return self._ok()
+        if cmd == "PING":
+            return self._s("PONG")
+        raise ResponseError(f"ERR unknown command '{name}'")
+
+    def pipeline(self, transaction: bool = True, shard_hint=None) -> "Pipeline":
+        return Pipeline(self)
+
+
+Redis = SketchClient  # redis.Redis(host=..., port=..., decode_responses=True) drop-in
+
+
+class BloomCommands:
+    """``client.bf()`` surface of redis-py (redis.commands.bf.BFCommands)."""
+
+    def __init__(self, client: SketchClient):
+        self.client = client
+
+    def create(self, key, errorRate, capacity, expansion=None, noScale=None):
+        self.client._bf_reserve(encode(key), errorRate, capacity, expansion, bool(noScale))
+        return True
+
+    reserve = create
+
+    def add(self, key, item):
+        return self.client.execute_command("BF.ADD", key, item)
+
+    def madd(self, key, *items):
+        return self.client.execute_command("BF.MADD", key, *items)
+
+    def exists(self, key, item):
+        return self.client.execute_command("BF.EXISTS", key, item)
+
+    def mexists(self, key, *items):
+        return self.client.execute_command("BF.MEXISTS", key, *items)
+
+    def info(self, key):
+        return BFInfo(self.client.bf_info(key))
+
+    def card(self, key):
+        return self.client.execute_command("BF.CARD", key)
+
+
+class BFInfo:
+    """redis.commands.bf.info.BFInfo attribute names."""
+
+    def __init__(self, d: dict):
+        self.capacity = d["Capacity"]
+        self.size = d["Size"]
+        self.filterNum = d["Number of filters"]
+        self.insertedNum = d["Number of items inserted"]
+        self.expansionRate = d["Expansion rate"]
+
+    def get(self, item):
+        return getattr(self, item)
+
+    def __getitem__(self, item):
+        return getattr(self, item)
+
+
+class Pipeline:
+    """redis-py pipeline: commands are queued and executed on ``execute()``.
+
+    Consecutive compatible commands run as ONE device batch with Redis's
+    sequential replies: a run of PFADDs (any keys) becomes one exact-order
+    ske_hll_pfadd; a run of BF.EXISTS/BF.MEXISTS on one key one
+    ske_bf_mexists; a run of BF.ADD/BF.MADD on one key one ske_bf_madd."""
+
+    def __init__(self, client: SketchClient):
+        self.client = client
+        self._cmds: list[tuple] = []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.reset()
+
+    def __len__(self):
+        return len(self._cmds)
+
+    def reset(self):
+        self._cmds = []
+
+    def execute_command(self, *args, **options):
+        self._cmds.append(args)
+        return self
+
+    def pfadd(self, name, *values):
+        return self.execute_command("PFADD", name, *values)
+
+    def pfcount(self, *sources):
+        return self.execute_command("PFCOUNT", *sources)
+
+    def pfmerge(self, dest, *sources):
+        return self.execute_command("PFMERGE", dest, *sources)
+
+    def bf(self):
+        p = self
+
+        class _B:
+            def add(self, key, item):
+                return p.execute_command("BF.ADD", key, item)
+
+            def madd(self, key, *items):
+                return p.execute_command("BF.MADD", key, *items)
+
+            def exists(self, key, item):
+                return p.execute_command("BF.EXISTS", key, item)
+
+            def mexists(self, key, *items):
+                return p.execute_command("BF.MEXISTS", key, *items)
+
+            def reserve(self, key, errorRate, capacity, expansion=None, noScale=None):
+                args = ["BF.RESERVE", key, errorRate, capacity]
+                if expansion is not None:
+                    args += ["EXPANSION", expansion]
+                if noScale:
+                    args += ["NONSCALING"]
+                return p.execute_command(*args)
+
+            create = reserve
+        return _B()
+
+    @staticmethod
+    def _name(c) -> str:
+        n = c[0]
+        return (n.decode() if isinstance(n, bytes) else str(n)).upper()
+
+    def execute(self, raise_on_error: bool = True) -> list:
+        cmds, self._cmds = self._cmds, []
+        out: list = []
+        i = 0
+        cl = self.client
+        while i < len(cmds):
+            name = self._name(cmds[i])
+            j = i + 1
+            try:
+                if name == "PFADD" and len(cmds[i]) >= 2:
+                    while j < len(cmds) and self._name(cmds[j]) == "PFADD" and len(cmds[j]) >= 2:
+                        j += 1
+                    out.extend(cl.pfadd_calls([c[1:] for c in cmds[i:j]]))
+                elif name in ("BF.EXISTS", "BF.MEXISTS") and len(cmds[i]) >= 3:
+                    key = encode(cmds[i][1])
+                    while (j < len(cmds) and self._name(cmds[j]) in ("BF.EXISTS", "BF.MEXISTS")
+                           and len(cmds[j]) >= 3 and encode(cmds[j][1]) == key):
+                        j += 1
+                    if any(self._name(c) == "BF.EXISTS" and len(c) != 3 for c in cmds[i:j]):
+                        raise ResponseError("ERR wrong number of arguments for 'bf.exists' command")
+                    items = [x for c in cmds[i:j] for x in c[2:]]
+                    buf, offs = pack(items)
+                    res = cl.bf_mexists_packed(key, buf, offs)
+                    p = 0
+                    for c in cmds[i:j]:
+                        m = len(c) - 2
+                        r = [int(x) for x in res[p:p + m]]
+                        out.append(r[0] if self._name(c) == "BF.EXISTS" else r)
+                        p += m
+                elif name in ("BF.ADD", "BF.MADD") and len(cmds[i]) >= 3:
+                    key = encode(cmds[i][1])
+                    while (j < len(cmds) and self._name(cmds[j]) in ("BF.ADD", "BF.MADD")
+                           and len(cmds[j]) >= 3 and encode(cmds[j][1]) == key):
+                        j += 1
+                    items = [x for c in cmds[i:j] for x in c[2:]]
+                    res = cl._bf_madd_reply(key, items)
+                    p = 0
+                    for c in cmds[i:j]:
+                        m = len(c) - 2
+                        out.append(res[p] if self._name(c) == "BF.ADD" else res[p:p + m])
+                        p += m
+                else:
+                    out.append(cl.execute_command(*cmds[i]))
+            except ResponseError as e:
+                out.extend([e] * (j - i))
+            i = j
+        if raise_on_error:
+            for r in out:
+                if isinstance(r, ResponseError):
+                    raise r
+        return out

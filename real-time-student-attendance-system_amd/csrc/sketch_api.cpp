@@ -1,0 +1,986 @@
+// sketch_api.cpp -- libsketch C-ABI (include/sketch.h): context, Bloom chains,
+// HLL register slab, host/device staging and the order-exact drivers.
+//
+// Host arithmetic here is the RedisBloom / Redis bookkeeping that is not
+// data-parallel: link geometry (deps/bloom/bloom.c bloom_init + calc_bpe),
+// chain growth (src/sb.c SBChain_Add), and the PFCOUNT estimator's
+// m*tau(.) / m*sigma(.) tables (src/hyperloglog.c hllTau / hllSigma) built
+// with the same libm calls as Redis.  Compiled with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/sketch.h"
+#include "sketch_common.h"
+#include "sketch_internal.h"
+
+namespace ske {
+Scratch *scratch_new();
+void scratch_delete(Scratch *s);
+hipError_t launch_bf_count_cands(uint64_t n, const uint8_t *state, unsigned long long *counter,
+                                 int cus, hipStream_t st);
+}  // namespace ske
+
+using namespace ske;
+
+namespace {
+
+struct Link {
+    uint8_t *bf = nullptr;  // device
+    uint64_t entries = 0, bytes = 0, bits = 0, size = 0;
+    double error = 0, bpe = 0;
+    int hashes = 0;
+    Divisor div{};
+};
+
+struct Filter {
+    bool exists = false;
+    std::vector<Link> links;
+    uint64_t size = 0;
+    uint32_t growth = 2;
+    bool nonscaling = false;
+};
+
+struct Staged {
+    const uint8_t *bytes = nullptr;
+    const uint32_t *offs = nullptr;
+};
+
+}  // namespace
+
+struct ske_ctx {
+    int device = 0;
+    int cus = 256;
+    hipStream_t own = nullptr;
+    hipStream_t st = nullptr;
+    std::vector<Filter> filters;
+    uint8_t *regs = nullptr;  // nslots * 16384
+    uint32_t nslots = 0;
+    double *tau = nullptr, *sig = nullptr;  // device estimator tables (lazy)
+    Scratch *scratch = nullptr;
+    // staging buffers (grow on demand)
+    void *stg[8] = {};
+    size_t stg_cap[8] = {};
+    unsigned int *err = nullptr;
+    unsigned long long *stats = nullptr;
+    int pb = 1;           // probe batch (1 = RedisBloom order)
+    int variant = -1;     // -1 auto, 0 global, 1 LDS
+    bool lds_ok = false;
+    std::string last_hip;
+};
+
+#define HIPCHK(ctx, expr)                                                                         \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess) {                                                                   \
+            (ctx)->last_hip = std::string(#expr) + ": " + hipGetErrorString(_e);                  \
+            return SKE_EHIP;                                                                      \
+        }                                                                                         \
+    } while (0)
+
+namespace {
+
+void *stage_buf(ske_ctx *c, int slot, size_t bytes, int *rc) {
+    if (bytes < 64) bytes = 64;
+    if (c->stg_cap[slot] < bytes) {
+        if (c->stg[slot]) (void)hipFree(c->stg[slot]);
+        c->stg[slot] = nullptr;
+        c->stg_cap[slot] = 0;
+        size_t want = bytes + bytes / 4 + 256;
+        hipError_t e = hipMalloc(&c->stg[slot], want);
+        if (e != hipSuccess) {
+            c->last_hip = std::string("hipMalloc(staging): ") + hipGetErrorString(e);
+            *rc = SKE_ENOMEM;
+            return nullptr;
+        }
+        c->stg_cap[slot] = want;
+    }
+    return c->stg[slot];
+}
+
+// Items to device.  SKE_MEM_DEVICE pointers are used in place; host items are
+// copied as the byte range [offs[0], offs[n]) plus offsets, and the device
+// bytes pointer is rebased so that offs[] index it unchanged.
+int stage_items(ske_ctx *c, const uint8_t *bytes, const uint32_t *offs, uint64_t n, int mem,
+                Staged *out, int slot_bytes = 0, int slot_offs = 1) {
+    if (mem == SKE_MEM_DEVICE) {
+        out->bytes = bytes;
+        out->offs = offs;
+        return SKE_OK;
+    }
+    if (!offs || (!bytes && offs[n] != offs[0])) return SKE_EINVAL;
+    for (uint64_t i = 0; i < n; i++)
+        if (offs[i + 1] < offs[i]) return SKE_EINVAL;
+    const uint64_t b0 = offs[0], total = uint64_t(offs[n]) - b0;
+    int rc = SKE_OK;
+    uint8_t *db = (uint8_t *)stage_buf(c, slot_bytes, total + 16, &rc);
+    uint32_t *dof = (uint32_t *)stage_buf(c, slot_offs, (n + 1) * 4, &rc);
+    if (rc) return rc;
+    if (total) HIPCHK(c, hipMemcpyAsync(db, bytes + b0, total, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, hipMemcpyAsync(dof, offs, (n + 1) * 4, hipMemcpyHostToDevice, c->st));
+    out->bytes = db - b0;
+    out->offs = dof;
+    return SKE_OK;
+}
+
+int stage_u32(ske_ctx *c, const uint32_t *p, uint64_t n, int mem, int slot, const uint32_t **out) {
+    if (mem == SKE_MEM_DEVICE || n == 0) {
+        *out = p;
+        return SKE_OK;
+    }
+    int rc = SKE_OK;
+    uint32_t *d = (uint32_t *)stage_buf(c, slot, n * 4, &rc);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(d, p, n * 4, hipMemcpyHostToDevice, c->st));
+    *out = d;
+    return SKE_OK;
+}
+
+// deps/bloom/bloom.c calc_bpe() + bloom_init() with BLOOM_OPT_NOROUND |
+// BLOOM_OPT_FORCE64, the options rebloom.c's bfCreateChain() passes.
+int link_geometry(uint64_t entries, double error, Link *L) {
+    if (entries < 1 || !(error > 0) || error >= 1.0) return SKE_EINVAL;
+    const double denom = 0.480453013918201;  // ln(2)^2
+    double bpe = -(log(error) / denom);
+    if (bpe < 0) bpe = -bpe;
+    uint64_t bits = (uint64_t)((double)entries * bpe);
+    if (bits == 0) bits = 1;
+    uint64_t bytes = (bits % 64) ? ((bits / 64) + 1) * 8 : bits / 8;
+    L->entries = entries;
+    L->error = error;
+    L->bpe = bpe;
+    L->bytes = bytes;
+    L->bits = bytes * 8;
+    L->hashes = (int)ceil(0.693147180559945 * bpe);
+    L->size = 0;
+    if (L->bits >= (uint64_t(1) << 62)) return SKE_ENOMEM;
+    L->div = make_divisor(L->bits);
+    return SKE_OK;
+}
+
+int add_link(ske_ctx *c, Filter &F, uint64_t entries, double error) {
+    if ((int)F.links.size() >= SKE_MAX_LINKS) return SKE_ENOMEM;
+    Link L;
+    int rc = link_geometry(entries, error, &L);
+    if (rc) return rc;
+    // pad to 16 bytes so 4-byte atomics and 16-byte staging never leave it
+    hipError_t e = hipMalloc(&L.bf, (L.bytes + 15) & ~uint64_t(15));
+    if (e != hipSuccess) {
+        c->last_hip = std::string("hipMalloc(bloom link): ") + hipGetErrorString(e);
+        return SKE_ENOMEM;
+    }
+    e = hipMemsetAsync(L.bf, 0, (L.bytes + 15) & ~uint64_t(15), c->st);
+    if (e != hipSuccess) {
+        (void)hipFree(L.bf);
+        c->last_hip = std::string("hipMemset(bloom link): ") + hipGetErrorString(e);
+        return SKE_EHIP;
+    }
+    F.links.push_back(L);
+    return SKE_OK;
+}
+
+void free_filter(Filter &F) {
+    for (auto &L : F.links)
+        if (L.bf) (void)hipFree(L.bf);
+    F = Filter();
+}
+
+ChainDev chain_dev(const Filter &F, size_t first = 0, size_t count = SIZE_MAX) {
+    ChainDev ch{};
+    ch.nlinks = 0;
+    uint32_t lds = 0;
+    const size_t end = std::min(F.links.size(), first + std::min(count, F.links.size()));
+    for (size_t i = first; i < end; i++) {
+        const Link &L = F.links[i];
+        LinkDev &D = ch.link[ch.nlinks++];
+        D.bf = L.bf;
+        D.div = L.div;
+        D.k = uint32_t(L.hashes);
+        D.lds_off = lds;
+        const uint64_t padded = (L.bytes + 15) & ~uint64_t(15);
+        lds = (lds + padded > 0xffffffffu) ? 0xffffffffu : uint32_t(lds + padded);
+    }
+    ch.lds_bytes = lds;
+    return ch;
+}
+
+LinkDev link_dev(const Link &L) {
+    LinkDev D{};
+    D.bf = L.bf;
+    D.div = L.div;
+    D.k = uint32_t(L.hashes);
+    D.lds_off = 0;
+    return D;
+}
+
+bool use_lds(const ske_ctx *c, const ChainDev &ch) {
+    if (!c->lds_ok || ch.nlinks == 0) return false;
+    if (c->variant == 0) return false;
+    return ch.lds_bytes <= lds_bloom_max();
+}
+
+Filter *get_filter(ske_ctx *c, uint32_t fid) {
+    if (fid >= c->filters.size()) return nullptr;
+    return &c->filters[fid];
+}
+
+// hllTau / hllSigma exactly as Redis src/hyperloglog.c (glibc sqrt, pow).
+double redis_sigma(double x) {
+    if (x == 1.) return INFINITY;
+    double zPrime, y = 1, z = x;
+    do {
+        x *= x;
+        zPrime = z;
+        z += x * y;
+        y += y;
+    } while (zPrime != z);
+    return z;
+}
+double redis_tau(double x) {
+    if (x == 0. || x == 1.) return 0.;
+    double zPrime, y = 1.0, z = 1 - x;
+    do {
+        x = sqrt(x);
+        zPrime = z;
+        y *= 0.5;
+        z -= pow(1 - x, 2) * y;
+    } while (zPrime != z);
+    return z / 3;
+}
+
+int ensure_tables(ske_ctx *c) {
+    if (c->tau) return SKE_OK;
+    const int M = SKE_HLL_REGISTERS;
+    std::vector<double> tau(M + 1), sig(M + 1);
+    const double m = M;
+    for (int j = 0; j <= M; j++) {
+        tau[j] = m * redis_tau((m - j) / (double)m);  // z = m * hllTau((m-H[Q+1])/m)
+        sig[j] = m * redis_sigma(j / (double)m);      // z += m * hllSigma(H[0]/m)
+    }
+    HIPCHK(c, hipMalloc(&c->tau, (M + 1) * sizeof(double)));
+    HIPCHK(c, hipMalloc(&c->sig, (M + 1) * sizeof(double)));
+    HIPCHK(c, hipMemcpy(c->tau, tau.data(), (M + 1) * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->sig, sig.data(), (M + 1) * sizeof(double), hipMemcpyHostToDevice));
+    return SKE_OK;
+}
+
+int check_err_flag(ske_ctx *c, int code_if_set) {
+    unsigned int h = 0;
+    HIPCHK(c, hipMemcpyAsync(&h, c->err, 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return h ? code_if_set : SKE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *ske_strerror(int code) {
+    switch (code) {
+    case SKE_OK: return "OK";
+    case SKE_EINVAL: return "ERR invalid argument";
+    case SKE_ENOMEM: return "ERR out of device memory";
+    case SKE_EHIP: return "ERR HIP runtime error";
+    case SKE_ENOFILTER: return "ERR not found";
+    case SKE_EEXISTS: return "ERR item exists";
+    case SKE_EFULL: return "ERR non scaling filter is full";
+    case SKE_ERANGE: return "ERR HLL slot out of range";
+    case SKE_EBADRATE: return "ERR (0 < error rate range < 1)";
+    case SKE_EBADCAP: return "ERR (capacity should be larger than 0)";
+    case SKE_EBADEXP: return "ERR expansion should be greater or equal to 1";
+    case SKE_EBADHLL: return "INVALIDOBJ Corrupted HLL object detected";
+    case SKE_ETOOLONG: return "ERR item too long";
+    default: return "ERR unknown";
+    }
+}
+
+const char *ske_last_hip_error(ske_ctx *c) { return c ? c->last_hip.c_str() : ""; }
+
+int ske_open(int device, ske_ctx **out) {
+    if (!out) return SKE_EINVAL;
+    *out = nullptr;
+    ske_ctx *c = new ske_ctx();
+    c->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        delete c;
+        return SKE_EHIP;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        c->cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return SKE_EHIP;
+    }
+    c->st = c->own;
+    c->filters.resize(SKE_MAX_FILTERS);
+    c->scratch = scratch_new();
+    if (hipMalloc(&c->err, 64) != hipSuccess || hipMalloc(&c->stats, 64) != hipSuccess) {
+        ske_close(c);
+        return SKE_ENOMEM;
+    }
+    c->lds_ok = lds_bloom_setup() == hipSuccess;
+    *out = c;
+    return SKE_OK;
+}
+
+int ske_close(ske_ctx *c) {
+    if (!c) return SKE_EINVAL;
+    (void)hipSetDevice(c->device);
+    if (c->st) (void)hipStreamSynchronize(c->st);
+    for (auto &F : c->filters) free_filter(F);
+    if (c->regs) (void)hipFree(c->regs);
+    if (c->tau) (void)hipFree(c->tau);
+    if (c->sig) (void)hipFree(c->sig);
+    for (int i = 0; i < 8; i++)
+        if (c->stg[i]) (void)hipFree(c->stg[i]);
+    if (c->err) (void)hipFree(c->err);
+    if (c->stats) (void)hipFree(c->stats);
+    if (c->scratch) scratch_delete(c->scratch);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+    return SKE_OK;
+}
+
+int ske_set_stream(ske_ctx *c, void *stream) {
+    if (!c) return SKE_EINVAL;
+    c->st = stream ? (hipStream_t)stream : c->own;
+    return SKE_OK;
+}
+
+int ske_sync(ske_ctx *c) {
+    if (!c) return SKE_EINVAL;
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+int ske_device_alloc(ske_ctx *c, uint64_t bytes, void **out) {
+    if (!c || !out) return SKE_EINVAL;
+    hipError_t e = hipMalloc(out, bytes ? bytes : 16);
+    if (e != hipSuccess) {
+        c->last_hip = std::string("hipMalloc: ") + hipGetErrorString(e);
+        return SKE_ENOMEM;
+    }
+    return SKE_OK;
+}
+
+int ske_device_free(ske_ctx *c, void *p) {
+    if (!c) return SKE_EINVAL;
+    HIPCHK(c, hipFree(p));
+    return SKE_OK;
+}
+
+int ske_memcpy(ske_ctx *c, void *dst, const void *src, uint64_t bytes, int kind) {
+    if (!c) return SKE_EINVAL;
+    if (!bytes) return SKE_OK;
+    hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice
+                      : kind == 1 ? hipMemcpyDeviceToHost
+                                  : hipMemcpyDeviceToDevice;
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, k, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
+    if (!c || !name) return SKE_EINVAL;
+    if (!strcmp(name, "probe_batch")) {
+        if (value != 1 && value != 2 && value != 4) return SKE_EINVAL;
+        c->pb = int(value);
+        return SKE_OK;
+    }
+    if (!strcmp(name, "variant")) {
+        if (value < -1 || value > 1) return SKE_EINVAL;
+        c->variant = int(value);
+        return SKE_OK;
+    }
+    return SKE_EINVAL;
+}
+
+// ------------------------------------------------------------------ Bloom
+int ske_bf_reserve(ske_ctx *c, uint32_t fid, double error_rate, uint64_t capacity,
+                   uint32_t expansion, int nonscaling) {
+    if (!c) return SKE_EINVAL;
+    Filter *F = get_filter(c, fid);
+    if (!F) return SKE_EINVAL;
+    if (!(error_rate > 0) || error_rate >= 1) return SKE_EBADRATE;
+    if (capacity == 0) return SKE_EBADCAP;
+    if (expansion < 1 && !nonscaling) return SKE_EBADEXP;
+    if (F->exists) return SKE_EEXISTS;
+    Filter nf;
+    nf.growth = expansion;
+    nf.nonscaling = nonscaling != 0;
+    // SB_NewChain(): first link error * ERROR_TIGHTENING_RATIO unless NONSCALING
+    const double tightening = nf.nonscaling ? 1.0 : 0.5;
+    int rc = add_link(c, nf, capacity, error_rate * tightening);
+    if (rc) {
+        free_filter(nf);
+        return rc;
+    }
+    nf.exists = true;
+    *F = nf;
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+int ske_bf_exists_key(ske_ctx *c, uint32_t fid) {
+    Filter *F = c ? get_filter(c, fid) : nullptr;
+    return (F && F->exists) ? 1 : 0;
+}
+
+int ske_bf_free(ske_ctx *c, uint32_t fid) {
+    Filter *F = c ? get_filter(c, fid) : nullptr;
+    if (!F) return SKE_EINVAL;
+    (void)hipStreamSynchronize(c->st);
+    free_filter(*F);
+    return SKE_OK;
+}
+
+int ske_bf_info(ske_ctx *c, uint32_t fid, ske_bf_info_t *out) {
+    Filter *F = c ? get_filter(c, fid) : nullptr;
+    if (!F || !out) return SKE_EINVAL;
+    if (!F->exists) return SKE_ENOFILTER;
+    memset(out, 0, sizeof(*out));
+    // SBChain_MemUsage(): sizeof(SBChain) + nfilters*sizeof(SBLink) + bytes
+    uint64_t mem = 32 + 64 * F->links.size();
+    for (auto &L : F->links) {
+        out->capacity += L.entries;
+        mem += L.bytes;
+    }
+    out->size_bytes = mem;
+    out->nfilters = uint32_t(F->links.size());
+    out->expansion = F->growth;
+    out->inserted = F->size;
+    out->nonscaling = F->nonscaling;
+    return SKE_OK;
+}
+
+int ske_bf_link_info(ske_ctx *c, uint32_t fid, uint32_t link, ske_bf_link_t *out) {
+    Filter *F = c ? get_filter(c, fid) : nullptr;
+    if (!F || !out) return SKE_EINVAL;
+    if (!F->exists) return SKE_ENOFILTER;
+    if (link >= F->links.size()) return SKE_EINVAL;
+    const Link &L = F->links[link];
+    memset(out, 0, sizeof(*out));
+    out->entries = L.entries;
+    out->bytes = L.bytes;
+    out->bits = L.bits;
+    out->size = L.size;
+    out->error = L.error;
+    out->bpe = L.bpe;
+    out->hashes = L.hashes;
+    return SKE_OK;
+}
+
+int ske_bf_export_link(ske_ctx *c, uint32_t fid, uint32_t link, uint8_t *out, uint64_t cap) {
+    Filter *F = c ? get_filter(c, fid) : nullptr;
+    if (!F || !out) return SKE_EINVAL;
+    if (!F->exists) return SKE_ENOFILTER;
+    if (link >= F->links.size()) return SKE_EINVAL;
+    const Link &L = F->links[link];
+    if (cap < L.bytes) return SKE_EINVAL;
+    HIPCHK(c, hipMemcpyAsync(out, L.bf, L.bytes, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+int ske_bf_import_link(ske_ctx *c, uint32_t fid, uint32_t link, const uint8_t *in,
+                       uint64_t nbytes) {
+    Filter *F = c ? get_filter(c, fid) : nullptr;
+    if (!F || !in) return SKE_EINVAL;
+    if (!F->exists) return SKE_ENOFILTER;
+    if (link >= F->links.size() || nbytes != F->links[link].bytes) return SKE_EINVAL;
+    HIPCHK(c, hipMemcpyAsync(F->links[link].bf, in, nbytes, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+int ske_bf_mexists(ske_ctx *c, uint32_t fid, const uint8_t *bytes, const uint32_t *offs,
+                   uint64_t n, uint8_t *out, int mem) {
+    if (!c || !out) return SKE_EINVAL;
+    Filter *F = get_filter(c, fid);
+    if (!F) return SKE_EINVAL;
+    if (n == 0) return SKE_OK;
+    if (!F->exists) {  // BFCheck on a missing key answers 0
+        if (mem == SKE_MEM_DEVICE) {
+            HIPCHK(c, hipMemsetAsync(out, 0, n, c->st));
+            HIPCHK(c, hipStreamSynchronize(c->st));
+        } else {
+            memset(out, 0, n);
+        }
+        return SKE_OK;
+    }
+    Staged s;
+    int rc = stage_items(c, bytes, offs, n, mem, &s);
+    if (rc) return rc;
+    uint8_t *dout = out;
+    if (mem != SKE_MEM_DEVICE) {
+        dout = (uint8_t *)stage_buf(c, 3, n, &rc);
+        if (rc) return rc;
+    }
+    const ChainDev ch = chain_dev(*F);
+    HIPCHK(c, launch_swipes(1, ch, use_lds(c, ch), c->pb, s.bytes, s.offs, nullptr, n, nullptr, 0,
+                            dout, nullptr, c->cus, c->st));
+    if (mem != SKE_MEM_DEVICE) HIPCHK(c, hipMemcpyAsync(out, dout, n, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+// BF.MADD with SBChain_Add's sequential semantics, in epochs: an epoch fills
+// the current link up to its remaining capacity with the candidates in
+// order ("first setter" per bit decides who is still absent when its turn
+// comes), then the chain grows and the rest continue in the new link.
+int ske_bf_madd(ske_ctx *c, uint32_t fid, const uint8_t *bytes, const uint32_t *offs, uint64_t n,
+                int8_t *out, int mem) {
+    if (!c) return SKE_EINVAL;
+    Filter *F = get_filter(c, fid);
+    if (!F) return SKE_EINVAL;
+    if (n == 0) return SKE_OK;
+    if (n >= 0xffffffffull) return SKE_EINVAL;
+    if (!F->exists) {  // rebloom.c BF.ADD / BF.MADD auto-create: 0.01, 100, expansion 2
+        int rc = ske_bf_reserve(c, fid, 0.01, 100, 2, 0);
+        if (rc) return rc;
+    }
+    Staged s;
+    int rc = stage_items(c, bytes, offs, n, mem, &s);
+    if (rc) return rc;
+    hipError_t e = hipSuccess;
+    uint64_t *ha = (uint64_t *)scratch_get(c->scratch, 10, n * 8, &e);
+    uint64_t *hb = (uint64_t *)scratch_get(c->scratch, 11, n * 8, &e);
+    uint8_t *state = (uint8_t *)scratch_get(c->scratch, 12, n, &e);
+    int8_t *res = (int8_t *)scratch_get(c->scratch, 13, n, &e);
+    uint32_t *absent = (uint32_t *)scratch_get(c->scratch, 14, n * 4, &e);
+    uint32_t *pos = (uint32_t *)scratch_get(c->scratch, 15, n * 4, &e);
+    if (e != hipSuccess) {
+        c->last_hip = hipGetErrorString(e);
+        return SKE_ENOMEM;
+    }
+    HIPCHK(c, hipMemsetAsync(state, 0, n, c->st));
+    HIPCHK(c, launch_bf_hash(s.bytes, s.offs, n, ha, hb, c->cus, c->st));
+    HIPCHK(c, launch_bf_settle_present(chain_dev(*F), n, ha, hb, state, res, c->cus, c->st));
+    for (int epoch = 0; epoch < 4 * SKE_MAX_LINKS + 4; epoch++) {
+        Link *L = &F->links.back();
+        uint64_t cap = L->size >= L->entries ? 0 : L->entries - L->size;
+        if (cap == 0) {
+            HIPCHK(c, hipMemsetAsync(c->stats, 0, 8, c->st));
+            HIPCHK(c, launch_bf_count_cands(n, state, c->stats, c->cus, c->st));
+            unsigned long long remaining = 0;
+            HIPCHK(c, hipMemcpyAsync(&remaining, c->stats, 8, hipMemcpyDeviceToHost, c->st));
+            HIPCHK(c, hipStreamSynchronize(c->st));
+            if (remaining == 0) break;
+            if (F->nonscaling) {
+                HIPCHK(c, launch_bf_fill_rest(n, state, res, -2, c->cus, c->st));
+                break;
+            }
+            // SBChain_Add(): next link entries * growth, error * 0.5
+            rc = add_link(c, *F, L->entries * (uint64_t)F->growth, L->error * 0.5);
+            if (rc) return rc;
+            L = &F->links.back();
+            cap = L->entries;
+        }
+        if (L->bits > 0xffffffffull * 4ull) return SKE_ENOMEM;
+        uint32_t *first = (uint32_t *)scratch_get(c->scratch, 0, L->bits * 4, &e);
+        if (e != hipSuccess) {
+            c->last_hip = hipGetErrorString(e);
+            return SKE_ENOMEM;
+        }
+        HIPCHK(c, hipMemsetAsync(first, 0xff, L->bits * 4, c->st));
+        const LinkDev D = link_dev(*L);
+        HIPCHK(c, launch_bf_first_setter(D, n, ha, hb, state, first, c->cus, c->st));
+        HIPCHK(c, launch_bf_absent(D, n, ha, hb, state, first, absent, c->cus, c->st));
+        HIPCHK(c, scan_inclusive_u32(c->scratch, absent, pos, n, c->st));
+        uint32_t total_absent = 0;
+        HIPCHK(c, hipMemcpyAsync(&total_absent, pos + (n - 1), 4, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(c, hipStreamSynchronize(c->st));
+        const uint32_t cap32 = cap > 0xffffffffull ? 0xffffffffu : uint32_t(cap);
+        HIPCHK(c, launch_bf_resolve(D, n, ha, hb, state, absent, pos, cap32, res, L->bf, c->cus,
+                                    c->st));
+        const uint64_t added = std::min<uint64_t>(cap, total_absent);
+        L->size += added;
+        F->size += added;
+        if (total_absent < cap) break;  // every candidate resolved
+        // the rest see this link as left by the resolved adds
+        ChainDev one{};
+        one.nlinks = 1;
+        one.link[0] = D;
+        HIPCHK(c, launch_bf_settle_present(one, n, ha, hb, state, res, c->cus, c->st));
+    }
+    if (out) {
+        if (mem == SKE_MEM_DEVICE)
+            HIPCHK(c, hipMemcpyAsync(out, res, n, hipMemcpyDeviceToDevice, c->st));
+        else
+            HIPCHK(c, hipMemcpyAsync(out, res, n, hipMemcpyDeviceToHost, c->st));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+// ------------------------------------------------------------------ HLL
+int ske_hll_reserve(ske_ctx *c, uint32_t nslots) {
+    if (!c) return SKE_EINVAL;
+    if (nslots <= c->nslots) return SKE_OK;
+    uint64_t want = std::max<uint64_t>(nslots, uint64_t(c->nslots) * 3 / 2);
+    want = std::max<uint64_t>(want, 16);
+    uint8_t *nr = nullptr;
+    hipError_t e = hipMalloc(&nr, want * SKE_HLL_REGISTERS);
+    if (e != hipSuccess) {
+        c->last_hip = std::string("hipMalloc(hll slab): ") + hipGetErrorString(e);
+        return SKE_ENOMEM;
+    }
+    HIPCHK(c, hipMemsetAsync(nr, 0, want * SKE_HLL_REGISTERS, c->st));
+    if (c->regs) {
+        HIPCHK(c, hipMemcpyAsync(nr, c->regs, uint64_t(c->nslots) * SKE_HLL_REGISTERS,
+                                 hipMemcpyDeviceToDevice, c->st));
+        HIPCHK(c, hipStreamSynchronize(c->st));
+        (void)hipFree(c->regs);
+    }
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    c->regs = nr;
+    c->nslots = uint32_t(want);
+    return SKE_OK;
+}
+
+uint32_t ske_hll_capacity(ske_ctx *c) { return c ? c->nslots : 0; }
+
+int ske_hll_clear(ske_ctx *c, uint32_t slot) {
+    if (!c) return SKE_EINVAL;
+    if (slot >= c->nslots) return SKE_ERANGE;
+    HIPCHK(c, hipMemsetAsync(c->regs + uint64_t(slot) * SKE_HLL_REGISTERS, 0, SKE_HLL_REGISTERS,
+                             c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+int ske_hll_pfadd(ske_ctx *c, const uint32_t *slot, const uint8_t *bytes, const uint32_t *offs,
+                  uint64_t n, uint8_t *changed, int mem) {
+    if (!c || !slot) return SKE_EINVAL;
+    if (n == 0) return SKE_OK;
+    if (n >= 0xffffffffull) return SKE_EINVAL;
+    Staged s;
+    int rc = stage_items(c, bytes, offs, n, mem, &s);
+    if (rc) return rc;
+    const uint32_t *dslot;
+    rc = stage_u32(c, slot, n, mem, 2, &dslot);
+    if (rc) return rc;
+    HIPCHK(c, hipMemsetAsync(c->err, 0, 4, c->st));
+    if (changed) {
+        uint8_t *dch = changed;
+        if (mem != SKE_MEM_DEVICE) {
+            dch = (uint8_t *)stage_buf(c, 3, n, &rc);
+            if (rc) return rc;
+        }
+        HIPCHK(c, pfadd_exact(c->scratch, dslot, s.bytes, s.offs, n, c->regs, c->nslots, dch,
+                              c->err, c->cus, c->st));
+        if (mem != SKE_MEM_DEVICE)
+            HIPCHK(c, hipMemcpyAsync(changed, dch, n, hipMemcpyDeviceToHost, c->st));
+    } else {
+        HIPCHK(c, launch_pfadd(dslot, s.bytes, s.offs, n, c->regs, c->nslots, c->err, c->cus,
+                               c->st));
+    }
+    return check_err_flag(c, SKE_ERANGE);
+}
+
+int ske_swipes(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *bytes,
+               const uint32_t *offs, uint64_t n, uint8_t *out_valid, int mem) {
+    if (!c || !slot) return SKE_EINVAL;
+    Filter *F = get_filter(c, fid);
+    if (!F) return SKE_EINVAL;
+    if (n == 0) return SKE_OK;
+    Staged s;
+    int rc = stage_items(c, bytes, offs, n, mem, &s);
+    if (rc) return rc;
+    const uint32_t *dslot;
+    rc = stage_u32(c, slot, n, mem, 2, &dslot);
+    if (rc) return rc;
+    uint8_t *dout = out_valid;
+    if (out_valid && mem != SKE_MEM_DEVICE) {
+        dout = (uint8_t *)stage_buf(c, 3, n, &rc);
+        if (rc) return rc;
+    }
+    HIPCHK(c, hipMemsetAsync(c->err, 0, 4, c->st));
+    const ChainDev ch = F->exists ? chain_dev(*F) : ChainDev{};
+    HIPCHK(c, launch_swipes(0, ch, use_lds(c, ch), c->pb, s.bytes, s.offs, dslot, n, c->regs,
+                            c->nslots, dout, (unsigned long long *)c->err, c->cus, c->st));
+    if (out_valid && mem != SKE_MEM_DEVICE)
+        HIPCHK(c, hipMemcpyAsync(out_valid, dout, n, hipMemcpyDeviceToHost, c->st));
+    return check_err_flag(c, SKE_ERANGE);
+}
+
+int ske_swipes_async(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *bytes,
+                     const uint32_t *offs, uint64_t n, uint8_t *out_valid) {
+    if (!c || !slot) return SKE_EINVAL;
+    Filter *F = get_filter(c, fid);
+    if (!F) return SKE_EINVAL;
+    const ChainDev ch = F->exists ? chain_dev(*F) : ChainDev{};
+    HIPCHK(c, launch_swipes(0, ch, use_lds(c, ch), c->pb, bytes, offs, slot, n, c->regs,
+                            c->nslots, out_valid, (unsigned long long *)c->err, c->cus, c->st));
+    return SKE_OK;
+}
+
+int ske_swipes_stats(ske_ctx *c, uint32_t fid, const uint8_t *bytes, const uint32_t *offs,
+                     uint64_t n, uint64_t *probes, uint64_t *nvalid) {
+    if (!c || !probes || !nvalid) return SKE_EINVAL;
+    Filter *F = get_filter(c, fid);
+    if (!F) return SKE_EINVAL;
+    const ChainDev ch = F->exists ? chain_dev(*F) : ChainDev{};
+    HIPCHK(c, hipMemsetAsync(c->stats, 0, 16, c->st));
+    // PB = 1: count RedisBloom's exact sequential probes
+    HIPCHK(c, launch_swipes(2, ch, use_lds(c, ch), 1, bytes, offs, nullptr, n, nullptr, 0, nullptr,
+                            c->stats, c->cus, c->st));
+    unsigned long long h[2] = {0, 0};
+    HIPCHK(c, hipMemcpyAsync(h, c->stats, 16, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    *probes = h[0];
+    *nvalid = h[1];
+    return SKE_OK;
+}
+
+int ske_swipes_variant(ske_ctx *c, uint32_t fid) {
+    Filter *F = c ? get_filter(c, fid) : nullptr;
+    if (!F) return SKE_EINVAL;
+    const ChainDev ch = F->exists ? chain_dev(*F) : ChainDev{};
+    return use_lds(c, ch) ? 1 : 0;
+}
+
+static int pfcount_impl(ske_ctx *c, const uint8_t *regs, const uint32_t *slots,
+                        const uint32_t *goffs, uint32_t ngroups, uint64_t *out, int mem) {
+    int rc = ensure_tables(c);
+    if (rc) return rc;
+    uint64_t *dout = out;
+    if (mem != SKE_MEM_DEVICE) {
+        dout = (uint64_t *)stage_buf(c, 5, uint64_t(ngroups) * 8, &rc);
+        if (rc) return rc;
+    }
+    HIPCHK(c, launch_pfcount(regs, slots, goffs, ngroups, c->tau, c->sig, dout, c->cus, c->st));
+    if (mem != SKE_MEM_DEVICE)
+        HIPCHK(c, hipMemcpyAsync(out, dout, uint64_t(ngroups) * 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+static int check_slots_host(ske_ctx *c, const uint32_t *slots, uint64_t n) {
+    for (uint64_t i = 0; i < n; i++)
+        if (slots[i] >= c->nslots) return SKE_ERANGE;
+    return SKE_OK;
+}
+
+int ske_hll_pfcount(ske_ctx *c, const uint32_t *slots, uint32_t nkeys, uint64_t *out) {
+    if (!c || !slots || !out || nkeys == 0) return SKE_EINVAL;
+    int rc = check_slots_host(c, slots, nkeys);
+    if (rc) return rc;
+    const uint32_t *ds;
+    rc = stage_u32(c, slots, nkeys, SKE_MEM_HOST, 6, &ds);
+    if (rc) return rc;
+    const uint32_t go[2] = {0, nkeys};
+    const uint32_t *dg;
+    rc = stage_u32(c, go, 2, SKE_MEM_HOST, 7, &dg);
+    if (rc) return rc;
+    return pfcount_impl(c, c->regs, ds, dg, 1, out, SKE_MEM_HOST);
+}
+
+int ske_hll_pfcount_each(ske_ctx *c, const uint32_t *slots, uint32_t nkeys, uint64_t *out,
+                         int mem) {
+    if (!c || !out) return SKE_EINVAL;
+    if (nkeys == 0) return SKE_OK;
+    if (mem != SKE_MEM_DEVICE) {
+        int rc = check_slots_host(c, slots, nkeys);
+        if (rc) return rc;
+    }
+    const uint32_t *ds = nullptr;
+    if (slots) {
+        int rc = stage_u32(c, slots, nkeys, mem, 6, &ds);
+        if (rc) return rc;
+    } else if (nkeys > c->nslots) {
+        return SKE_ERANGE;
+    }
+    return pfcount_impl(c, c->regs, ds, nullptr, nkeys, out, mem);
+}
+
+int ske_hll_pfcount_groups(ske_ctx *c, const uint32_t *slots, const uint32_t *goffs,
+                           uint32_t ngroups, uint64_t *out, int mem) {
+    if (!c || !slots || !goffs || !out) return SKE_EINVAL;
+    if (ngroups == 0) return SKE_OK;
+    int rc;
+    if (mem != SKE_MEM_DEVICE) {
+        for (uint32_t g = 0; g < ngroups; g++)
+            if (goffs[g + 1] < goffs[g]) return SKE_EINVAL;
+        rc = check_slots_host(c, slots + goffs[0], goffs[ngroups] - goffs[0]);
+        if (rc) return rc;
+    }
+    const uint32_t *ds, *dg;
+    const uint64_t nslots_total = mem == SKE_MEM_DEVICE ? 0 : goffs[ngroups];
+    if (mem == SKE_MEM_DEVICE) {
+        ds = slots;
+        dg = goffs;
+    } else {
+        rc = stage_u32(c, slots, nslots_total, mem, 6, &ds);
+        if (rc) return rc;
+        rc = stage_u32(c, goffs, uint64_t(ngroups) + 1, mem, 7, &dg);
+        if (rc) return rc;
+    }
+    return pfcount_impl(c, c->regs, ds, dg, ngroups, out, mem);
+}
+
+int ske_hll_merge_groups_dev(ske_ctx *c, const uint32_t *slots, const uint32_t *goffs,
+                             uint32_t ngroups, uint8_t *dst_dev) {
+    if (!c || !goffs || !dst_dev) return SKE_EINVAL;
+    if (ngroups == 0) return SKE_OK;
+    for (uint32_t g = 0; g < ngroups; g++)
+        if (goffs[g + 1] < goffs[g]) return SKE_EINVAL;
+    const uint64_t total = goffs[ngroups];
+    if (total && !slots) return SKE_EINVAL;
+    int rc = check_slots_host(c, slots, total);
+    if (rc) return rc;
+    const uint32_t *ds, *dg;
+    rc = stage_u32(c, slots, total, SKE_MEM_HOST, 6, &ds);
+    if (rc) return rc;
+    rc = stage_u32(c, goffs, uint64_t(ngroups) + 1, SKE_MEM_HOST, 7, &dg);
+    if (rc) return rc;
+    HIPCHK(c, launch_merge_groups(c->regs, ds, dg, ngroups, dst_dev, c->cus, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+int ske_hll_count_raw_dev(ske_ctx *c, const uint8_t *regs_dev, uint32_t nkeys, uint64_t *out) {
+    if (!c || !regs_dev || !out) return SKE_EINVAL;
+    if (nkeys == 0) return SKE_OK;
+    return pfcount_impl(c, regs_dev, nullptr, nullptr, nkeys, out, SKE_MEM_HOST);
+}
+
+int ske_hll_pfmerge(ske_ctx *c, uint32_t dst, const uint32_t *srcs, uint32_t n) {
+    if (!c || (n && !srcs)) return SKE_EINVAL;
+    if (dst >= c->nslots) return SKE_ERANGE;
+    int rc = check_slots_host(c, srcs, n);
+    if (rc) return rc;
+    if (n == 0) return SKE_OK;
+    const uint32_t *ds;
+    rc = stage_u32(c, srcs, n, SKE_MEM_HOST, 6, &ds);
+    if (rc) return rc;
+    HIPCHK(c, launch_pfmerge(c->regs, dst, ds, n, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+int ske_hll_histogram(ske_ctx *c, uint32_t slot, uint32_t *out64) {
+    if (!c || !out64) return SKE_EINVAL;
+    if (slot >= c->nslots) return SKE_ERANGE;
+    int rc = SKE_OK;
+    uint32_t *d = (uint32_t *)stage_buf(c, 5, 256, &rc);
+    if (rc) return rc;
+    HIPCHK(c, launch_histogram(c->regs + uint64_t(slot) * SKE_HLL_REGISTERS, d, c->st));
+    HIPCHK(c, hipMemcpyAsync(out64, d, 256, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+int ske_hll_export_raw(ske_ctx *c, uint32_t slot, uint8_t *out) {
+    if (!c || !out) return SKE_EINVAL;
+    if (slot >= c->nslots) return SKE_ERANGE;
+    HIPCHK(c, hipMemcpyAsync(out, c->regs + uint64_t(slot) * SKE_HLL_REGISTERS, SKE_HLL_REGISTERS,
+                             hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+int ske_hll_export_dense(ske_ctx *c, uint32_t slot, uint8_t *out) {
+    if (!c || !out) return SKE_EINVAL;
+    if (slot >= c->nslots) return SKE_ERANGE;
+    int rc = SKE_OK;
+    uint8_t *d = (uint8_t *)stage_buf(c, 5, SKE_HLL_DENSE_BYTES, &rc);
+    if (rc) return rc;
+    HIPCHK(c, launch_dense(c->regs + uint64_t(slot) * SKE_HLL_REGISTERS, d, c->st));
+    HIPCHK(c, hipMemcpyAsync(out, d, SKE_HLL_DENSE_BYTES, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+int ske_hll_import_raw(ske_ctx *c, uint32_t slot, const uint8_t *in) {
+    if (!c || !in) return SKE_EINVAL;
+    if (slot >= c->nslots) return SKE_ERANGE;
+    for (int i = 0; i < SKE_HLL_REGISTERS; i++)
+        if (in[i] > 51) return SKE_EBADHLL;  // no register can exceed Q+1
+    HIPCHK(c, hipMemcpyAsync(c->regs + uint64_t(slot) * SKE_HLL_REGISTERS, in, SKE_HLL_REGISTERS,
+                             hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+int ske_hll_slab(ske_ctx *c, void **p, uint64_t *bytes) {
+    if (!c || !p || !bytes) return SKE_EINVAL;
+    *p = c->regs;
+    *bytes = uint64_t(c->nslots) * SKE_HLL_REGISTERS;
+    return SKE_OK;
+}
+
+// ------------------------------------------------------------------ generator
+int ske_gen_id_width(const ske_gen_params_t *p) {
+    if (!p || p->id_hi <= p->id_lo) return SKE_EINVAL;
+    uint64_t x = p->id_hi - 1;
+    int w = 1;
+    while (x >= 10) {
+        x /= 10;
+        w++;
+    }
+    return w;
+}
+
+static int gen_dev(const ske_gen_params_t *p, GenDev *g) {
+    const int w = ske_gen_id_width(p);
+    if (w < 1 || w > 19) return SKE_EINVAL;
+    uint64_t p10 = 1;
+    for (int i = 0; i < 20; i++) {
+        g->pow10[i] = p10;
+        if (i < 19) p10 *= 10;
+    }
+    if (p->id_lo < g->pow10[w - 1]) return SKE_EINVAL;  // all IDs share the digit count
+    const uint64_t R = p->id_hi - p->id_lo;
+    if (R >= (uint64_t(1) << 32) || p->n_members == 0 || p->n_members > R) return SKE_EINVAL;
+    if (p->perm_mul % R == 0 || (unsigned __int128)(p->perm_mul % R) * (p->perm_mul_inv % R) % R != 1 % R)
+        return SKE_EINVAL;
+    if (p->n_keys == 0) return SKE_EINVAL;
+    g->seed = p->seed;
+    g->lo = p->id_lo;
+    g->R = R;
+    g->N = p->n_members;
+    g->mul = p->perm_mul % R;
+    g->add = p->perm_add % R;
+    g->inv = p->perm_mul_inv % R;
+    g->inv_thr = p->invalid_thresh;
+    g->near_thr = p->near_thresh;
+    g->n_keys = p->n_keys;
+    g->slot_base = p->slot_base;
+    g->width = uint32_t(w);
+    g->key_cdf = p->key_cdf;
+    return SKE_OK;
+}
+
+int ske_gen_members(ske_ctx *c, const ske_gen_params_t *p, uint64_t start, uint64_t n,
+                    uint8_t *bytes_dev, uint32_t *offs_dev) {
+    if (!c || !p || !bytes_dev || !offs_dev) return SKE_EINVAL;
+    GenDev g{};
+    int rc = gen_dev(p, &g);
+    if (rc) return rc;
+    if (start + n > g.N || n * g.width >= 0xffffffffull) return SKE_EINVAL;
+    HIPCHK(c, launch_gen_members(g, start, n, bytes_dev, offs_dev, c->cus, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+int ske_gen_swipes(ske_ctx *c, const ske_gen_params_t *p, uint64_t start, uint64_t n,
+                   uint8_t *bytes_dev, uint32_t *offs_dev, uint32_t *slot_dev) {
+    if (!c || !p || !bytes_dev || !offs_dev || !slot_dev) return SKE_EINVAL;
+    GenDev g{};
+    int rc = gen_dev(p, &g);
+    if (rc) return rc;
+    if (n * g.width >= 0xffffffffull) return SKE_EINVAL;
+    HIPCHK(c, launch_gen_swipes(g, start, n, bytes_dev, offs_dev, slot_dev, c->cus, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+}  // extern "C"

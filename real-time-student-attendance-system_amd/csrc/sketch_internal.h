@@ -1,0 +1,64 @@
+// sketch_internal.h -- launcher declarations shared by the libsketch TUs.
+#pragma once
+#include "sketch_common.h"
+
+namespace ske {
+
+// sketch_kernels.hip
+hipError_t launch_swipes(int mode, const ChainDev &ch, bool lds, int pb, const uint8_t *bytes,
+                         const uint32_t *offs, const uint32_t *slot, uint64_t n, uint8_t *regs,
+                         uint32_t nslots, uint8_t *out, unsigned long long *stats, int cus,
+                         hipStream_t st);
+hipError_t lds_bloom_setup();
+uint32_t lds_bloom_max();
+hipError_t launch_pfadd(const uint32_t *slot, const uint8_t *bytes, const uint32_t *offs,
+                        uint64_t n, uint8_t *regs, uint32_t nslots, unsigned int *err, int cus,
+                        hipStream_t st);
+hipError_t launch_pfcount(const uint8_t *regs, const uint32_t *slots, const uint32_t *goffs,
+                          uint32_t ngroups, const double *tau, const double *sig, uint64_t *out,
+                          int cus, hipStream_t st);
+hipError_t launch_histogram(const uint8_t *regs, uint32_t *out64, hipStream_t st);
+hipError_t launch_pfmerge(uint8_t *regs, uint32_t dst, const uint32_t *srcs, uint32_t n,
+                          hipStream_t st);
+hipError_t launch_merge_groups(const uint8_t *regs, const uint32_t *slots, const uint32_t *goffs,
+                               uint32_t ngroups, uint8_t *dst, int cus, hipStream_t st);
+hipError_t launch_dense(const uint8_t *regs, uint8_t *dense, hipStream_t st);
+hipError_t launch_gen_swipes(const GenDev &g, uint64_t start, uint64_t n, uint8_t *bytes,
+                             uint32_t *offs, uint32_t *slot, int cus, hipStream_t st);
+hipError_t launch_gen_members(const GenDev &g, uint64_t start, uint64_t n, uint8_t *bytes,
+                              uint32_t *offs, int cus, hipStream_t st);
+
+// sketch_order.hip -- order-exact paths (replies that depend on item order)
+struct Scratch;  // growable device scratch, owned by the context
+void *scratch_get(Scratch *s, int slot, size_t bytes, hipError_t *err);
+
+// PFADD with per-element "changed" flags in sequential order.
+hipError_t pfadd_exact(Scratch *s, const uint32_t *slot, const uint8_t *bytes,
+                       const uint32_t *offs, uint64_t n, uint8_t *regs, uint32_t nslots,
+                       uint8_t *changed_dev, unsigned int *err_dev, int cus, hipStream_t st);
+
+// BF.MADD helpers (the epoch driver lives in the API TU, which owns links)
+hipError_t launch_bf_hash(const uint8_t *bytes, const uint32_t *offs, uint64_t n, uint64_t *ha,
+                          uint64_t *hb, int cus, hipStream_t st);
+// items with state==0 that are present in any of ch's links: state=1, res=0
+hipError_t launch_bf_settle_present(const ChainDev &ch, uint64_t n, const uint64_t *ha,
+                                    const uint64_t *hb, uint8_t *state, int8_t *res, int cus,
+                                    hipStream_t st);
+hipError_t launch_bf_first_setter(const LinkDev &L, uint64_t n, const uint64_t *ha,
+                                  const uint64_t *hb, const uint8_t *state, uint32_t *first,
+                                  int cus, hipStream_t st);
+hipError_t launch_bf_absent(const LinkDev &L, uint64_t n, const uint64_t *ha, const uint64_t *hb,
+                            const uint8_t *state, const uint32_t *first, uint32_t *absent,
+                            int cus, hipStream_t st);
+hipError_t scan_inclusive_u32(Scratch *s, const uint32_t *in, uint32_t *out, uint64_t n,
+                              hipStream_t st);
+// resolve candidates with index <= cutoff; absent ones are added (bits set)
+hipError_t launch_bf_resolve(const LinkDev &L, uint64_t n, const uint64_t *ha, const uint64_t *hb,
+                             uint8_t *state, const uint32_t *absent, const uint32_t *pos,
+                             uint32_t cap, int8_t *res, uint8_t *bf_mut, int cus,
+                             hipStream_t st);
+// mark every remaining candidate with a result code (non-scaling full)
+hipError_t launch_bf_fill_rest(uint64_t n, uint8_t *state, int8_t *res, int8_t code, int cus,
+                               hipStream_t st);
+
+}  // namespace ske

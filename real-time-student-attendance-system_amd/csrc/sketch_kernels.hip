@@ -1,0 +1,488 @@
+// sketch_kernels.hip -- gfx950 kernels of the validate-and-count hot path.
+//
+//  K1  k_swipes      fused BF.EXISTS (SBChain_Check newest->oldest) + valid-gated
+//                    PFADD (hllPatLen + register max) per swipe
+//                    (attendance_processor.py:109-113 + :127-129)
+//  K1e k_swipes<Exists>   BF.MEXISTS only (attendance_processor.py:109, :78)
+//  K1s k_swipes<Stats>    probe statistics for the roofline (untimed)
+//      k_pfadd       PFADD of (slot, element) pairs without reply flags
+//  K2  k_pfcount     per-group register max-merge + 64-bin histogram + Ertl
+//                    estimator (hllCount) on device (attendance_processor.py:152)
+//  K3  k_pfmerge     PFMERGE register max
+//      k_dense       HLL_DENSE_SET_REGISTER packing for export
+//      k_gen_*       counter-based synthetic stream (DESIGN.md "Synthetic workload")
+//
+// Data layout in HBM: Bloom links are RedisBloom's own LSB-first bit arrays
+// (bit x at byte x>>3, mask 1<<(x&7)); HLL keys are 16384-byte slabs, one
+// byte per register (Redis HLL_RAW view), key s at regs + s*16384.
+#include "sketch_common.h"
+#include "sketch_internal.h"
+
+namespace ske {
+
+// Byte max into a register slab.  There is no byte atomic max, so the byte's
+// aligned 32-bit word is updated with a CAS loop; the loop starts from a
+// plain load, which may be stale but never too high (registers only grow).
+__device__ __forceinline__ bool reg_max(uint8_t *reg, uint32_t rank) {
+    uintptr_t a = reinterpret_cast<uintptr_t>(reg);
+    uint32_t *w = reinterpret_cast<uint32_t *>(a & ~uintptr_t(3));
+    const uint32_t sh = uint32_t(a & 3) * 8;
+    uint32_t old = *w;
+    bool changed = false;
+    while (((old >> sh) & 0xffu) < rank) {
+        uint32_t nw = (old & ~(0xffu << sh)) | (rank << sh);
+        uint32_t prev = atomicCAS(w, old, nw);
+        if (prev == old) {
+            changed = true;
+            break;
+        }
+        old = prev;
+    }
+    return changed;
+}
+
+enum SwipeMode { kModeSwipes = 0, kModeExists = 1, kModeStats = 2 };
+
+// Membership of one item in one link: k probes of the sequence
+// x_i = (a + i*b) mod 2^64 mod bits, PB probe loads in flight per batch,
+// early exit between batches (PB = 1 is RedisBloom's exact probe order).
+template <bool kLds, int PB>
+__device__ __forceinline__ bool link_check(const LinkDev &L, const uint8_t *lds, uint64_t ha,
+                                           uint64_t hb, uint32_t &probes) {
+    ProbeCursor c;
+    c.init(ha, hb, L.div);
+    const uint32_t k = L.k;
+    for (uint32_t j0 = 0; j0 < k; j0 += PB) {
+        uint8_t byte[PB];
+        uint32_t bit[PB];
+#pragma unroll
+        for (int u = 0; u < PB; u++) {
+            if (j0 + u < k) {
+                const uint64_t x = c.x;
+                bit[u] = uint32_t(x & 7);
+                byte[u] = kLds ? lds[L.lds_off + uint32_t(x >> 3)] : L.bf[x >> 3];
+                c.step(L.div);
+            } else {
+                bit[u] = 0;
+                byte[u] = 1;
+            }
+        }
+        bool all = true;
+#pragma unroll
+        for (int u = 0; u < PB; u++) {
+            if (j0 + u < k) {
+                probes++;
+                if (!((byte[u] >> bit[u]) & 1)) {
+                    all = false;
+                    break;
+                }
+            }
+        }
+        if (!all) return false;
+    }
+    return true;
+}
+
+template <bool kLds, int PB>
+__device__ __forceinline__ bool chain_check(const ChainDev &ch, const uint8_t *lds, uint64_t ha,
+                                            uint64_t hb, uint32_t &probes) {
+    for (int l = ch.nlinks - 1; l >= 0; --l)
+        if (link_check<kLds, PB>(ch.link[l], lds, ha, hb, probes)) return true;
+    return false;
+}
+
+constexpr int kLdsBloomMax = 152 * 1024;  // LDS image budget (160 KiB per CU)
+
+template <int kMode, bool kLds, int PB>
+__global__ void __launch_bounds__(kLds ? 1024 : 256)
+    k_swipes(const ChainDev ch, const uint8_t *__restrict__ bytes,
+             const uint32_t *__restrict__ offs, const uint32_t *__restrict__ slot, uint64_t n,
+             uint8_t *__restrict__ regs, uint32_t nslots, uint8_t *__restrict__ out,
+             unsigned long long *__restrict__ stats) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_img[];
+    if constexpr (kLds) {
+        // stage every link's bit array into LDS (8-byte granules: link bytes
+        // are multiples of 8 by bloom_init's rounding)
+        for (int l = 0; l < ch.nlinks; l++) {
+            const LinkDev &L = ch.link[l];
+            const uint64_t *src = reinterpret_cast<const uint64_t *>(L.bf);
+            uint64_t *dst = reinterpret_cast<uint64_t *>(lds_img + L.lds_off);
+            const uint32_t nw = uint32_t(L.div.d >> 6);
+            for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) dst[w] = src[w];
+        }
+        __syncthreads();
+    }
+    uint32_t probes = 0, nvalid = 0;
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t b = offs[i], e = offs[i + 1];
+        const Item it = load_item(bytes, b, e);
+        const uint64_t ha = murmur_item(it, kBloomSeed);
+        const uint64_t hb = murmur_item(it, ha);
+        const bool valid = chain_check<kLds, PB>(ch, lds_img, ha, hb, probes);
+        if constexpr (kMode == kModeSwipes) {
+            if (valid) {
+                const uint32_t s = slot[i];
+                if (s < nslots) {
+                    uint32_t idx, rank;
+                    hll_patlen(murmur_item(it, kHllSeed), idx, rank);
+                    reg_max(regs + size_t(s) * kHllRegs + idx, rank);
+                } else {
+                    atomicOr(reinterpret_cast<unsigned int *>(stats), 1u);
+                }
+            }
+            if (out) out[i] = valid;
+        } else if constexpr (kMode == kModeExists) {
+            out[i] = valid;
+        } else {
+            nvalid += valid;
+        }
+    }
+    if constexpr (kMode == kModeStats) {
+        atomicAdd(&stats[0], (unsigned long long)probes);
+        atomicAdd(&stats[1], (unsigned long long)nvalid);
+    }
+}
+
+__global__ void __launch_bounds__(256)
+    k_pfadd(const uint32_t *__restrict__ slot, const uint8_t *__restrict__ bytes,
+            const uint32_t *__restrict__ offs, uint64_t n, uint8_t *__restrict__ regs,
+            uint32_t nslots, unsigned int *__restrict__ err) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t s = slot[i];
+        if (s >= nslots) {
+            atomicOr(err, 1u);
+            continue;
+        }
+        const Item it = load_item(bytes, offs[i], offs[i + 1]);
+        uint32_t idx, rank;
+        hll_patlen(murmur_item(it, kHllSeed), idx, rank);
+        reg_max(regs + size_t(s) * kHllRegs + idx, rank);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K2: PFCOUNT.  One 256-thread block per group; each thread owns 4 x 16-byte
+// chunks (64 registers), max-merges them across the group's keys, and bins
+// them into a per-wave LDS histogram.  Thread 0 then runs hllCount()'s
+// estimator with the Redis operation order; m*tau(.) and m*sigma(.) come from
+// host tables built with the same libm calls as Redis (tau_tab[H51],
+// sig_tab[H0]) so only IEEE add / mul / div (correctly rounded) run here.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint4 max_u8x16(uint4 a, uint4 b) {
+    uint32_t av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int s = 0; s < 32; s += 8) {
+            uint32_t x = (av[q] >> s) & 0xff, y = (bv[q] >> s) & 0xff;
+            r |= (x > y ? x : y) << s;
+        }
+        av[q] = r;
+    }
+    return make_uint4(av[0], av[1], av[2], av[3]);
+}
+
+__device__ __forceinline__ uint64_t hll_estimate_dev(const uint32_t *h, const double *tau_tab,
+                                                     const double *sig_tab) {
+    double z = tau_tab[h[kHllQ + 1]];
+    for (int j = kHllQ; j >= 1; --j) {
+        z = __dadd_rn(z, double(h[j]));
+        z = __dmul_rn(z, 0.5);
+    }
+    z = __dadd_rn(z, sig_tab[h[0]]);
+    // HLL_ALPHA_INF * m * m, exact (m = 2^14)
+    const double num = 0.721347520444481703680 * 16384.0 * 16384.0;
+    const double q = num / z;
+    // Redis: E = llroundl(q); return (uint64_t)E.  When q is +inf (every
+    // register 51) or >= 2^63, x86-64 llroundl yields LLONG_MIN and the
+    // double -> uint64 conversion of -2^63 gives 2^63; reproduce that.
+    if (!(q < 9223372036854775808.0)) return uint64_t(1) << 63;
+    return uint64_t(double(llround(q)));
+}
+
+__global__ void __launch_bounds__(256)
+    k_pfcount(const uint8_t *__restrict__ regs, const uint32_t *__restrict__ slots,
+              const uint32_t *__restrict__ goffs, uint32_t ngroups,
+              const double *__restrict__ tau_tab, const double *__restrict__ sig_tab,
+              uint64_t *__restrict__ out) {
+    __shared__ uint32_t hist[4][64];
+    const int tid = threadIdx.x, wave = tid >> 6;
+    for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+        for (int q = tid; q < 4 * 64; q += 256) (&hist[0][0])[q] = 0;
+        __syncthreads();
+        const uint32_t s0 = goffs ? goffs[g] : g, s1 = goffs ? goffs[g + 1] : g + 1;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t chunk = c * 256 + tid;  // 1024 chunks of 16 B
+            uint4 v = make_uint4(0, 0, 0, 0);
+            for (uint32_t s = s0; s < s1; s++) {
+                const uint32_t key = slots ? slots[s] : s;
+                const uint4 r = reinterpret_cast<const uint4 *>(regs + size_t(key) * kHllRegs)[chunk];
+                v = (s == s0) ? r : max_u8x16(v, r);
+            }
+            const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+#pragma unroll
+                for (int sft = 0; sft < 32; sft += 8) atomicAdd(&hist[wave][(vv[q] >> sft) & 63], 1u);
+        }
+        __syncthreads();
+        if (tid < 64) hist[0][tid] += hist[1][tid] + hist[2][tid] + hist[3][tid];
+        __syncthreads();
+        if (tid == 0) out[g] = (s1 > s0) ? hll_estimate_dev(hist[0], tau_tab, sig_tab) : 0;
+        __syncthreads();
+    }
+}
+
+// Register histogram of one key (for the oracle cross-check of K2's bins).
+__global__ void __launch_bounds__(256)
+    k_histogram(const uint8_t *__restrict__ regs, uint32_t *__restrict__ out64) {
+    __shared__ uint32_t hist[64];
+    if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < kHllRegs; r += blockDim.x) atomicAdd(&hist[regs[r] & 63], 1u);
+    __syncthreads();
+    if (threadIdx.x < 64) out64[threadIdx.x] = hist[threadIdx.x];
+}
+
+// K3: PFMERGE dst = max(dst, srcs...)
+__global__ void __launch_bounds__(256)
+    k_pfmerge(uint8_t *__restrict__ regs, uint32_t dst, const uint32_t *__restrict__ srcs,
+              uint32_t n) {
+    const uint32_t chunk = blockIdx.x * blockDim.x + threadIdx.x;
+    if (chunk >= kHllRegs / 16) return;
+    uint4 *d = reinterpret_cast<uint4 *>(regs + size_t(dst) * kHllRegs) + chunk;
+    uint4 v = *d;
+    for (uint32_t s = 0; s < n; s++)
+        v = max_u8x16(v, reinterpret_cast<const uint4 *>(regs + size_t(srcs[s]) * kHllRegs)[chunk]);
+    *d = v;
+}
+
+// K3 into an external buffer: dst[g] = max over the group's slots
+__global__ void __launch_bounds__(256)
+    k_merge_groups(const uint8_t *__restrict__ regs, const uint32_t *__restrict__ slots,
+                   const uint32_t *__restrict__ goffs, uint32_t ngroups, uint8_t *__restrict__ dst) {
+    const uint32_t chunk = threadIdx.x + (blockIdx.x & 3) * 256;  // 1024 x 16 B per key
+    for (uint32_t g = blockIdx.x >> 2; g < ngroups; g += gridDim.x >> 2) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        for (uint32_t s = goffs[g]; s < goffs[g + 1]; s++)
+            v = max_u8x16(v, reinterpret_cast<const uint4 *>(regs + size_t(slots[s]) * kHllRegs)[chunk]);
+        reinterpret_cast<uint4 *>(dst + size_t(g) * kHllRegs)[chunk] = v;
+    }
+}
+
+hipError_t launch_merge_groups(const uint8_t *regs, const uint32_t *slots, const uint32_t *goffs,
+                               uint32_t ngroups, uint8_t *dst, int cus, hipStream_t st) {
+    if (ngroups == 0) return hipSuccess;
+    const unsigned g = ngroups < unsigned(cus) * 4 ? ngroups : unsigned(cus) * 4;
+    hipLaunchKernelGGL(k_merge_groups, dim3(g * 4), dim3(256), 0, st, regs, slots, goffs, ngroups, dst);
+    return hipGetLastError();
+}
+
+// HLL_DENSE_SET_REGISTER packing: registers 4j..4j+3 -> bytes 3j..3j+2
+__global__ void __launch_bounds__(256)
+    k_dense(const uint8_t *__restrict__ regs, uint8_t *__restrict__ dense) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= kHllRegs / 4) return;
+    const uint32_t w = reinterpret_cast<const uint32_t *>(regs)[j];
+    const uint32_t r0 = w & 63, r1 = (w >> 8) & 63, r2 = (w >> 16) & 63, r3 = (w >> 24) & 63;
+    const uint32_t bits = r0 | (r1 << 6) | (r2 << 12) | (r3 << 18);
+    dense[3 * j + 0] = uint8_t(bits);
+    dense[3 * j + 1] = uint8_t(bits >> 8);
+    dense[3 * j + 2] = uint8_t(bits >> 16);
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic stream
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void write_decimal(uint8_t *dst, uint64_t x, uint32_t width) {
+    for (int d = int(width) - 1; d >= 0; --d) {
+        dst[d] = uint8_t('0' + x % 10);
+        x /= 10;
+    }
+}
+
+__device__ uint64_t gen_swipe_id(const GenDev &g, uint64_t i) {
+    const uint64_t u0 = mix(g.seed, i, 0);
+    if (uint32_t(u0 >> 32) >= g.inv_thr) return gen_member(g, mix(g.seed, i, 1) % g.N);
+    if (g.near_thr && uint32_t(mix(g.seed, i, 1) >> 32) < g.near_thr) {
+        const uint64_t base = gen_member(g, mix(g.seed, i, 2) % g.N);
+        const uint64_t u = mix(g.seed, i, 3);
+        int64_t cand;
+        if ((u & 1) == 0) {
+            cand = ((u >> 1) & 1) ? int64_t(base) + 1 : int64_t(base) - 1;
+        } else {
+            const uint32_t pos = uint32_t((u >> 8) % g.width);
+            const int64_t p10 = int64_t(g.pow10[pos]);
+            const int64_t dold = int64_t(base / uint64_t(p10)) % 10;
+            const int64_t dnew = (dold + 1 + int64_t((u >> 16) % 9)) % 10;
+            cand = int64_t(base) + (dnew - dold) * p10;
+        }
+        if (cand >= int64_t(g.lo) && cand < int64_t(g.lo + g.R) && !gen_is_member(g, uint64_t(cand)))
+            return uint64_t(cand);
+    }
+    uint64_t x = 0;
+    for (uint32_t t = 0; t < 64; t++) {
+        x = g.lo + mix(g.seed, i, 4 + t) % g.R;
+        if (!gen_is_member(g, x)) break;
+    }
+    return x;
+}
+
+__global__ void __launch_bounds__(256)
+    k_gen_swipes(const GenDev g, uint64_t start, uint64_t n, uint8_t *__restrict__ bytes,
+                 uint32_t *__restrict__ offs, uint32_t *__restrict__ slot) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < n; t += stride) {
+        const uint64_t i = start + t;
+        write_decimal(bytes + t * g.width, gen_swipe_id(g, i), g.width);
+        offs[t] = uint32_t(t * g.width);
+        if (t == n - 1) offs[n] = uint32_t(n * g.width);
+        uint32_t s;
+        if (g.key_cdf) {
+            const uint32_t u = uint32_t(mix(g.seed, i, 200) >> 32);
+            uint32_t lo = 0, hi = g.n_keys - 1;  // first j with cdf[j] > u; last key absorbs
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (g.key_cdf[mid] > u) hi = mid; else lo = mid + 1;
+            }
+            s = lo;
+        } else {
+            s = uint32_t(mix(g.seed, i, 200) % g.n_keys);
+        }
+        slot[t] = g.slot_base + s;
+    }
+}
+
+__global__ void __launch_bounds__(256)
+    k_gen_members(const GenDev g, uint64_t start, uint64_t n, uint8_t *__restrict__ bytes,
+                  uint32_t *__restrict__ offs) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < n; t += stride) {
+        write_decimal(bytes + t * g.width, gen_member(g, start + t), g.width);
+        offs[t] = uint32_t(t * g.width);
+        if (t == n - 1) offs[n] = uint32_t(n * g.width);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
+    uint64_t g = (n + block - 1) / block;
+    if (g < 1) g = 1;
+    return unsigned(g < cap ? g : cap);
+}
+
+template <int kMode, int PB>
+static hipError_t launch_swipes_pb(const ChainDev &ch, bool lds, const uint8_t *bytes,
+                                   const uint32_t *offs, const uint32_t *slot, uint64_t n,
+                                   uint8_t *regs, uint32_t nslots, uint8_t *out,
+                                   unsigned long long *stats, int cus, hipStream_t st) {
+    if (lds) {
+        const unsigned grid = grid_for(n, 1024, unsigned(cus));
+        hipLaunchKernelGGL((k_swipes<kMode, true, PB>), dim3(grid), dim3(1024), ch.lds_bytes, st, ch,
+                           bytes, offs, slot, n, regs, nslots, out, stats);
+    } else {
+        const unsigned grid = grid_for(n, 256, unsigned(cus) * 16);
+        hipLaunchKernelGGL((k_swipes<kMode, false, PB>), dim3(grid), dim3(256), 0, st, ch, bytes,
+                           offs, slot, n, regs, nslots, out, stats);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_swipes(int mode, const ChainDev &ch, bool lds, int pb, const uint8_t *bytes,
+                         const uint32_t *offs, const uint32_t *slot, uint64_t n, uint8_t *regs,
+                         uint32_t nslots, uint8_t *out, unsigned long long *stats, int cus,
+                         hipStream_t st) {
+    if (n == 0) return hipSuccess;
+#define SKE_PB(P)                                                                                  \
+    if (mode == kModeSwipes)                                                                       \
+        return launch_swipes_pb<kModeSwipes, P>(ch, lds, bytes, offs, slot, n, regs, nslots, out,  \
+                                                stats, cus, st);                                   \
+    if (mode == kModeExists)                                                                       \
+        return launch_swipes_pb<kModeExists, P>(ch, lds, bytes, offs, slot, n, regs, nslots, out,  \
+                                                stats, cus, st);                                   \
+    return launch_swipes_pb<kModeStats, P>(ch, lds, bytes, offs, slot, n, regs, nslots, out,       \
+                                           stats, cus, st);
+    if (pb >= 4) {
+        SKE_PB(4)
+    } else if (pb >= 2) {
+        SKE_PB(2)
+    } else {
+        SKE_PB(1)
+    }
+#undef SKE_PB
+}
+
+hipError_t lds_bloom_setup() {
+    // allow the LDS-staged variant to declare up to kLdsBloomMax bytes
+    hipError_t e = hipSuccess;
+#define SKE_ATTR(M, P)                                                                             \
+    e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_swipes<M, true, P>),                 \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBloomMax);             \
+    if (e != hipSuccess) return e;
+    SKE_ATTR(kModeSwipes, 1) SKE_ATTR(kModeSwipes, 2) SKE_ATTR(kModeSwipes, 4)
+    SKE_ATTR(kModeExists, 1) SKE_ATTR(kModeExists, 2) SKE_ATTR(kModeExists, 4)
+    SKE_ATTR(kModeStats, 1) SKE_ATTR(kModeStats, 2) SKE_ATTR(kModeStats, 4)
+#undef SKE_ATTR
+    return e;
+}
+
+uint32_t lds_bloom_max() { return kLdsBloomMax; }
+
+hipError_t launch_pfadd(const uint32_t *slot, const uint8_t *bytes, const uint32_t *offs,
+                        uint64_t n, uint8_t *regs, uint32_t nslots, unsigned int *err, int cus,
+                        hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pfadd, dim3(grid_for(n, 256, cus * 16)), dim3(256), 0, st, slot, bytes,
+                       offs, n, regs, nslots, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_pfcount(const uint8_t *regs, const uint32_t *slots, const uint32_t *goffs,
+                          uint32_t ngroups, const double *tau, const double *sig, uint64_t *out,
+                          int cus, hipStream_t st) {
+    if (ngroups == 0) return hipSuccess;
+    const unsigned grid = ngroups < unsigned(cus) * 8 ? ngroups : unsigned(cus) * 8;
+    hipLaunchKernelGGL(k_pfcount, dim3(grid), dim3(256), 0, st, regs, slots, goffs, ngroups, tau,
+                       sig, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_histogram(const uint8_t *regs, uint32_t *out64, hipStream_t st) {
+    hipLaunchKernelGGL(k_histogram, dim3(1), dim3(256), 0, st, regs, out64);
+    return hipGetLastError();
+}
+
+hipError_t launch_pfmerge(uint8_t *regs, uint32_t dst, const uint32_t *srcs, uint32_t n,
+                          hipStream_t st) {
+    hipLaunchKernelGGL(k_pfmerge, dim3(kHllRegs / 16 / 256), dim3(256), 0, st, regs, dst, srcs, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_dense(const uint8_t *regs, uint8_t *dense, hipStream_t st) {
+    hipLaunchKernelGGL(k_dense, dim3(kHllRegs / 4 / 256), dim3(256), 0, st, regs, dense);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_swipes(const GenDev &g, uint64_t start, uint64_t n, uint8_t *bytes,
+                             uint32_t *offs, uint32_t *slot, int cus, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_swipes, dim3(grid_for(n, 256, cus * 16)), dim3(256), 0, st, g, start,
+                       n, bytes, offs, slot);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_members(const GenDev &g, uint64_t start, uint64_t n, uint8_t *bytes,
+                              uint32_t *offs, int cus, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_members, dim3(grid_for(n, 256, cus * 16)), dim3(256), 0, st, g, start,
+                       n, bytes, offs);
+    return hipGetLastError();
+}
+
+}  // namespace ske

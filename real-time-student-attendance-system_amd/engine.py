@@ -1,0 +1,188 @@
+"""Device-resident batches and the device-side driver used by the benchmark,
+the GPU parity tests and the sharded runner.
+
+Inputs of the hot path are kept resident in HBM (``DeviceBatch``: packed id
+bytes + u32 offsets + u32 key slots), generated on the GPU by the
+counter-based generator, so a timed step is one K1 launch over a batch that
+is already on the device.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import Context, GenParams, SKE_MEM_DEVICE
+from . import synthetic
+
+
+class DeviceBuffer:
+    def __init__(self, ctx: Context, nbytes: int):
+        self.ctx = ctx
+        p = C.c_void_p()
+        ctx.call("ske_device_alloc", int(max(nbytes, 16)), C.byref(p))
+        self.ptr = p.value
+        self.nbytes = int(nbytes)
+
+    def free(self):
+        if self.ptr:
+            self.ctx.call("ske_device_free", C.c_void_p(self.ptr))
+            self.ptr = None
+
+    def to_host(self, dtype, count) -> np.ndarray:
+        out = np.zeros(count, dtype)
+        if out.nbytes:
+            self.ctx.call("ske_memcpy", out.ctypes.data_as(C.c_void_p), C.c_void_p(self.ptr),
+                          out.nbytes, 1)
+        return out
+
+    def from_host(self, arr: np.ndarray):
+        a = np.ascontiguousarray(arr)
+        assert a.nbytes <= self.nbytes
+        if a.nbytes:
+            self.ctx.call("ske_memcpy", C.c_void_p(self.ptr), a.ctypes.data_as(C.c_void_p),
+                          a.nbytes, 0)
+
+
+class DeviceBatch:
+    """Packed swipes resident on the device."""
+
+    def __init__(self, ctx: Context, n: int, width: int):
+        self.ctx, self.n, self.width = ctx, int(n), int(width)
+        self.bytes = DeviceBuffer(ctx, self.n * width + 64)
+        self.offs = DeviceBuffer(ctx, (self.n + 1) * 4)
+        self.slot = DeviceBuffer(ctx, self.n * 4 + 16)
+
+    @classmethod
+    def from_host(cls, ctx: Context, buf: np.ndarray, offs: np.ndarray, slot: np.ndarray):
+        b = cls.__new__(cls)
+        b.ctx, b.n, b.width = ctx, len(offs) - 1, 0
+        b.bytes = DeviceBuffer(ctx, buf.nbytes + 64)
+        b.offs = DeviceBuffer(ctx, offs.nbytes)
+        b.slot = DeviceBuffer(ctx, max(slot.nbytes, 16))
+        b.bytes.from_host(np.ascontiguousarray(buf, np.uint8))
+        b.offs.from_host(np.ascontiguousarray(offs, np.uint32))
+        b.slot.from_host(np.ascontiguousarray(slot, np.uint32))
+        return b
+
+    def to_host(self):
+        offs = self.offs.to_host(np.uint32, self.n + 1)
+        buf = self.bytes.to_host(np.uint8, int(offs[-1]))
+        slot = self.slot.to_host(np.uint32, self.n)
+        return buf, offs, slot
+
+    def free(self):
+        for b in (self.bytes, self.offs, self.slot):
+            b.free()
+
+
+class SketchEngine:
+    """Device-pointer driver over one libsketch context."""
+
+    def __init__(self, device: int = 0, ctx: Context | None = None):
+        self.ctx = ctx if ctx is not None else Context(device)
+        self._cdf_bufs = []
+
+    # ---- Bloom
+    def reserve(self, fid: int, error: float, capacity: int, expansion: int = 2,
+                nonscaling: bool = False):
+        self.ctx.call("ske_bf_reserve", fid, float(error), int(capacity), int(expansion),
+                      1 if nonscaling else 0)
+
+    def gen_params(self, w: synthetic.Workload, seed=None, slot_base=0) -> GenParams:
+        cdf = synthetic.key_cdf(w)
+        dev = None
+        if cdf is not None:
+            buf = DeviceBuffer(self.ctx, cdf.nbytes)
+            buf.from_host(cdf)
+            self._cdf_bufs.append(buf)
+            dev = buf.ptr
+        return synthetic.gen_params(w, seed=seed, slot_base=slot_base, key_cdf_dev=dev)
+
+    def members_batch(self, p: GenParams, start: int, n: int) -> DeviceBatch:
+        width = self.ctx.lib.ske_gen_id_width(C.byref(p))
+        b = DeviceBatch(self.ctx, n, width)
+        self.ctx.call("ske_gen_members", C.byref(p), int(start), int(n), C.c_void_p(b.bytes.ptr),
+                      C.c_void_p(b.offs.ptr))
+        return b
+
+    def preload(self, fid: int, p: GenParams, n: int, chunk: int = 1 << 24,
+                replies: bool = False) -> np.ndarray | None:
+        """BF.MADD of the first n members (data_generator.py:57-63 scaled)."""
+        outs = []
+        for s in range(0, n, chunk):
+            m = min(chunk, n - s)
+            b = self.members_batch(p, s, m)
+            out = DeviceBuffer(self.ctx, m) if replies else None
+            self.ctx.call("ske_bf_madd", fid, C.c_void_p(b.bytes.ptr), C.c_void_p(b.offs.ptr), m,
+                          C.c_void_p(out.ptr) if out else None, SKE_MEM_DEVICE)
+            if out:
+                outs.append(out.to_host(np.int8, m))
+                out.free()
+            b.free()
+        return np.concatenate(outs) if replies else None
+
+    def swipe_batch(self, p: GenParams, start: int, n: int) -> DeviceBatch:
+        width = self.ctx.lib.ske_gen_id_width(C.byref(p))
+        b = DeviceBatch(self.ctx, n, width)
+        self.ctx.call("ske_gen_swipes", C.byref(p), int(start), int(n), C.c_void_p(b.bytes.ptr),
+                      C.c_void_p(b.offs.ptr), C.c_void_p(b.slot.ptr))
+        return b
+
+    # ---- hot path
+    def hll_reserve(self, nslots: int):
+        self.ctx.call("ske_hll_reserve", int(nslots))
+
+    def swipes(self, fid: int, b: DeviceBatch, out: DeviceBuffer | None = None):
+        self.ctx.call("ske_swipes", fid, C.c_void_p(b.slot.ptr), C.c_void_p(b.bytes.ptr),
+                      C.c_void_p(b.offs.ptr), b.n, C.c_void_p(out.ptr) if out else None,
+                      SKE_MEM_DEVICE)
+
+    def swipes_async(self, fid: int, b: DeviceBatch, out: DeviceBuffer | None = None):
+        self.ctx.call("ske_swipes_async", fid, C.c_void_p(b.slot.ptr), C.c_void_p(b.bytes.ptr),
+                      C.c_void_p(b.offs.ptr), b.n, C.c_void_p(out.ptr) if out else None)
+
+    def swipes_stats(self, fid: int, b: DeviceBatch) -> tuple[int, int]:
+        probes, nvalid = C.c_uint64(), C.c_uint64()
+        self.ctx.call("ske_swipes_stats", fid, C.c_void_p(b.bytes.ptr), C.c_void_p(b.offs.ptr),
+                      b.n, C.byref(probes), C.byref(nvalid))
+        return probes.value, nvalid.value
+
+    def variant(self, fid: int) -> int:
+        return self.ctx.lib.ske_swipes_variant(self.ctx.ptr, fid)
+
+    def set_option(self, name: str, value: int):
+        self.ctx.call("ske_set_option", name.encode(), int(value))
+
+    def set_stream(self, stream_ptr: int | None):
+        self.ctx.call("ske_set_stream", C.c_void_p(stream_ptr) if stream_ptr else None)
+
+    def sync(self):
+        self.ctx.call("ske_sync")
+
+    # ---- HLL reads
+    def registers(self, slot: int) -> np.ndarray:
+        out = np.zeros(16384, np.uint8)
+        self.ctx.call("ske_hll_export_raw", int(slot), out.ctypes.data_as(C.c_void_p))
+        return out
+
+    def registers_all(self, nslots: int) -> np.ndarray:
+        p, nb = C.c_void_p(), C.c_uint64()
+        self.ctx.call("ske_hll_slab", C.byref(p), C.byref(nb))
+        out = np.zeros((nslots, 16384), np.uint8)
+        assert nslots * 16384 <= nb.value
+        self.ctx.call("ske_memcpy", out.ctypes.data_as(C.c_void_p), p, out.nbytes, 1)
+        return out
+
+    def pfcount_each(self, slots) -> np.ndarray:
+        s = np.ascontiguousarray(slots, dtype=np.uint32)
+        out = np.zeros(s.size, np.uint64)
+        if s.size:
+            self.ctx.call("ske_hll_pfcount_each", s.ctypes.data_as(C.c_void_p), s.size,
+                          out.ctypes.data_as(C.c_void_p), 0)
+        return out
+
+    def bloom_bits(self, fid: int, link: int, nbytes: int) -> np.ndarray:
+        out = np.zeros(nbytes, np.uint8)
+        self.ctx.call("ske_bf_export_link", fid, link, out.ctypes.data_as(C.c_void_p), nbytes)
+        return out

@@ -1,0 +1,143 @@
+"""Batched counterpart of the reference's processor and analytics callers.
+
+``AttendanceProcessor`` mirrors attendance_processor.py:26-165 with the
+transport (Pulsar) and persistence (Cassandra) removed: messages arrive as an
+iterable of JSON payloads, and the per-event loop at :100-137 (decode ->
+``BF.EXISTS`` -> valid-gated ``PFADD``) runs as one fused device call per
+batch.  The rows it returns are what the reference inserts into Cassandra
+(:116-124), including invalid events.
+
+``lecture_rankings`` is attendance_analysis.py:87-97 in the PFCOUNT form the
+README describes (README.md:179: "rank by unique daily counts (from HLL)").
+"""
+from __future__ import annotations
+
+import json
+import logging
+from datetime import datetime, timezone
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from .client import SketchClient
+from .config import AttendanceConfig
+from .exceptions import ResponseError
+
+logger = logging.getLogger(__name__)
+
+
+class AttendanceProcessor:
+    def __init__(self, client: SketchClient | None = None, config: AttendanceConfig | None = None):
+        self.config = config or AttendanceConfig()
+        # attendance_processor.py:37-41
+        self.redis_client = client or SketchClient(decode_responses=True, device=self.config.device)
+        self.acked = 0
+        self.nacked = 0
+
+    # attendance_processor.py:74-92
+    def _setup_bloom_filter(self):
+        cfg = self.config
+        try:
+            self.redis_client.execute_command("BF.EXISTS", cfg.bloom_filter_key, "test")
+            logger.info("Bloom Filter already exists")
+            if cfg.faithful_setup:
+                return
+            if self.redis_client.exists(cfg.bloom_filter_key):
+                return
+            raise ResponseError("ERR not found")
+        except ResponseError:
+            try:
+                self.redis_client.execute_command("BF.RESERVE", cfg.bloom_filter_key,
+                                                  cfg.bloom_filter_error_rate,
+                                                  cfg.bloom_filter_capacity)
+                logger.info("Created new Bloom Filter")
+            except ResponseError as e:
+                if "already exists" not in str(e):
+                    raise
+
+    def hll_key(self, lecture_id: str, timestamp: datetime) -> str:
+        """attendance_processor.py:128 (code form) or README.md:105-106 form."""
+        if self.config.hll_key_form == "code":
+            return f"{self.config.hll_key_prefix}{lecture_id}"
+        if timestamp.tzinfo is not None:
+            timestamp = timestamp.astimezone(timezone.utc)
+        return f"{self.config.hll_key_prefix}{lecture_id}:{timestamp.date().isoformat()}"
+
+    def process_batch(self, messages: Sequence) -> list[dict]:
+        """One batch of the loop at attendance_processor.py:100-137.
+
+        Returns one row per decodable message: student_id, lecture_id,
+        timestamp, is_valid (what :121-124 inserts).  Undecodable messages are
+        negatively acknowledged (:134-136) and produce no row."""
+        ids, keys, rows = [], [], []
+        for m in messages:
+            try:
+                data = json.loads(m.decode() if isinstance(m, (bytes, bytearray)) else m) \
+                    if not isinstance(m, dict) else m
+                student_id = data["student_id"]
+                lecture_id = data["lecture_id"]
+                ts = datetime.fromisoformat(data["timestamp"])
+            except Exception as e:  # :134-136
+                logger.error(f"Error processing message: {e}")
+                self.nacked += 1
+                continue
+            ids.append(student_id)
+            keys.append(self.hll_key(lecture_id, ts))
+            rows.append({"student_id": student_id, "lecture_id": lecture_id, "timestamp": ts})
+        if rows:
+            valid = self.redis_client.swipes(self.config.bloom_filter_key, keys, ids)
+            for r, v in zip(rows, valid):
+                r["is_valid"] = bool(v)
+            self.acked += len(rows)
+        return rows
+
+    def process_attendance(self, source: Iterable, batch_size: int | None = None):
+        """attendance_processor.py:94-141 over an in-memory message source;
+        yields the rows of each processed batch."""
+        logger.info("Starting attendance processing...")
+        self._setup_bloom_filter()
+        bs = batch_size or self.config.batch_size
+        batch = []
+        for m in source:
+            batch.append(m)
+            if len(batch) >= bs:
+                yield self.process_batch(batch)
+                batch = []
+        if batch:
+            yield self.process_batch(batch)
+
+    # attendance_processor.py:149-165 (the Cassandra half is out of scope)
+    def get_attendance_stats(self, lecture_id: str, day: str | None = None) -> dict:
+        if self.config.hll_key_form == "code" or day is None:
+            key = f"{self.config.hll_key_prefix}{lecture_id}" + (f":{day}" if day else "")
+        else:
+            key = f"{self.config.hll_key_prefix}{lecture_id}:{day}"
+        return {"unique_attendees": self.redis_client.pfcount(key)}
+
+
+def lecture_rankings(client: SketchClient, keys: Sequence[str], k: int = 3) -> dict:
+    """Most / least attended lecture-day keys by PFCOUNT (one K2 launch).
+
+    Order: count descending, then key ascending (the reference's pandas
+    ``sort_values(ascending=False)`` leaves ties in quicksort order; a total
+    order is used here so results are reproducible).  ``least_attended`` is
+    the tail of the same order, as ``.tail(3)`` (attendance_analysis.py:95)."""
+    keys = list(keys)
+    counts = client.pfcount_each(keys).astype(np.int64)
+    order = sorted(range(len(keys)), key=lambda i: (-counts[i], keys[i]))
+    head = order[:k]
+    tail = order[-k:] if k else []
+    return {"most_attended": {keys[i]: int(counts[i]) for i in head},
+            "least_attended": {keys[i]: int(counts[i]) for i in tail}}
+
+
+def campus_rollup(client: SketchClient, groups: dict, dest: str | None = None) -> dict:
+    """Per-lecture unions over their day keys (PFCOUNT k1..kn per lecture, one
+    launch) and, when ``dest`` is given, a campus-wide PFMERGE of every key."""
+    names = list(groups)
+    counts = client.pfcount_groups([groups[n] for n in names])
+    out = {"per_lecture": {n: int(c) for n, c in zip(names, counts)}}
+    if dest is not None:
+        client.pfmerge(dest, *[k for n in names for k in groups[n]])
+        out["campus_unique"] = client.pfcount(dest)
+    return out
