@@ -35,9 +35,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="swipes per step (default: config)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--probe-batch", type=int, default=0)
+    ap.add_argument("--tile", type=int, default=0, help="K1 swipes per thread in flight (1,2,4,8)")
     ap.add_argument("--variant", type=int, default=-1, help="-1 auto, 0 global Bloom, 1 LDS Bloom")
     ap.add_argument("--max-batches", type=int, default=64)
+    ap.add_argument("--ablate", type=int, default=0, help="diagnostic: K1 parts removed (bits)")
     return ap.parse_args()
 
 
@@ -95,10 +96,12 @@ def main():
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     engine.set_stream(stream.cuda_stream)
-    if args.probe_batch:
-        engine.set_option("probe_batch", args.probe_batch)
+    if args.tile:
+        engine.set_option("tile", args.tile)
     if args.variant >= 0:
         engine.set_option("variant", args.variant)
+    if args.ablate:
+        engine.set_option("ablate", args.ablate)
 
     # Bloom preload (replicated on every rank), HLL key shard of this rank
     engine.reserve(0, w.bf_error, w.bf_capacity)
@@ -166,7 +169,7 @@ def main():
                    "bloom": {"error": w.bf_error, "capacity": w.bf_capacity},
                    "id_bytes": width, "parallelism": f"dp{world} (key-sharded, Bloom replicated)",
                    "k1_variant": "lds-bloom" if engine.variant(0) else "global-bloom",
-                   "probe_batch": args.probe_batch or 1},
+                   "tile": args.tile or 4},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "k_swipes", "kernel_ms": kern_ms,

@@ -68,8 +68,9 @@ struct ske_ctx {
     size_t stg_cap[8] = {};
     unsigned int *err = nullptr;
     unsigned long long *stats = nullptr;
-    int pb = 1;           // probe batch (1 = RedisBloom order)
+    int pb = 4;           // K1 tile: swipes per thread in flight (1, 2, 4, 8)
     int variant = -1;     // -1 auto, 0 global, 1 LDS
+    uint32_t ablate = 0;  // diagnostic only (kAblate* bits)
     bool lds_ok = false;
     std::string last_hip;
 };
@@ -389,9 +390,14 @@ int ske_memcpy(ske_ctx *c, void *dst, const void *src, uint64_t bytes, int kind)
 
 int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
     if (!c || !name) return SKE_EINVAL;
-    if (!strcmp(name, "probe_batch")) {
-        if (value != 1 && value != 2 && value != 4) return SKE_EINVAL;
+    if (!strcmp(name, "tile")) {
+        if (value != 1 && value != 2 && value != 4 && value != 8) return SKE_EINVAL;
         c->pb = int(value);
+        return SKE_OK;
+    }
+    if (!strcmp(name, "ablate")) {
+        if (value < 0 || value > 7) return SKE_EINVAL;
+        c->ablate = uint32_t(value);
         return SKE_OK;
     }
     if (!strcmp(name, "variant")) {
@@ -717,7 +723,9 @@ int ske_swipes_async(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8
     Filter *F = get_filter(c, fid);
     if (!F) return SKE_EINVAL;
     const ChainDev ch = F->exists ? chain_dev(*F) : ChainDev{};
-    HIPCHK(c, launch_swipes(0, ch, use_lds(c, ch), c->pb, bytes, offs, slot, n, c->regs,
+    ChainDev cha = ch;
+    cha.ablate = c->ablate;
+    HIPCHK(c, launch_swipes(0, cha, use_lds(c, ch), c->pb, bytes, offs, slot, n, c->regs,
                             c->nslots, out_valid, (unsigned long long *)c->err, c->cus, c->st));
     return SKE_OK;
 }
@@ -729,8 +737,9 @@ int ske_swipes_stats(ske_ctx *c, uint32_t fid, const uint8_t *bytes, const uint3
     if (!F) return SKE_EINVAL;
     const ChainDev ch = F->exists ? chain_dev(*F) : ChainDev{};
     HIPCHK(c, hipMemsetAsync(c->stats, 0, 16, c->st));
-    // PB = 1: count RedisBloom's exact sequential probes
-    HIPCHK(c, launch_swipes(2, ch, use_lds(c, ch), 1, bytes, offs, nullptr, n, nullptr, 0, nullptr,
+    // every tile size follows RedisBloom's per-swipe probe order, so the
+    // count is the sequential one
+    HIPCHK(c, launch_swipes(2, ch, use_lds(c, ch), c->pb, bytes, offs, nullptr, n, nullptr, 0, nullptr,
                             c->stats, c->cus, c->st));
     unsigned long long h[2] = {0, 0};
     HIPCHK(c, hipMemcpyAsync(h, c->stats, 16, hipMemcpyDeviceToHost, c->st));

@@ -43,99 +43,164 @@ __device__ __forceinline__ bool reg_max(uint8_t *reg, uint32_t rank) {
 
 enum SwipeMode { kModeSwipes = 0, kModeExists = 1, kModeStats = 2 };
 
-// Membership of one item in one link: k probes of the sequence
-// x_i = (a + i*b) mod 2^64 mod bits, PB probe loads in flight per batch,
-// early exit between batches (PB = 1 is RedisBloom's exact probe order).
-template <bool kLds, int PB>
-__device__ __forceinline__ bool link_check(const LinkDev &L, const uint8_t *lds, uint64_t ha,
-                                           uint64_t hb, uint32_t &probes) {
-    ProbeCursor c;
-    c.init(ha, hb, L.div);
-    const uint32_t k = L.k;
-    for (uint32_t j0 = 0; j0 < k; j0 += PB) {
-        uint8_t byte[PB];
-        uint32_t bit[PB];
-#pragma unroll
-        for (int u = 0; u < PB; u++) {
-            if (j0 + u < k) {
-                const uint64_t x = c.x;
-                bit[u] = uint32_t(x & 7);
-                byte[u] = kLds ? lds[L.lds_off + uint32_t(x >> 3)] : L.bf[x >> 3];
-                c.step(L.div);
-            } else {
-                bit[u] = 0;
-                byte[u] = 1;
-            }
-        }
-        bool all = true;
-#pragma unroll
-        for (int u = 0; u < PB; u++) {
-            if (j0 + u < k) {
-                probes++;
-                if (!((byte[u] >> bit[u]) & 1)) {
-                    all = false;
-                    break;
-                }
-            }
-        }
-        if (!all) return false;
-    }
-    return true;
-}
-
-template <bool kLds, int PB>
-__device__ __forceinline__ bool chain_check(const ChainDev &ch, const uint8_t *lds, uint64_t ha,
-                                            uint64_t hb, uint32_t &probes) {
-    for (int l = ch.nlinks - 1; l >= 0; --l)
-        if (link_check<kLds, PB>(ch.link[l], lds, ha, hb, probes)) return true;
-    return false;
-}
-
 constexpr int kLdsBloomMax = 152 * 1024;  // LDS image budget (160 KiB per CU)
 
-template <int kMode, bool kLds, int PB>
+// Copy every link's bit array into the LDS image (16-byte granules over the
+// 16-B padded links, 4 loads in flight per thread before the stores).
+__device__ __forceinline__ void stage_bloom(const ChainDev &ch, uint8_t *lds) {
+    for (int l = 0; l < ch.nlinks; l++) {
+        const LinkDev &L = ch.link[l];
+        const uint4 *src = reinterpret_cast<const uint4 *>(L.bf);
+        uint4 *dst = reinterpret_cast<uint4 *>(lds + L.lds_off);
+        const uint32_t nq = uint32_t(((L.div.d >> 3) + 15) >> 4);
+        uint32_t q = threadIdx.x;
+        for (; q + 3 * blockDim.x < nq; q += 4 * blockDim.x) {
+            const uint4 a = src[q], b = src[q + blockDim.x], c = src[q + 2 * blockDim.x],
+                        d = src[q + 3 * blockDim.x];
+            dst[q] = a;
+            dst[q + blockDim.x] = b;
+            dst[q + 2 * blockDim.x] = c;
+            dst[q + 3 * blockDim.x] = d;
+        }
+        for (; q < nq; q += blockDim.x) dst[q] = src[q];
+    }
+}
+
+// K1, tiled: every thread owns U swipes of a tile (swipe base + u*T + tid,
+// so a wave's 64 lanes read 64 consecutive offsets / ids).  All loads of a
+// tile are issued before any is consumed, and the Bloom test advances the U
+// swipes in lock step -- round j issues the j-th probe of every swipe still
+// undecided -- so each thread keeps U probe loads in flight while every swipe
+// still follows RedisBloom's sequential order (newest link first, stop at the
+// first unset bit; the probe count equals the CPU oracle's).  Each block
+// works on one contiguous chunk of the batch.  LDS variant: the Bloom image
+// is staged while the first tile's loads are in flight.
+template <int kMode, bool kLds, int U>
 __global__ void __launch_bounds__(kLds ? 1024 : 256)
     k_swipes(const ChainDev ch, const uint8_t *__restrict__ bytes,
              const uint32_t *__restrict__ offs, const uint32_t *__restrict__ slot, uint64_t n,
              uint8_t *__restrict__ regs, uint32_t nslots, uint8_t *__restrict__ out,
              unsigned long long *__restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_img[];
-    if constexpr (kLds) {
-        // stage every link's bit array into LDS (8-byte granules: link bytes
-        // are multiples of 8 by bloom_init's rounding)
-        for (int l = 0; l < ch.nlinks; l++) {
-            const LinkDev &L = ch.link[l];
-            const uint64_t *src = reinterpret_cast<const uint64_t *>(L.bf);
-            uint64_t *dst = reinterpret_cast<uint64_t *>(lds_img + L.lds_off);
-            const uint32_t nw = uint32_t(L.div.d >> 6);
-            for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) dst[w] = src[w];
-        }
-        __syncthreads();
-    }
+    const uint32_t T = blockDim.x, tid = threadIdx.x;
+    const uint64_t per_block = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t c0 = uint64_t(blockIdx.x) * per_block;
+    const uint64_t c1 = c0 + per_block < n ? c0 + per_block : n;
+    bool staged = !kLds;
     uint32_t probes = 0, nvalid = 0;
-    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint32_t b = offs[i], e = offs[i + 1];
-        const Item it = load_item(bytes, b, e);
-        const uint64_t ha = murmur_item(it, kBloomSeed);
-        const uint64_t hb = murmur_item(it, ha);
-        const bool valid = chain_check<kLds, PB>(ch, lds_img, ha, hb, probes);
+    const bool ablate_probe = kMode == kModeSwipes && (ch.ablate & kAblateProbe);
+    const bool do_hll = kMode == kModeSwipes && !(ch.ablate & kAblateHll);
+    // a block with no work still joins the staging barrier below
+    for (uint64_t base = c0; base < c1 || !staged; base += uint64_t(T) * U) {
+        Item it[U];
+        uint32_t sl[U];
+        bool act[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t i = base + uint64_t(u) * T + tid;
+            act[u] = i < c1;
+            it[u].len = 0;
+            sl[u] = 0;
+            if (act[u]) {
+                const uint32_t b = offs[i], e = offs[i + 1];
+                it[u] = load_item(bytes, b, e);
+                if (do_hll) sl[u] = slot[i];
+            }
+        }
+        if (!staged) {
+            stage_bloom(ch, lds_img);
+            __syncthreads();
+            staged = true;
+        }
+        uint64_t ha[U], hb[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            ha[u] = murmur_item(it[u], kBloomSeed);
+            hb[u] = murmur_item(it[u], ha[u]);
+        }
+        bool valid[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) valid[u] = ablate_probe && act[u];
+        if (!ablate_probe) {
+            for (int l = ch.nlinks - 1; l >= 0; --l) {
+                const LinkDev &L = ch.link[l];
+                ProbeCursor c[U];
+                bool alive[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    alive[u] = act[u] && !valid[u];
+                    c[u].init(ha[u], hb[u], L.div);
+                }
+                for (uint32_t j = 0; j < L.k; j++) {
+                    uint8_t byte[U];
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        const uint64_t x = c[u].x;
+                        byte[u] = alive[u] ? (kLds ? lds_img[L.lds_off + uint32_t(x >> 3)]
+                                                   : L.bf[x >> 3])
+                                           : uint8_t(0);
+                    }
+                    bool any = false;
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        if (alive[u]) {
+                            probes++;
+                            alive[u] = (byte[u] >> (c[u].x & 7)) & 1;
+                            c[u].step(L.div);
+                            any |= alive[u];
+                        }
+                    }
+                    if (!any) break;
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) valid[u] |= alive[u];
+            }
+        }
         if constexpr (kMode == kModeSwipes) {
-            if (valid) {
-                const uint32_t s = slot[i];
-                if (s < nslots) {
-                    uint32_t idx, rank;
-                    hll_patlen(murmur_item(it, kHllSeed), idx, rank);
-                    reg_max(regs + size_t(s) * kHllRegs + idx, rank);
-                } else {
-                    atomicOr(reinterpret_cast<unsigned int *>(stats), 1u);
+            if (do_hll) {
+                uint8_t *reg[U];
+                uint32_t rank[U], cur[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    reg[u] = nullptr;
+                    rank[u] = 0;
+                    if (valid[u]) {
+                        if (sl[u] < nslots) {
+                            uint32_t idx;
+                            hll_patlen(murmur_item(it[u], kHllSeed), idx, rank[u]);
+                            reg[u] = regs + size_t(sl[u]) * kHllRegs + idx;
+                        } else {
+                            atomicOr(reinterpret_cast<unsigned int *>(stats), 1u);
+                        }
+                    }
+                }
+                // pre-check loads of all U registers in flight together; a
+                // stale value is never too high (registers only grow)
+#pragma unroll
+                for (int u = 0; u < U; u++) cur[u] = reg[u] ? *reg[u] : 0xffu;
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    if (cur[u] < rank[u]) {
+                        if (ch.ablate & kAblateCas) {
+                            if (out) out[base + uint64_t(u) * T + tid] = 2;
+                        } else {
+                            reg_max(reg[u], rank[u]);
+                        }
+                    }
                 }
             }
-            if (out) out[i] = valid;
+            if (out) {
+#pragma unroll
+                for (int u = 0; u < U; u++)
+                    if (act[u]) out[base + uint64_t(u) * T + tid] = valid[u];
+            }
         } else if constexpr (kMode == kModeExists) {
-            out[i] = valid;
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (act[u]) out[base + uint64_t(u) * T + tid] = valid[u];
         } else {
-            nvalid += valid;
+#pragma unroll
+            for (int u = 0; u < U; u++) nvalid += valid[u];
         }
     }
     if constexpr (kMode == kModeStats) {
@@ -377,57 +442,60 @@ static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
     return unsigned(g < cap ? g : cap);
 }
 
-template <int kMode, int PB>
-static hipError_t launch_swipes_pb(const ChainDev &ch, bool lds, const uint8_t *bytes,
-                                   const uint32_t *offs, const uint32_t *slot, uint64_t n,
-                                   uint8_t *regs, uint32_t nslots, uint8_t *out,
-                                   unsigned long long *stats, int cus, hipStream_t st) {
+template <int kMode, int U>
+static hipError_t launch_swipes_u(const ChainDev &ch, bool lds, const uint8_t *bytes,
+                                  const uint32_t *offs, const uint32_t *slot, uint64_t n,
+                                  uint8_t *regs, uint32_t nslots, uint8_t *out,
+                                  unsigned long long *stats, int cus, hipStream_t st) {
     if (lds) {
-        const unsigned grid = grid_for(n, 1024, unsigned(cus));
-        hipLaunchKernelGGL((k_swipes<kMode, true, PB>), dim3(grid), dim3(1024), ch.lds_bytes, st, ch,
+        // one 1024-thread block per CU (the LDS image caps residency at one)
+        const unsigned grid = grid_for(n, 1024 * U, unsigned(cus));
+        hipLaunchKernelGGL((k_swipes<kMode, true, U>), dim3(grid), dim3(1024), ch.lds_bytes, st, ch,
                            bytes, offs, slot, n, regs, nslots, out, stats);
     } else {
-        const unsigned grid = grid_for(n, 256, unsigned(cus) * 16);
-        hipLaunchKernelGGL((k_swipes<kMode, false, PB>), dim3(grid), dim3(256), 0, st, ch, bytes,
+        const unsigned grid = grid_for(n, 256 * U, unsigned(cus) * 8);
+        hipLaunchKernelGGL((k_swipes<kMode, false, U>), dim3(grid), dim3(256), 0, st, ch, bytes,
                            offs, slot, n, regs, nslots, out, stats);
     }
     return hipGetLastError();
 }
 
-hipError_t launch_swipes(int mode, const ChainDev &ch, bool lds, int pb, const uint8_t *bytes,
+hipError_t launch_swipes(int mode, const ChainDev &ch, bool lds, int tile, const uint8_t *bytes,
                          const uint32_t *offs, const uint32_t *slot, uint64_t n, uint8_t *regs,
                          uint32_t nslots, uint8_t *out, unsigned long long *stats, int cus,
                          hipStream_t st) {
     if (n == 0) return hipSuccess;
-#define SKE_PB(P)                                                                                  \
+#define SKE_U(UU)                                                                                  \
     if (mode == kModeSwipes)                                                                       \
-        return launch_swipes_pb<kModeSwipes, P>(ch, lds, bytes, offs, slot, n, regs, nslots, out,  \
+        return launch_swipes_u<kModeSwipes, UU>(ch, lds, bytes, offs, slot, n, regs, nslots, out,  \
                                                 stats, cus, st);                                   \
     if (mode == kModeExists)                                                                       \
-        return launch_swipes_pb<kModeExists, P>(ch, lds, bytes, offs, slot, n, regs, nslots, out,  \
+        return launch_swipes_u<kModeExists, UU>(ch, lds, bytes, offs, slot, n, regs, nslots, out,  \
                                                 stats, cus, st);                                   \
-    return launch_swipes_pb<kModeStats, P>(ch, lds, bytes, offs, slot, n, regs, nslots, out,       \
+    return launch_swipes_u<kModeStats, UU>(ch, lds, bytes, offs, slot, n, regs, nslots, out,       \
                                            stats, cus, st);
-    if (pb >= 4) {
-        SKE_PB(4)
-    } else if (pb >= 2) {
-        SKE_PB(2)
+    if (tile >= 8) {
+        SKE_U(8)
+    } else if (tile >= 4) {
+        SKE_U(4)
+    } else if (tile >= 2) {
+        SKE_U(2)
     } else {
-        SKE_PB(1)
+        SKE_U(1)
     }
-#undef SKE_PB
+#undef SKE_U
 }
 
 hipError_t lds_bloom_setup() {
     // allow the LDS-staged variant to declare up to kLdsBloomMax bytes
     hipError_t e = hipSuccess;
-#define SKE_ATTR(M, P)                                                                             \
-    e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_swipes<M, true, P>),                 \
+#define SKE_ATTR(M, UU)                                                                            \
+    e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_swipes<M, true, UU>),                \
                             hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBloomMax);             \
     if (e != hipSuccess) return e;
-    SKE_ATTR(kModeSwipes, 1) SKE_ATTR(kModeSwipes, 2) SKE_ATTR(kModeSwipes, 4)
-    SKE_ATTR(kModeExists, 1) SKE_ATTR(kModeExists, 2) SKE_ATTR(kModeExists, 4)
-    SKE_ATTR(kModeStats, 1) SKE_ATTR(kModeStats, 2) SKE_ATTR(kModeStats, 4)
+    SKE_ATTR(kModeSwipes, 1) SKE_ATTR(kModeSwipes, 2) SKE_ATTR(kModeSwipes, 4) SKE_ATTR(kModeSwipes, 8)
+    SKE_ATTR(kModeExists, 1) SKE_ATTR(kModeExists, 2) SKE_ATTR(kModeExists, 4) SKE_ATTR(kModeExists, 8)
+    SKE_ATTR(kModeStats, 1) SKE_ATTR(kModeStats, 2) SKE_ATTR(kModeStats, 4) SKE_ATTR(kModeStats, 8)
 #undef SKE_ATTR
     return e;
 }

@@ -1,0 +1,51 @@
+"""redis-py argument encoding (Encoder.encode) and the packed-item layout."""
+import numpy as np
+import pytest
+
+
+def test_encode_rules(pkg):
+    enc = pkg.encode
+    assert enc(12345) == b"12345"            # data_generator.py:113 ints
+    assert enc(-7) == b"-7"
+    assert enc(0.01) == b"0.01"              # BF.RESERVE error rate (attendance_processor.py:86)
+    assert enc("S123456") == b"S123456"      # README.md:93 string ids
+    assert enc("é") == "é".encode("utf-8")
+    assert enc(b"\x00\xff") == b"\x00\xff"
+    assert enc(memoryview(b"ab")) == b"ab"
+    assert enc(np.int64(42)) == b"42"
+    with pytest.raises(pkg.DataError):
+        enc(True)
+    with pytest.raises(pkg.DataError):
+        enc(None)
+    with pytest.raises(pkg.DataError):
+        enc([1])
+
+
+def test_pack_layout(pkg):
+    buf, offs = pkg.pack([1, "ab", b"", 99999])
+    assert offs.tolist() == [0, 1, 3, 3, 8]
+    assert bytes(buf) == b"1ab99999"
+    buf, offs = pkg.pack([])
+    assert offs.tolist() == [0] and buf.size == 0
+
+
+def test_pack_ints_matches_pack(pkg):
+    rng = np.random.default_rng(0)
+    vals = np.concatenate([
+        np.array([0, 1, 9, 10, 99, 100, 999, 10**9, 10**18, 2**63 - 1, 2**64 - 1], dtype=np.uint64),
+        rng.integers(0, 2**63, 500, dtype=np.uint64),
+        rng.integers(0, 10**7, 500).astype(np.uint64)])
+    b1, o1 = pkg.pack_ints(vals)
+    b2, o2 = pkg.pack([int(v) for v in vals])
+    assert np.array_equal(o1, o2) and np.array_equal(b1, b2)
+    b, o = pkg.pack_ints(np.zeros(0, np.uint64))
+    assert b.size == 0 and o.tolist() == [0]
+
+
+def test_keyhash_matches_oracle(orc):
+    from rtsas_amd.keyhash import murmur64a
+    rng = np.random.default_rng(1)
+    for n in list(range(0, 30)) + [64, 100]:
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        for seed in (0, 0xADC83B19, 2**64 - 1):
+            assert murmur64a(d, seed) == orc.murmur64a(d, seed)

@@ -37,10 +37,10 @@ def test_mexists_random_bytes_vs_oracle(client, orc):
 
 
 @pytest.mark.parametrize("variant", [0, 1])
-@pytest.mark.parametrize("pb", [1, 2, 4])
+@pytest.mark.parametrize("pb", [1, 2, 4, 8])
 def test_mexists_variants(client, orc, variant, pb):
     client.ctx.call("ske_set_option", b"variant", variant)
-    client.ctx.call("ske_set_option", b"probe_batch", pb)
+    client.ctx.call("ske_set_option", b"tile", pb)
     rng = np.random.default_rng(2)
     ids = rng.choice(np.arange(10**6, 10**7), 30000, replace=False)
     client.execute_command("BF.RESERVE", "bf", 0.01, 20000)
@@ -228,7 +228,7 @@ def _oracle_swipes(orc, chain, nkeys, buf, offs, slot):
 
 
 @pytest.mark.parametrize("variant", [0, 1])
-@pytest.mark.parametrize("pb", [1, 4])
+@pytest.mark.parametrize("pb", [1, 4, 8])
 def test_swipes_c2_shape_vs_oracle(engine, orc, variant, pb):
     """Fused BF.EXISTS + PFADD on a C2-shaped stream (7-digit ids, 10 %
     invalid, 50 keys) generated on device: valid flags and all 50 register
@@ -237,7 +237,7 @@ def test_swipes_c2_shape_vs_oracle(engine, orc, variant, pb):
     w = synthetic.WORKLOADS["c2"]
     w = synthetic.Workload(**{**w.__dict__, "n_members": 20000, "bf_capacity": 20000})
     engine.set_option("variant", variant)
-    engine.set_option("probe_batch", pb)
+    engine.set_option("tile", pb)
     engine.reserve(0, w.bf_error, w.bf_capacity)
     p = engine.gen_params(w)
     engine.preload(0, p, w.n_members)

@@ -1,0 +1,144 @@
+"""Processor counterpart (attendance_processor.py:26-165) and rankings
+(attendance_analysis.py:87-97): host logic on CPU with an oracle-backed
+client double; the real device client in the gpu-marked test."""
+import json
+from datetime import datetime, timedelta
+
+import numpy as np
+import pytest
+
+
+def reference_messages(seed=0, n_students=200, days=3):
+    """Messages with the reference generator's schema and mix
+    (data_generator.py:84-185): entry + exit per student-day, ~15 % invalid
+    attempts from a 6-digit pool, plus 20 standalone invalids."""
+    rng = np.random.default_rng(seed)
+    valid = [int(x) for x in rng.choice(np.arange(10000, 100000), n_students, replace=False)]
+    invalid = [int(x) for x in rng.choice(np.arange(100000, 1000000), 50, replace=False)]
+    base = datetime(2025, 3, 17)
+    msgs = []
+    for sid in valid:
+        for d in rng.choice(days, int(rng.integers(1, days + 1)), replace=False):
+            day = base + timedelta(days=int(d))
+            entry = day.replace(hour=int(rng.integers(8, 12)), minute=int(rng.integers(0, 60)))
+            exit_ = entry + timedelta(hours=int(rng.integers(3, 5)))
+            for ts, et in ((entry, "entry"), (exit_, "exit")):
+                msgs.append({"student_id": sid, "timestamp": ts.isoformat(),
+                             "lecture_id": f"LECTURE_{ts.strftime('%Y%m%d')}", "is_valid": True,
+                             "event_type": et})
+            if rng.random() < 0.15:
+                msgs.append({"student_id": int(rng.choice(invalid)), "timestamp": entry.isoformat(),
+                             "lecture_id": f"LECTURE_{entry.strftime('%Y%m%d')}",
+                             "is_valid": False, "event_type": "entry"})
+    for _ in range(20):
+        day = base + timedelta(days=int(rng.integers(0, days)))
+        msgs.append({"student_id": int(rng.choice(invalid)), "timestamp": day.isoformat(),
+                     "lecture_id": f"LECTURE_{day.strftime('%Y%m%d')}", "is_valid": False,
+                     "event_type": "entry"})
+    return valid, [json.dumps(m).encode() for m in msgs]
+
+
+class OracleClient:
+    """Test double with the SketchClient methods the processor uses."""
+
+    def __init__(self, orc):
+        self.orc = orc
+        self.chains, self.hlls, self.calls = {}, {}, []
+
+    def execute_command(self, *a):
+        self.calls.append(a[0])
+        if a[0] == "BF.EXISTS":
+            c = self.chains.get(a[1])
+            return c.exists(str(a[2]).encode()) if c else 0
+        if a[0] == "BF.RESERVE":
+            self.chains[a[1]] = self.orc.Chain(int(a[3]), float(a[2]))
+            return "OK"
+        if a[0] == "BF.ADD":
+            c = self.chains.setdefault(a[1], self.orc.Chain(100, 0.01))
+            return c.add(str(a[2]).encode())
+        raise NotImplementedError(a[0])
+
+    def exists(self, k):
+        return int(k in self.chains or k in self.hlls)
+
+    def swipes(self, bf_key, keys, ids):
+        c = self.chains.get(bf_key)
+        out = []
+        for k, i in zip(keys, ids):
+            v = bool(c.exists(str(i).encode())) if c else False
+            if v:
+                self.hlls.setdefault(k, self.orc.HLL()).add(str(i).encode())
+            out.append(v)
+        return np.array(out)
+
+    def pfcount(self, *keys):
+        u = self.orc.HLL()
+        for k in keys:
+            if k in self.hlls:
+                u.merge(self.hlls[k])
+        return u.count()
+
+
+def test_setup_quirk_and_batches(pkg, orc):
+    """BF.EXISTS on the missing key answers 0, so the reference's BF.RESERVE
+    branch never runs (attendance_processor.py:76-92) -- reproduced."""
+    cl = OracleClient(orc)
+    p = pkg.AttendanceProcessor(client=cl, config=pkg.AttendanceConfig(batch_size=100))
+    valid, msgs = reference_messages()
+    for sid in valid:  # data_generator.py:57-63: BF.ADD per id (auto-create)
+        cl.execute_command("BF.ADD", "bf:students", sid)
+    rows = [r for batch in p.process_attendance(msgs + [b"{not json", b'{"student_id": 1}'])
+            for r in batch]
+    assert "BF.RESERVE" not in cl.calls
+    assert len(rows) == len(msgs) and p.nacked == 2 and p.acked == len(msgs)
+    truth = [json.loads(m)["is_valid"] for m in msgs]
+    assert sum(r["is_valid"] for r in rows) >= sum(truth)      # Bloom: no false negatives
+    assert all(r["is_valid"] for r, t in zip(rows, truth) if t)
+    key = "hll:unique:LECTURE_20250317:2025-03-17"
+    assert key in cl.hlls
+    assert p.get_attendance_stats("LECTURE_20250317", "2025-03-17")["unique_attendees"] == \
+        cl.hlls[key].count()
+
+
+def test_non_faithful_setup_reserves(pkg, orc):
+    cl = OracleClient(orc)
+    cfg = pkg.AttendanceConfig(faithful_setup=False)
+    pkg.AttendanceProcessor(client=cl, config=cfg)._setup_bloom_filter()
+    assert "BF.RESERVE" in cl.calls
+    assert cl.chains["bf:students"].link_info(0)["entries"] == 100000
+
+
+def test_key_forms(pkg, orc):
+    p = pkg.AttendanceProcessor(client=OracleClient(orc))
+    ts = datetime.fromisoformat("2025-03-19T23:30:00-02:00")
+    assert p.hll_key("CS101-L1", ts) == "hll:unique:CS101-L1:2025-03-20"   # UTC day
+    p.config.hll_key_form = "code"
+    assert p.hll_key("LECTURE_20250319", ts) == "hll:unique:LECTURE_20250319"
+
+
+@pytest.mark.gpu
+def test_processor_end_to_end_on_device(pkg, orc):
+    client = pkg.SketchClient(decode_responses=True)
+    p = pkg.AttendanceProcessor(client=client, config=pkg.AttendanceConfig(batch_size=257))
+    ref = OracleClient(orc)
+    pref = pkg.AttendanceProcessor(client=ref)
+    valid, msgs = reference_messages(seed=3, n_students=1000, days=7)
+    for sid in valid:
+        client.execute_command("BF.ADD", "bf:students", sid)
+        ref.execute_command("BF.ADD", "bf:students", sid)
+    rows = [r for b in p.process_attendance(msgs) for r in b]
+    want = [r for b in pref.process_attendance(msgs) for r in b]
+    assert [r["is_valid"] for r in rows] == [r["is_valid"] for r in want]
+    keys = sorted(ref.hlls)
+    for k in keys:
+        assert np.array_equal(client.hll_registers(k), ref.hlls[k].regs)
+    got = pkg.lecture_rankings(client, keys, k=3)
+    counts = {k: ref.hlls[k].count() for k in keys}
+    order = sorted(keys, key=lambda k: (-counts[k], k))
+    assert list(got["most_attended"]) == order[:3]
+    assert list(got["least_attended"]) == order[-3:]
+    roll = pkg.campus_rollup(client, {"all": keys}, dest="hll:campus")
+    u = orc.HLL()
+    for k in keys:
+        u.merge(ref.hlls[k])
+    assert roll["per_lecture"]["all"] == u.count() == roll["campus_unique"]

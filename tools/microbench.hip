@@ -1,0 +1,91 @@
+// microbench.hip -- what bounds K1's base path (offsets -> id bytes -> hash)?
+// Standalone diagnostic (not part of libsketch): times kernels that add one
+// stage at a time over n packed 7-byte ids, at several n.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "../real-time-student-attendance-system_amd/csrc/sketch_common.h"
+
+using namespace ske;
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+__global__ void k_stream16(const uint4 *p, uint64_t nq, uint32_t *sink) {
+    uint32_t acc = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint4 v = p[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+template <int STAGE>
+__global__ void k_base(const uint8_t *bytes, const uint32_t *offs, uint64_t n, uint32_t *sink) {
+    uint64_t acc = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t b = offs[i], e = offs[i + 1];
+        if (STAGE == 0) { acc += b ^ e; continue; }
+        const Item it = load_item(bytes, b, e);
+        if (STAGE == 1) { acc += it.w0; continue; }
+        const uint64_t ha = murmur_item(it, kBloomSeed);
+        if (STAGE == 2) { acc += ha; continue; }
+        const uint64_t hb = murmur_item(it, ha);
+        const uint64_t hh = murmur_item(it, kHllSeed);
+        acc += hb ^ hh;
+    }
+    if (acc == 0x123456789ull) sink[0] = 1;
+}
+
+template <typename F>
+float time_it(F f, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; i++) f();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; i++) f();
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms; CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps * 1000.f;  // us per launch
+}
+
+int main() {
+    const uint64_t NMAX = 1ull << 26;
+    const int W = 7;
+    std::vector<uint8_t> hb(NMAX * W + 64);
+    std::vector<uint32_t> ho(NMAX + 1);
+    for (uint64_t i = 0; i < NMAX; i++) {
+        uint64_t x = 1000000 + (i * 2654435761ull) % 9000000;
+        for (int d = W - 1; d >= 0; --d) { hb[i * W + d] = '0' + x % 10; x /= 10; }
+        ho[i] = uint32_t(i * W);
+    }
+    ho[NMAX] = uint32_t(NMAX * W);
+    uint8_t *db; uint32_t *dof, *sink;
+    CK(hipMalloc(&db, hb.size())); CK(hipMalloc(&dof, ho.size() * 4)); CK(hipMalloc(&sink, 64));
+    CK(hipMemcpy(db, hb.data(), hb.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dof, ho.data(), ho.size() * 4, hipMemcpyHostToDevice));
+    int cus = 256;
+    hipDeviceProp_t pr; CK(hipGetDeviceProperties(&pr, 0)); cus = pr.multiProcessorCount;
+    printf("CUs=%d\n", cus);
+    for (uint64_t n : {1ull << 16, 1ull << 18, 1ull << 20, 1ull << 22, 1ull << 24, 1ull << 26}) {
+        const uint64_t bytes = n * 11;
+        const uint64_t nq = bytes / 16;
+        for (int blk : {256}) {
+            for (int gmul : {4, 16, 64}) {
+                uint64_t g = std::min<uint64_t>((n + blk - 1) / blk, (uint64_t)cus * gmul);
+                float s = time_it([&] { hipLaunchKernelGGL(k_stream16, dim3(g), dim3(blk), 0, 0, (const uint4 *)db, nq, sink); }, 50);
+                float t0 = time_it([&] { hipLaunchKernelGGL(k_base<0>, dim3(g), dim3(blk), 0, 0, db, dof, n, sink); }, 50);
+                float t1 = time_it([&] { hipLaunchKernelGGL(k_base<1>, dim3(g), dim3(blk), 0, 0, db, dof, n, sink); }, 50);
+                float t2 = time_it([&] { hipLaunchKernelGGL(k_base<2>, dim3(g), dim3(blk), 0, 0, db, dof, n, sink); }, 50);
+                float t3 = time_it([&] { hipLaunchKernelGGL(k_base<3>, dim3(g), dim3(blk), 0, 0, db, dof, n, sink); }, 50);
+                printf("n=%9llu grid=%6llu  stream(11B/elt) %8.2f us (%.2f TB/s) | offs %8.2f | +bytes %8.2f | +1 hash %8.2f | +3 hash %8.2f us  (%.2f Gswipe/s)\n",
+                       (unsigned long long)n, (unsigned long long)g, s, bytes / s / 1e6, t0, t1, t2, t3, n / t3 / 1e3);
+            }
+        }
+    }
+    hipLaunchKernelGGL(k_base<0>, dim3(1), dim3(64), 0, 0, db, dof, 0, sink);
+    float e = time_it([&] { hipLaunchKernelGGL(k_base<0>, dim3(1), dim3(64), 0, 0, db, dof, 0, sink); }, 200);
+    printf("empty launch (back to back) %.2f us\n", e);
+    return 0;
+}
