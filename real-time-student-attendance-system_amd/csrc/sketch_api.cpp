@@ -40,6 +40,8 @@ struct Link {
 
 struct Filter {
     bool exists = false;
+    bool dev_ok = false;  // `dev` matches `links`
+    ChainDev dev{};       // cached kernel view of the chain (rebuilt on growth)
     std::vector<Link> links;
     uint64_t size = 0;
     uint32_t growth = 2;
@@ -182,6 +184,7 @@ int add_link(ske_ctx *c, Filter &F, uint64_t entries, double error) {
         return SKE_EHIP;
     }
     F.links.push_back(L);
+    F.dev_ok = false;
     return SKE_OK;
 }
 
@@ -208,6 +211,14 @@ ChainDev chain_dev(const Filter &F, size_t first = 0, size_t count = SIZE_MAX) {
     }
     ch.lds_bytes = lds;
     return ch;
+}
+
+const ChainDev &cached_chain(Filter &F) {
+    if (!F.dev_ok) {
+        F.dev = chain_dev(F);
+        F.dev_ok = true;
+    }
+    return F.dev;
 }
 
 LinkDev link_dev(const Link &L) {
@@ -722,10 +733,16 @@ int ske_swipes_async(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8
     if (!c || !slot) return SKE_EINVAL;
     Filter *F = get_filter(c, fid);
     if (!F) return SKE_EINVAL;
-    const ChainDev ch = F->exists ? chain_dev(*F) : ChainDev{};
-    ChainDev cha = ch;
-    cha.ablate = c->ablate;
-    HIPCHK(c, launch_swipes(0, cha, use_lds(c, ch), c->pb, bytes, offs, slot, n, c->regs,
+    static const ChainDev empty{};
+    const ChainDev &ch = F->exists ? cached_chain(*F) : empty;
+    if (c->ablate) {
+        ChainDev cha = ch;
+        cha.ablate = c->ablate;
+        HIPCHK(c, launch_swipes(0, cha, use_lds(c, ch), c->pb, bytes, offs, slot, n, c->regs,
+                                c->nslots, out_valid, (unsigned long long *)c->err, c->cus, c->st));
+        return SKE_OK;
+    }
+    HIPCHK(c, launch_swipes(0, ch, use_lds(c, ch), c->pb, bytes, offs, slot, n, c->regs,
                             c->nslots, out_valid, (unsigned long long *)c->err, c->cus, c->st));
     return SKE_OK;
 }

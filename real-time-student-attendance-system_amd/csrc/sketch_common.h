@@ -43,10 +43,11 @@ SKE_HD uint64_t mm_final(uint64_t h) {
 
 // Little-endian value of nb (1..8) bytes at p, zero padded, from aligned
 // 64-bit words only (never touches a word that holds no byte of the item).
+// (pointer arithmetic on p itself, never an integer round trip, so the load
+// stays a global_load and does not become a flat_load.)
 __device__ __forceinline__ uint64_t load_le(const uint8_t *p, uint32_t nb) {
-    uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint64_t *w = reinterpret_cast<const uint64_t *>(a & ~uintptr_t(7));
-    uint32_t off = uint32_t(a & 7);
+    const uint32_t off = uint32_t(reinterpret_cast<uintptr_t>(p) & 7);
+    const uint64_t *w = reinterpret_cast<const uint64_t *>(p - off);
     uint64_t v = w[0] >> (off * 8);
     if (off + nb > 8) v |= w[1] << (64 - off * 8);
     if (nb < 8) v &= (uint64_t(1) << (nb * 8)) - 1;
@@ -154,6 +155,29 @@ struct ProbeCursor {
         x += bm;
         if (x >= D.d) x -= D.d;
         if (carry) x = (x >= D.t) ? x - D.t : x + D.d - D.t;
+    }
+};
+
+// The same cursor with x kept in 32 bits, valid when d <= 2^31 (every Bloom
+// link up to ~2^31 bits: all configs; x + bm < 2^32 cannot overflow).  v, the
+// 64-bit running sum a + i*b, is still tracked for its carry.
+struct ProbeCursor32 {
+    uint64_t v, b;
+    uint32_t x, bm;
+    SKE_HD void init(uint64_t a, uint64_t b_, const Divisor &D) {
+        v = a;
+        b = b_;
+        x = uint32_t(fastmod(a, D));
+        bm = uint32_t(fastmod(b_, D));
+    }
+    SKE_HD void step(const Divisor &D) {
+        const uint64_t vn = v + b;
+        const bool carry = vn < v;
+        v = vn;
+        const uint32_t d = uint32_t(D.d), t = uint32_t(D.t);
+        x += bm;
+        x = x >= d ? x - d : x;
+        if (carry) x = x >= t ? x - t : x + (d - t);
     }
 };
 

@@ -24,9 +24,9 @@ namespace ske {
 // aligned 32-bit word is updated with a CAS loop; the loop starts from a
 // plain load, which may be stale but never too high (registers only grow).
 __device__ __forceinline__ bool reg_max(uint8_t *reg, uint32_t rank) {
-    uintptr_t a = reinterpret_cast<uintptr_t>(reg);
-    uint32_t *w = reinterpret_cast<uint32_t *>(a & ~uintptr_t(3));
-    const uint32_t sh = uint32_t(a & 3) * 8;
+    const uint32_t b = uint32_t(reinterpret_cast<uintptr_t>(reg) & 3);
+    uint32_t *w = reinterpret_cast<uint32_t *>(reg - b);
+    const uint32_t sh = b * 8;
     uint32_t old = *w;
     bool changed = false;
     while (((old >> sh) & 0xffu) < rank) {
@@ -45,25 +45,58 @@ enum SwipeMode { kModeSwipes = 0, kModeExists = 1, kModeStats = 2 };
 
 constexpr int kLdsBloomMax = 152 * 1024;  // LDS image budget (160 KiB per CU)
 
-// Copy every link's bit array into the LDS image (16-byte granules over the
-// 16-B padded links, 4 loads in flight per thread before the stores).
+// Copy every link's bit array into the LDS image by LDS-DMA
+// (global_load_lds_dwordx4: one wave-instruction moves 1 KiB straight into
+// LDS, no VGPR round trip), every piece of the block in flight at once; the
+// caller's __syncthreads() waits for them (vmcnt(0) + barrier).
 __device__ __forceinline__ void stage_bloom(const ChainDev &ch, uint8_t *lds) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
     for (int l = 0; l < ch.nlinks; l++) {
         const LinkDev &L = ch.link[l];
-        const uint4 *src = reinterpret_cast<const uint4 *>(L.bf);
-        uint4 *dst = reinterpret_cast<uint4 *>(lds + L.lds_off);
-        const uint32_t nq = uint32_t(((L.div.d >> 3) + 15) >> 4);
-        uint32_t q = threadIdx.x;
-        for (; q + 3 * blockDim.x < nq; q += 4 * blockDim.x) {
-            const uint4 a = src[q], b = src[q + blockDim.x], c = src[q + 2 * blockDim.x],
-                        d = src[q + 3 * blockDim.x];
-            dst[q] = a;
-            dst[q + blockDim.x] = b;
-            dst[q + 2 * blockDim.x] = c;
-            dst[q + 3 * blockDim.x] = d;
+        const uint32_t nbytes = uint32_t((((L.div.d >> 3) + 15) >> 4) << 4);  // 16-B padded link
+        for (uint32_t piece = wave; piece * 1024 < nbytes; piece += nwaves) {
+            const uint32_t off = piece * 1024 + lane * 16;
+            if (off < nbytes)
+                __builtin_amdgcn_global_load_lds(L.bf + off, lds + L.lds_off + piece * 1024, 16, 0, 0);
         }
-        for (; q < nq; q += blockDim.x) dst[q] = src[q];
     }
+}
+
+// Membership of U swipes in one link, advanced in lock step (round j issues
+// the j-th probe of every swipe still undecided); Cursor is ProbeCursor32
+// when bits <= 2^31, else the 64-bit ProbeCursor.
+template <bool kLds, int U, typename Cursor>
+__device__ __forceinline__ void link_probe(const LinkDev &L, const uint8_t *lds, const uint64_t *ha,
+                                           const uint64_t *hb, const bool *act, bool *valid,
+                                           uint32_t &probes) {
+    Cursor c[U];
+    bool alive[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        alive[u] = act[u] && !valid[u];
+        c[u].init(ha[u], hb[u], L.div);
+    }
+    for (uint32_t j = 0; j < L.k; j++) {
+        uint8_t byte[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t x = c[u].x;
+            byte[u] = alive[u] ? (kLds ? lds[L.lds_off + uint32_t(x >> 3)] : L.bf[x >> 3]) : uint8_t(0);
+        }
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (alive[u]) {
+                probes++;
+                alive[u] = (byte[u] >> (c[u].x & 7)) & 1;
+                c[u].step(L.div);
+                any |= alive[u];
+            }
+        }
+        if (!any) break;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) valid[u] |= alive[u];
 }
 
 // K1, tiled: every thread owns U swipes of a tile (swipe base + u*T + tid,
@@ -118,69 +151,47 @@ __global__ void __launch_bounds__(kLds ? 1024 : 256)
             ha[u] = murmur_item(it[u], kBloomSeed);
             hb[u] = murmur_item(it[u], ha[u]);
         }
+        // HLL half, issued before the probes so its register pre-check loads
+        // fly while the Bloom is tested (a swipe found invalid later simply
+        // discards them).  hllPatLen -> (register, rank).
+        uint8_t *reg[U];
+        uint32_t rank[U], cur[U];
+        if constexpr (kMode == kModeSwipes) {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                reg[u] = nullptr;
+                rank[u] = 0;
+                cur[u] = 0xffu;
+                if (do_hll && act[u] && sl[u] < nslots) {
+                    uint32_t idx;
+                    hll_patlen(murmur_item(it[u], kHllSeed), idx, rank[u]);
+                    reg[u] = regs + size_t(sl[u]) * kHllRegs + idx;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) cur[u] = reg[u] ? *reg[u] : 0xffu;
+        }
         bool valid[U];
 #pragma unroll
         for (int u = 0; u < U; u++) valid[u] = ablate_probe && act[u];
         if (!ablate_probe) {
             for (int l = ch.nlinks - 1; l >= 0; --l) {
                 const LinkDev &L = ch.link[l];
-                ProbeCursor c[U];
-                bool alive[U];
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    alive[u] = act[u] && !valid[u];
-                    c[u].init(ha[u], hb[u], L.div);
-                }
-                for (uint32_t j = 0; j < L.k; j++) {
-                    uint8_t byte[U];
-#pragma unroll
-                    for (int u = 0; u < U; u++) {
-                        const uint64_t x = c[u].x;
-                        byte[u] = alive[u] ? (kLds ? lds_img[L.lds_off + uint32_t(x >> 3)]
-                                                   : L.bf[x >> 3])
-                                           : uint8_t(0);
-                    }
-                    bool any = false;
-#pragma unroll
-                    for (int u = 0; u < U; u++) {
-                        if (alive[u]) {
-                            probes++;
-                            alive[u] = (byte[u] >> (c[u].x & 7)) & 1;
-                            c[u].step(L.div);
-                            any |= alive[u];
-                        }
-                    }
-                    if (!any) break;
-                }
-#pragma unroll
-                for (int u = 0; u < U; u++) valid[u] |= alive[u];
+                if (L.div.d <= (uint64_t(1) << 31))
+                    link_probe<kLds, U, ProbeCursor32>(L, lds_img, ha, hb, act, valid, probes);
+                else
+                    link_probe<kLds, U, ProbeCursor>(L, lds_img, ha, hb, act, valid, probes);
             }
         }
         if constexpr (kMode == kModeSwipes) {
             if (do_hll) {
-                uint8_t *reg[U];
-                uint32_t rank[U], cur[U];
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    reg[u] = nullptr;
-                    rank[u] = 0;
-                    if (valid[u]) {
-                        if (sl[u] < nslots) {
-                            uint32_t idx;
-                            hll_patlen(murmur_item(it[u], kHllSeed), idx, rank[u]);
-                            reg[u] = regs + size_t(sl[u]) * kHllRegs + idx;
-                        } else {
-                            atomicOr(reinterpret_cast<unsigned int *>(stats), 1u);
-                        }
-                    }
-                }
-                // pre-check loads of all U registers in flight together; a
-                // stale value is never too high (registers only grow)
-#pragma unroll
-                for (int u = 0; u < U; u++) cur[u] = reg[u] ? *reg[u] : 0xffu;
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    if (cur[u] < rank[u]) {
+                    if (!valid[u]) continue;
+                    if (sl[u] >= nslots) {
+                        atomicOr(reinterpret_cast<unsigned int *>(stats), 1u);
+                    } else if (cur[u] < rank[u]) {
+                        // the pre-check may be stale but is never too high
                         if (ch.ablate & kAblateCas) {
                             if (out) out[base + uint64_t(u) * T + tid] = 2;
                         } else {

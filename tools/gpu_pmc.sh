@@ -1,20 +1,16 @@
 #!/bin/bash
-# GPU session: K1 ablations + PMC counter passes (one counter group per pass).
-mkdir -p gpurun_out/pmc
+# PMC passes (one counter group per rocprofv3 run, --pmc only) over the
+# default bench; summary of K1 into gpurun_out/pmc_<tag>.json.
+# usage: TAG=r01 BENCH_ARGS="..." bash tools/gpu_pmc.sh
+mkdir -p gpurun_out/pmc_$TAG
 export TMPDIR=/tmp
-summ() { python -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['config']['k1_variant'])"; }
-for a in 0 1 2 3 4; do
-  for v in 1 0; do
-    timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu --ablate $a --variant $v > gpurun_out/abl.log 2>&1; rc=$?
-    if [ $rc -ne 0 ]; then tail -5 gpurun_out/abl.log; exit $rc; fi
-    echo -n "ablate=$a variant=$v: "; summ gpurun_out/abl.log
-  done
-done
-timeout -k 10 120 rocprofv3 -L > gpurun_out/pmc/counters.txt 2>&1
-for c in FETCH_SIZE WRITE_SIZE "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES" "TCC_EA0_ATOMIC_sum" ; do
+GROUPS_=("FETCH_SIZE" "WRITE_SIZE" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum"
+ "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS"
+ "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES" "SQ_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT")
+for c in "${GROUPS_[@]}"; do
   tag=$(echo $c | tr ' ' '_')
-  timeout -k 10 300 rocprofv3 --pmc $c -d gpurun_out/pmc/$tag -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/pmc/$tag.log 2>&1; rc=$?
-  echo "pmc $c rc=$rc"
-  if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc/$tag.log; fi
+  timeout -k 10 300 rocprofv3 --pmc $c -d gpurun_out/pmc_$TAG/$tag -o run --output-format csv -- python bench.py --steps 12 --warmup 3 --no-cpu $BENCH_ARGS > gpurun_out/pmc_$TAG/$tag.log 2>&1; rc=$?
+  echo "pmc [$c] rc=$rc"
+  if [ $rc -ne 0 ]; then tail -3 gpurun_out/pmc_$TAG/$tag.log; fi
 done
-exit 0
+python tools/pmc_summary.py gpurun_out/pmc_$TAG "k_swipes<0" gpurun_out/pmc_$TAG.json 3 > /dev/null && echo "summary written"

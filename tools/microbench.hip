@@ -69,7 +69,8 @@ int main() {
     hipDeviceProp_t pr; CK(hipGetDeviceProperties(&pr, 0)); cus = pr.multiProcessorCount;
     printf("CUs=%d\n", cus);
     for (uint64_t n : {1ull << 16, 1ull << 18, 1ull << 20, 1ull << 22, 1ull << 24, 1ull << 26}) {
-        const uint64_t bytes = n * 11;
+        // stream over a prefix of the id buffer: never past its allocation
+        const uint64_t bytes = std::min<uint64_t>(n * 11, NMAX * W);
         const uint64_t nq = bytes / 16;
         for (int blk : {256}) {
             for (int gmul : {4, 16, 64}) {
