@@ -39,6 +39,7 @@ import numpy as np
 from . import _lib
 from ._lib import (BfInfo, BfLink, Context, SketchLibError, SKE_MEM_DEVICE, SKE_MEM_HOST,
                    HLL_DENSE_BYTES, HLL_REGISTERS)
+from . import formats
 from .encoding import encode, pack
 from .exceptions import DataError, ResponseError, WRONGTYPE
 
@@ -417,6 +418,22 @@ class SketchClient:
             raise DataError("expected 16384 registers")
         self.ctx.call("ske_hll_import_raw", self.keys.slot[k], _ptr(r))
 
+    def dump_hll(self, name) -> bytes | None:
+        """The key as Redis stores it (GET of an HLL key): "HYLL" header +
+        canonical sparse or dense payload (formats.encode_hll)."""
+        k = encode(name)
+        if not self.keys.expect(k, "hll"):
+            return None
+        return formats.encode_hll(self.hll_registers(k))
+
+    def load_hll(self, name, value: bytes) -> None:
+        """SET of a Redis HLL string (dense or sparse) into a key."""
+        regs = formats.decode_hll(bytes(value))
+        k = encode(name)
+        if k in self.keys.kind and self.keys.kind[k] != "hll":
+            self.keys.drop(k)  # SET replaces a key of any type
+        self.hll_load_registers(k, regs)
+
     def key_slot(self, name, create: bool = True) -> int:
         """Slot of an HLL key (creating it when asked) for batched calls."""
         k = encode(name)
@@ -545,6 +562,16 @@ class SketchClient:
         if cmd == "PFMERGE":
             need(1)
             self.pfmerge(*a)
+            return self._ok()
+        if cmd == "GET":
+            need(1, 1)
+            k = encode(a[0])
+            if self.keys.type_of(k) == "bf":
+                raise ResponseError(WRONGTYPE)
+            return self.dump_hll(k)
+        if cmd == "SET":
+            need(2, 2)
+            self.load_hll(a[0], encode(a[1]))
             return self._ok()
         if cmd in ("DEL", "UNLINK"):
             need(1)

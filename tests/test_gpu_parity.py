@@ -356,3 +356,18 @@ def test_empty_and_single(client):
     assert client.swipes("bf", "hll:a", []).size == 0
     assert client.swipes("bf", "hll:a", [5]).tolist() == [True]
     assert client.pfcount("hll:a") == 1
+
+
+def test_hll_get_set_interop(client, orc):
+    """GET of an HLL key gives a Redis HYLL string the oracle decodes to the
+    same registers; SET of that string into another key reproduces them."""
+    vals = list(range(50000, 52000))
+    client.pfadd("hll:a", *vals)
+    s = client.execute_command("GET", "hll:a")
+    regs = orc.hll_decode_string(s)
+    h = orc.HLL()
+    h.add(*[str(v).encode() for v in vals])
+    assert np.array_equal(regs, h.regs)
+    assert client.execute_command("SET", "hll:b", s) == "OK"
+    assert np.array_equal(client.hll_registers("hll:b"), h.regs)
+    assert client.pfcount("hll:b") == h.count()
