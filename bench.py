@@ -89,8 +89,9 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    w = synthetic.WORKLOADS[args.config]
-    n = args.batch or w.n_swipes
+    w_all = synthetic.WORKLOADS[args.config]
+    w = synthetic.shard(w_all, world)
+    n = args.batch or w.step_swipes
     engine = SketchEngine(local)
     # a dedicated (non-null) stream shared by libsketch and the timing events
     stream = torch.cuda.Stream()
@@ -152,6 +153,16 @@ def main():
     # u32 offset + u32 slot + u8 answer), one 64-B sector per RedisBloom probe
     # (sequential count, measured), one 64-B sector read + write per PFADD
     s_io = width + 4 + 4 + 1
+    # HBM-side bytes per K1 dispatch from the committed rocprofv3 PMC passes of
+    # this same command (FETCH_SIZE + WRITE_SIZE, separate passes; see
+    # profiles/README.md), or null when no summary exists for this workload
+    traffic, traffic_src = None, None
+    pmc_path = os.path.join(ROOT, "profiles", f"k1_pmc_{args.config}.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            pmc = json.load(f)
+        traffic = pmc.get("hbm_bytes_per_dispatch")
+        traffic_src = os.path.relpath(pmc_path, ROOT)
     alg_bytes = n * s_io + 64 * probes + 128 * nvalid
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     line = {
@@ -168,13 +179,15 @@ def main():
         "dtype": "u64",
         "data": "synthetic (device counter-based generator, seed %d)" % w.seed,
         "config": {"workload": w.name, "swipes_per_step": n, "students": w.n_members,
+                   "hll_keys_total": w_all.n_keys,
                    "hll_keys_per_gpu": w.n_keys, "invalid_frac": w.invalid_frac,
                    "bloom": {"error": w.bf_error, "capacity": w.bf_capacity},
                    "id_bytes": width, "parallelism": f"dp{world} (key-sharded, Bloom replicated)",
                    "k1_variant": "lds-bloom" if engine.variant(0) else "global-bloom",
                    "tile": args.tile or 4},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel": "k_swipes", "kernel_ms": kern_ms,
                      "alg_bytes_per_swipe": alg_bytes / n,
                      "probes_per_swipe": probes / n, "valid_frac": nvalid / n},

@@ -85,6 +85,18 @@ __device__ __forceinline__ uint64_t murmur_item(const Item &it, uint64_t seed) {
     return mm_final(h);
 }
 
+// MurmurHash64A of an item of at most 8 bytes held in w (zero padded).
+SKE_HD uint64_t murmur_short(uint64_t w, uint32_t len, uint64_t seed) {
+    uint64_t h = seed ^ (uint64_t(len) * kMurmurM);
+    if (len == 8) {
+        h = mm_block(h, w);
+    } else if (len) {
+        h ^= w;
+        h *= kMurmurM;
+    }
+    return mm_final(h);
+}
+
 // hllPatLen(): index = low 14 bits, count = 1 + trailing zeros of
 // (hash >> 14) | 1<<50, in [1, 51].
 SKE_HD void hll_patlen(uint64_t hash, uint32_t &idx, uint32_t &rank) {
@@ -158,6 +170,8 @@ struct ProbeCursor {
     }
 };
 
+SKE_HD uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }  // v_min_u32
+
 // The same cursor with x kept in 32 bits, valid when d <= 2^31 (every Bloom
 // link up to ~2^31 bits: all configs; x + bm < 2^32 cannot overflow).  v, the
 // 64-bit running sum a + i*b, is still tracked for its carry.
@@ -170,14 +184,18 @@ struct ProbeCursor32 {
         x = uint32_t(fastmod(a, D));
         bm = uint32_t(fastmod(b_, D));
     }
-    SKE_HD void step(const Divisor &D) {
+    SKE_HD void step(const Divisor &D) { step(uint32_t(D.d), uint32_t(D.t)); }
+    // x, bm < d <= 2^31: "x = min(x, x - d)" is the conditional subtract (a
+    // wrapped x - d is the larger one); the wrap of v subtracts t = 2^64 mod d,
+    // and "min(x, x + d)" undoes an underflow the same way.
+    SKE_HD void step(uint32_t d, uint32_t t) {
         const uint64_t vn = v + b;
-        const bool carry = vn < v;
+        const uint32_t tsel = vn < v ? t : 0u;
         v = vn;
-        const uint32_t d = uint32_t(D.d), t = uint32_t(D.t);
         x += bm;
-        x = x >= d ? x - d : x;
-        if (carry) x = x >= t ? x - t : x + (d - t);
+        x = umin32(x, x - d);
+        x -= tsel;
+        x = umin32(x, x + d);
     }
 };
 

@@ -65,6 +65,40 @@ __device__ __forceinline__ void stage_bloom(const ChainDev &ch, uint8_t *lds) {
 // Membership of U swipes in one link, advanced in lock step (round j issues
 // the j-th probe of every swipe still undecided); Cursor is ProbeCursor32
 // when bits <= 2^31, else the 64-bit ProbeCursor.
+// LDS image, bits <= 2^31: branch-free rounds.  Every swipe of the tile reads
+// its byte each round (a decided swipe re-reads a valid address and ignores
+// it); the loop exit is wave-uniform (no lane has an undecided swipe left).
+template <int U>
+__device__ __forceinline__ void link_probe_lds32(const LinkDev &L, const uint8_t *lds,
+                                                 const uint64_t *ha, const uint64_t *hb,
+                                                 const bool *act, bool *valid, uint32_t &probes) {
+    const uint32_t d = uint32_t(L.div.d), t = uint32_t(L.div.t);
+    const uint8_t *img = lds + L.lds_off;
+    ProbeCursor32 c[U];
+    bool alive[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        alive[u] = act[u] && !valid[u];
+        c[u].init(ha[u], hb[u], L.div);
+    }
+    for (uint32_t j = 0; j < L.k; j++) {
+        uint32_t byte[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) byte[u] = img[c[u].x >> 3];
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            probes += alive[u];
+            alive[u] = alive[u] && ((byte[u] >> (c[u].x & 7)) & 1);
+            any |= alive[u];
+            c[u].step(d, t);
+        }
+        if (!__any(any)) break;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) valid[u] |= alive[u];
+}
+
 template <bool kLds, int U, typename Cursor>
 __device__ __forceinline__ void link_probe(const LinkDev &L, const uint8_t *lds, const uint64_t *ha,
                                            const uint64_t *hb, const bool *act, bool *valid,
@@ -145,11 +179,27 @@ __global__ void __launch_bounds__(kLds ? 1024 : 256)
             __syncthreads();
             staged = true;
         }
-        uint64_t ha[U], hb[U];
+        // ids of at most 8 bytes (every config's decimal student id) take the
+        // short MurmurHash64A path, chosen per wave
+        bool short_ids = true;
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            ha[u] = murmur_item(it[u], kBloomSeed);
-            hb[u] = murmur_item(it[u], ha[u]);
+        for (int u = 0; u < U; u++) short_ids &= it[u].len <= 8;
+        short_ids = __all(short_ids);
+        uint64_t ha[U], hb[U], hh[U];
+        if (short_ids) {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                ha[u] = murmur_short(it[u].w0, it[u].len, kBloomSeed);
+                hh[u] = murmur_short(it[u].w0, it[u].len, kHllSeed);
+                hb[u] = murmur_short(it[u].w0, it[u].len, ha[u]);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                ha[u] = murmur_item(it[u], kBloomSeed);
+                hh[u] = murmur_item(it[u], kHllSeed);
+                hb[u] = murmur_item(it[u], ha[u]);
+            }
         }
         // HLL half, issued before the probes so its register pre-check loads
         // fly while the Bloom is tested (a swipe found invalid later simply
@@ -164,7 +214,7 @@ __global__ void __launch_bounds__(kLds ? 1024 : 256)
                 cur[u] = 0xffu;
                 if (do_hll && act[u] && sl[u] < nslots) {
                     uint32_t idx;
-                    hll_patlen(murmur_item(it[u], kHllSeed), idx, rank[u]);
+                    hll_patlen(hh[u], idx, rank[u]);
                     reg[u] = regs + size_t(sl[u]) * kHllRegs + idx;
                 }
             }
@@ -177,7 +227,9 @@ __global__ void __launch_bounds__(kLds ? 1024 : 256)
         if (!ablate_probe) {
             for (int l = ch.nlinks - 1; l >= 0; --l) {
                 const LinkDev &L = ch.link[l];
-                if (L.div.d <= (uint64_t(1) << 31))
+                if (kLds && L.div.d <= (uint64_t(1) << 31))
+                    link_probe_lds32<U>(L, lds_img, ha, hb, act, valid, probes);
+                else if (L.div.d <= (uint64_t(1) << 31))
                     link_probe<kLds, U, ProbeCursor32>(L, lds_img, ha, hb, act, valid, probes);
                 else
                     link_probe<kLds, U, ProbeCursor>(L, lds_img, ha, hb, act, valid, probes);

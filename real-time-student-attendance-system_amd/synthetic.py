@@ -46,6 +46,7 @@ class Workload:
     zipf_days: int = 0
     zipf_s: float = 1.1
     gpus: int = 1
+    step_swipes: int = 1_000_000     # swipes per benchmark step (one K1 launch)
     seed: int = SEED
     notes: str = ""
     extra: dict = field(default_factory=dict)
@@ -61,14 +62,31 @@ WORKLOADS = {
                    1_000_000, 50, 0.10),
     # C3: 1B swipes, 10M students (0.001), 100k lecture-day keys (Zipf lectures)
     "c3": Workload("c3-1B-10M-100kkeys", 0.001, 10_000_000, 10_000_000, 100_000_000, 10_000_000,
-                   1_000_000_000, 100_000, 0.10, zipf_lectures=1000, zipf_days=100, gpus=8),
+                   1_000_000_000, 100_000, 0.10, zipf_lectures=1000, zipf_days=100, gpus=8,
+                   step_swipes=16_000_000),
     # C4: adversarial, 50% invalid of which half near-collisions
     "c4": Workload("c4-adversarial", 0.01, 100_000, 1_000_000, 10_000_000, 100_000, 1_000_000, 50,
                    0.50, near_frac=0.5),
     # C5: campus-year rollup 365 days x 5000 lectures
     "c5": Workload("c5-campus-year", 0.001, 10_000_000, 10_000_000, 100_000_000, 10_000_000,
-                   1_000_000_000, 365 * 5000, 0.10, zipf_lectures=5000, zipf_days=365, gpus=8),
+                   1_000_000_000, 365 * 5000, 0.10, zipf_lectures=5000, zipf_days=365, gpus=8,
+                   step_swipes=16_000_000),
 }
+
+
+def shard(w: Workload, world: int) -> Workload:
+    """This rank's share of a multi-GPU workload: the key space split over
+    `world` owners (keys are routed to their owner at ingest), swipes per step
+    unchanged (weak scaling).  Zipf lectures are split the same way."""
+    if world <= 1:
+        return w
+    d = dict(w.__dict__)
+    if w.zipf_lectures:
+        d["zipf_lectures"] = max(1, w.zipf_lectures // world)
+        d["n_keys"] = d["zipf_lectures"] * w.zipf_days
+    else:
+        d["n_keys"] = max(1, -(-w.n_keys // world))
+    return Workload(**d)
 
 
 def _coprime_mul(R: int, seed: int) -> int:

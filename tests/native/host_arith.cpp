@@ -12,6 +12,7 @@ static uint64_t rnd() { s = ske::splitmix_fin(s + 0x9e3779b97f4a7c15ULL); return
 
 int main() {
     std::vector<uint64_t> divs = {64, 128, 1152, 2496, 5568, 12288, 1102784, 158202880,
+                                  (1ULL << 31), (1ULL << 31) - 64, 3019840,
                                   (1ULL << 32), (1ULL << 32) + 64, 3ULL << 40, (1ULL << 62) + 64};
     for (int i = 0; i < 200; i++) divs.push_back(64 * (1 + rnd() % (1ULL << 30)));
     for (int i = 0; i < 50; i++) divs.push_back(2 + rnd() % (1ULL << 61));
@@ -42,6 +43,18 @@ int main() {
                     break;
                 }
                 c.step(D);
+            }
+            if (d <= (1ULL << 31)) {  // the 32-bit cursor of the LDS / small-filter path
+                ske::ProbeCursor32 c32;
+                c32.init(a, b, D);
+                for (uint64_t i = 0; i < 40; i++) {
+                    checks++;
+                    if (c32.x != (a + i * b) % d) {
+                        if (bad++ < 5) printf("cursor32 mismatch d=%llu i=%llu\n", (unsigned long long)d, (unsigned long long)i);
+                        break;
+                    }
+                    c32.step(D);
+                }
             }
         }
     }
