@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--variant", type=int, default=-1, help="-1 auto, 0 global Bloom, 1 LDS Bloom")
     ap.add_argument("--max-batches", type=int, default=64)
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: K1 parts removed (bits)")
+    ap.add_argument("--layout", default="offsets", choices=["offsets", "fixed"],
+                    help="id batch layout: bytes + u32 offsets, or fixed-width ids")
     return ap.parse_args()
 
 
@@ -117,8 +119,13 @@ def main():
     probes, nvalid = engine.swipes_stats(0, batches[0])
     width = len(str(w.id_hi - 1))
 
+    fixed = args.layout == "fixed"
+
     def step(j):
-        engine.swipes_async(0, batches[j % nb])
+        if fixed:
+            engine.swipes_fixed_async(0, batches[j % nb])
+        else:
+            engine.swipes_async(0, batches[j % nb])
 
     for j in range(args.warmup):
         step(j)
@@ -152,7 +159,7 @@ def main():
     # algorithmic bytes per launch: S_io per swipe (id bytes +
     # u32 offset + u32 slot + u8 answer), one 64-B sector per RedisBloom probe
     # (sequential count, measured), one 64-B sector read + write per PFADD
-    s_io = width + 4 + 4 + 1
+    s_io = width + (0 if fixed else 4) + 4 + 1
     # HBM-side bytes per K1 dispatch from the committed rocprofv3 PMC passes of
     # this same command (FETCH_SIZE + WRITE_SIZE, separate passes; see
     # profiles/README.md), or null when no summary exists for this workload
@@ -184,7 +191,7 @@ def main():
                    "bloom": {"error": w.bf_error, "capacity": w.bf_capacity},
                    "id_bytes": width, "parallelism": f"dp{world} (key-sharded, Bloom replicated)",
                    "k1_variant": "lds-bloom" if engine.variant(0) else "global-bloom",
-                   "tile": args.tile or 4},
+                   "tile": args.tile or 2, "layout": args.layout},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src,

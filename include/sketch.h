@@ -175,6 +175,13 @@ int ske_swipes(ske_ctx *ctx, uint32_t fid, const uint32_t *slot, const uint8_t *
 /* device-pointer form that only enqueues (no sync); for the benchmark */
 int ske_swipes_async(ske_ctx *ctx, uint32_t fid, const uint32_t *slot, const uint8_t *bytes,
                      const uint32_t *offs, uint64_t n, uint8_t *out_valid);
+/* fixed-width form: id i is the `width` bytes at bytes + i*width (no offset
+ * array -- e.g. fixed-digit student ids, which every config uses).  Same
+ * semantics as ske_swipes; the id load needs no offset load first. */
+int ske_swipes_fixed(ske_ctx *ctx, uint32_t fid, const uint32_t *slot, const uint8_t *bytes,
+                     uint32_t width, uint64_t n, uint8_t *out_valid, int mem);
+int ske_swipes_fixed_async(ske_ctx *ctx, uint32_t fid, const uint32_t *slot,
+                           const uint8_t *bytes, uint32_t width, uint64_t n, uint8_t *out_valid);
 /* probe statistics of the same swipes (untimed): Bloom bit tests performed
  * and valid count, to price the algorithmic bytes of the roofline. */
 int ske_swipes_stats(ske_ctx *ctx, uint32_t fid, const uint8_t *bytes, const uint32_t *offs,

@@ -100,6 +100,10 @@ SIGNATURES = {
     "ske_hll_count_raw_dev": (C.c_int, [_CTX, _u8p, C.c_uint32, _u64p]),
     "ske_swipes": (C.c_int, [_CTX, C.c_uint32, _u32p, _u8p, _u32p, C.c_uint64, _u8p, C.c_int]),
     "ske_swipes_async": (C.c_int, [_CTX, C.c_uint32, _u32p, _u8p, _u32p, C.c_uint64, _u8p]),
+    "ske_swipes_fixed": (C.c_int, [_CTX, C.c_uint32, _u32p, _u8p, C.c_uint32, C.c_uint64, _u8p,
+                                   C.c_int]),
+    "ske_swipes_fixed_async": (C.c_int, [_CTX, C.c_uint32, _u32p, _u8p, C.c_uint32, C.c_uint64,
+                                         _u8p]),
     "ske_swipes_stats": (C.c_int, [_CTX, C.c_uint32, _u8p, _u32p, C.c_uint64,
                                    C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "ske_swipes_variant": (C.c_int, [_CTX, C.c_uint32]),

@@ -70,7 +70,7 @@ struct ske_ctx {
     size_t stg_cap[8] = {};
     unsigned int *err = nullptr;
     unsigned long long *stats = nullptr;
-    int pb = 4;           // K1 tile: swipes per thread in flight (1, 2, 4, 8)
+    int pb = 2;           // K1 tile: swipes per thread in flight (1, 2, 4, 8)
     int variant = -1;     // -1 auto, 0 global, 1 LDS
     uint32_t ablate = 0;  // diagnostic only (kAblate* bits)
     bool lds_ok = false;
@@ -541,7 +541,7 @@ int ske_bf_mexists(ske_ctx *c, uint32_t fid, const uint8_t *bytes, const uint32_
         if (rc) return rc;
     }
     const ChainDev ch = chain_dev(*F);
-    HIPCHK(c, launch_swipes(1, ch, use_lds(c, ch), c->pb, s.bytes, s.offs, nullptr, n, nullptr, 0,
+    HIPCHK(c, launch_swipes(1, ch, use_lds(c, ch), c->pb, s.bytes, s.offs, 0, nullptr, n, nullptr, 0,
                             dout, nullptr, c->cus, c->st));
     if (mem != SKE_MEM_DEVICE) HIPCHK(c, hipMemcpyAsync(out, dout, n, hipMemcpyDeviceToHost, c->st));
     HIPCHK(c, hipStreamSynchronize(c->st));
@@ -721,7 +721,7 @@ int ske_swipes(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *by
     }
     HIPCHK(c, hipMemsetAsync(c->err, 0, 4, c->st));
     const ChainDev ch = F->exists ? chain_dev(*F) : ChainDev{};
-    HIPCHK(c, launch_swipes(0, ch, use_lds(c, ch), c->pb, s.bytes, s.offs, dslot, n, c->regs,
+    HIPCHK(c, launch_swipes(0, ch, use_lds(c, ch), c->pb, s.bytes, s.offs, 0, dslot, n, c->regs,
                             c->nslots, dout, (unsigned long long *)c->err, c->cus, c->st));
     if (out_valid && mem != SKE_MEM_DEVICE)
         HIPCHK(c, hipMemcpyAsync(out_valid, dout, n, hipMemcpyDeviceToHost, c->st));
@@ -738,13 +738,55 @@ int ske_swipes_async(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8
     if (c->ablate) {
         ChainDev cha = ch;
         cha.ablate = c->ablate;
-        HIPCHK(c, launch_swipes(0, cha, use_lds(c, ch), c->pb, bytes, offs, slot, n, c->regs,
+        HIPCHK(c, launch_swipes(0, cha, use_lds(c, ch), c->pb, bytes, offs, 0, slot, n, c->regs,
                                 c->nslots, out_valid, (unsigned long long *)c->err, c->cus, c->st));
         return SKE_OK;
     }
-    HIPCHK(c, launch_swipes(0, ch, use_lds(c, ch), c->pb, bytes, offs, slot, n, c->regs,
+    HIPCHK(c, launch_swipes(0, ch, use_lds(c, ch), c->pb, bytes, offs, 0, slot, n, c->regs,
                             c->nslots, out_valid, (unsigned long long *)c->err, c->cus, c->st));
     return SKE_OK;
+}
+
+int ske_swipes_fixed_async(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *bytes,
+                           uint32_t width, uint64_t n, uint8_t *out_valid) {
+    if (!c || !slot || width == 0 || width > 4096) return SKE_EINVAL;
+    Filter *F = get_filter(c, fid);
+    if (!F) return SKE_EINVAL;
+    static const ChainDev empty{};
+    const ChainDev &ch = F->exists ? cached_chain(*F) : empty;
+    HIPCHK(c, launch_swipes(0, ch, use_lds(c, ch), c->pb, bytes, nullptr, width, slot, n, c->regs,
+                            c->nslots, out_valid, (unsigned long long *)c->err, c->cus, c->st));
+    return SKE_OK;
+}
+
+int ske_swipes_fixed(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *bytes,
+                     uint32_t width, uint64_t n, uint8_t *out_valid, int mem) {
+    if (!c || !slot || width == 0 || width > 4096) return SKE_EINVAL;
+    Filter *F = get_filter(c, fid);
+    if (!F) return SKE_EINVAL;
+    if (n == 0) return SKE_OK;
+    int rc = SKE_OK;
+    const uint8_t *db = bytes;
+    const uint32_t *dslot = slot;
+    uint8_t *dout = out_valid;
+    if (mem != SKE_MEM_DEVICE) {
+        uint8_t *b = (uint8_t *)stage_buf(c, 0, n * width + 16, &rc);
+        if (rc) return rc;
+        HIPCHK(c, hipMemcpyAsync(b, bytes, n * width, hipMemcpyHostToDevice, c->st));
+        db = b;
+        rc = stage_u32(c, slot, n, mem, 2, &dslot);
+        if (rc) return rc;
+        if (out_valid) {
+            dout = (uint8_t *)stage_buf(c, 3, n, &rc);
+            if (rc) return rc;
+        }
+    }
+    HIPCHK(c, hipMemsetAsync(c->err, 0, 4, c->st));
+    rc = ske_swipes_fixed_async(c, fid, dslot, db, width, n, dout);
+    if (rc) return rc;
+    if (out_valid && mem != SKE_MEM_DEVICE)
+        HIPCHK(c, hipMemcpyAsync(out_valid, dout, n, hipMemcpyDeviceToHost, c->st));
+    return check_err_flag(c, SKE_ERANGE);
 }
 
 int ske_swipes_stats(ske_ctx *c, uint32_t fid, const uint8_t *bytes, const uint32_t *offs,
@@ -756,7 +798,7 @@ int ske_swipes_stats(ske_ctx *c, uint32_t fid, const uint8_t *bytes, const uint3
     HIPCHK(c, hipMemsetAsync(c->stats, 0, 16, c->st));
     // every tile size follows RedisBloom's per-swipe probe order, so the
     // count is the sequential one
-    HIPCHK(c, launch_swipes(2, ch, use_lds(c, ch), c->pb, bytes, offs, nullptr, n, nullptr, 0, nullptr,
+    HIPCHK(c, launch_swipes(2, ch, use_lds(c, ch), c->pb, bytes, offs, 0, nullptr, n, nullptr, 0, nullptr,
                             c->stats, c->cus, c->st));
     unsigned long long h[2] = {0, 0};
     HIPCHK(c, hipMemcpyAsync(h, c->stats, 16, hipMemcpyDeviceToHost, c->st));

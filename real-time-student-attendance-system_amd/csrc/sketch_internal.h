@@ -5,8 +5,9 @@
 namespace ske {
 
 // sketch_kernels.hip
-hipError_t launch_swipes(int mode, const ChainDev &ch, bool lds, int pb, const uint8_t *bytes,
-                         const uint32_t *offs, const uint32_t *slot, uint64_t n, uint8_t *regs,
+hipError_t launch_swipes(int mode, const ChainDev &ch, bool lds, int tile, const uint8_t *bytes,
+                         const uint32_t *offs, uint32_t fixed_w, const uint32_t *slot, uint64_t n,
+                         uint8_t *regs,
                          uint32_t nslots, uint8_t *out, unsigned long long *stats, int cus,
                          hipStream_t st);
 hipError_t lds_bloom_setup();

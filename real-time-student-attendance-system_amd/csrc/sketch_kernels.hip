@@ -145,9 +145,11 @@ __device__ __forceinline__ void link_probe(const LinkDev &L, const uint8_t *lds,
 template <int kMode, bool kLds, int U>
 __global__ void __launch_bounds__(kLds ? 1024 : 256)
     k_swipes(const ChainDev ch, const uint8_t *__restrict__ bytes,
-             const uint32_t *__restrict__ offs, const uint32_t *__restrict__ slot, uint64_t n,
-             uint8_t *__restrict__ regs, uint32_t nslots, uint8_t *__restrict__ out,
-             unsigned long long *__restrict__ stats) {
+             const uint32_t *__restrict__ offs, uint32_t fixed_w,
+             const uint32_t *__restrict__ slot, uint64_t n, uint8_t *__restrict__ regs,
+             uint32_t nslots, uint8_t *__restrict__ out, unsigned long long *__restrict__ stats) {
+    // fixed_w > 0: ids are packed at a fixed width (id i at bytes + i*fixed_w,
+    // offs unused) -- the id load then needs no offset load first
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_img[];
     const uint32_t T = blockDim.x, tid = threadIdx.x;
     const uint64_t per_block = (n + gridDim.x - 1) / gridDim.x;
@@ -169,7 +171,8 @@ __global__ void __launch_bounds__(kLds ? 1024 : 256)
             it[u].len = 0;
             sl[u] = 0;
             if (act[u]) {
-                const uint32_t b = offs[i], e = offs[i + 1];
+                const uint64_t b = fixed_w ? i * fixed_w : offs[i];
+                const uint64_t e = fixed_w ? b + fixed_w : offs[i + 1];
                 it[u] = load_item(bytes, b, e);
                 if (do_hll) sl[u] = slot[i];
             }
@@ -507,35 +510,35 @@ static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
 
 template <int kMode, int U>
 static hipError_t launch_swipes_u(const ChainDev &ch, bool lds, const uint8_t *bytes,
-                                  const uint32_t *offs, const uint32_t *slot, uint64_t n,
+                                  const uint32_t *offs, uint32_t fixed_w, const uint32_t *slot, uint64_t n,
                                   uint8_t *regs, uint32_t nslots, uint8_t *out,
                                   unsigned long long *stats, int cus, hipStream_t st) {
     if (lds) {
         // one 1024-thread block per CU (the LDS image caps residency at one)
         const unsigned grid = grid_for(n, 1024 * U, unsigned(cus));
         hipLaunchKernelGGL((k_swipes<kMode, true, U>), dim3(grid), dim3(1024), ch.lds_bytes, st, ch,
-                           bytes, offs, slot, n, regs, nslots, out, stats);
+                           bytes, offs, fixed_w, slot, n, regs, nslots, out, stats);
     } else {
         const unsigned grid = grid_for(n, 256 * U, unsigned(cus) * 8);
         hipLaunchKernelGGL((k_swipes<kMode, false, U>), dim3(grid), dim3(256), 0, st, ch, bytes,
-                           offs, slot, n, regs, nslots, out, stats);
+                           offs, fixed_w, slot, n, regs, nslots, out, stats);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_swipes(int mode, const ChainDev &ch, bool lds, int tile, const uint8_t *bytes,
-                         const uint32_t *offs, const uint32_t *slot, uint64_t n, uint8_t *regs,
+                         const uint32_t *offs, uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *regs,
                          uint32_t nslots, uint8_t *out, unsigned long long *stats, int cus,
                          hipStream_t st) {
     if (n == 0) return hipSuccess;
 #define SKE_U(UU)                                                                                  \
     if (mode == kModeSwipes)                                                                       \
-        return launch_swipes_u<kModeSwipes, UU>(ch, lds, bytes, offs, slot, n, regs, nslots, out,  \
+        return launch_swipes_u<kModeSwipes, UU>(ch, lds, bytes, offs, fixed_w, slot, n, regs, nslots, out,  \
                                                 stats, cus, st);                                   \
     if (mode == kModeExists)                                                                       \
-        return launch_swipes_u<kModeExists, UU>(ch, lds, bytes, offs, slot, n, regs, nslots, out,  \
+        return launch_swipes_u<kModeExists, UU>(ch, lds, bytes, offs, fixed_w, slot, n, regs, nslots, out,  \
                                                 stats, cus, st);                                   \
-    return launch_swipes_u<kModeStats, UU>(ch, lds, bytes, offs, slot, n, regs, nslots, out,       \
+    return launch_swipes_u<kModeStats, UU>(ch, lds, bytes, offs, fixed_w, slot, n, regs, nslots, out,       \
                                            stats, cus, st);
     if (tile >= 8) {
         SKE_U(8)

@@ -142,6 +142,16 @@ class SketchEngine:
         self.ctx.call("ske_swipes_async", fid, C.c_void_p(b.slot.ptr), C.c_void_p(b.bytes.ptr),
                       C.c_void_p(b.offs.ptr), b.n, C.c_void_p(out.ptr) if out else None)
 
+    def swipes_fixed(self, fid: int, b: DeviceBatch, out: DeviceBuffer | None = None):
+        """K1 over a fixed-width batch (ids at bytes + i*width, no offsets)."""
+        assert b.width > 0
+        self.ctx.call("ske_swipes_fixed", fid, C.c_void_p(b.slot.ptr), C.c_void_p(b.bytes.ptr),
+                      b.width, b.n, C.c_void_p(out.ptr) if out else None, SKE_MEM_DEVICE)
+
+    def swipes_fixed_async(self, fid: int, b: DeviceBatch, out: DeviceBuffer | None = None):
+        self.ctx.call("ske_swipes_fixed_async", fid, C.c_void_p(b.slot.ptr),
+                      C.c_void_p(b.bytes.ptr), b.width, b.n, C.c_void_p(out.ptr) if out else None)
+
     def swipes_stats(self, fid: int, b: DeviceBatch) -> tuple[int, int]:
         probes, nvalid = C.c_uint64(), C.c_uint64()
         self.ctx.call("ske_swipes_stats", fid, C.c_void_p(b.bytes.ptr), C.c_void_p(b.offs.ptr),

@@ -371,3 +371,32 @@ def test_hll_get_set_interop(client, orc):
     assert client.execute_command("SET", "hll:b", s) == "OK"
     assert np.array_equal(client.hll_registers("hll:b"), h.regs)
     assert client.pfcount("hll:b") == h.count()
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_swipes_fixed_width_equals_offsets(engine, orc, variant):
+    """ske_swipes_fixed (ids at bytes + i*width, no offsets) == ske_swipes on
+    the same batch == the oracle, registers and flags."""
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import DeviceBuffer
+    w = synthetic.WORKLOADS["c4"]
+    engine.set_option("variant", variant)
+    engine.reserve(0, w.bf_error, w.bf_capacity)
+    p = engine.gen_params(w)
+    engine.preload(0, p, w.n_members)
+    engine.hll_reserve(2 * w.n_keys)
+    b = engine.swipe_batch(p, 0, 250_000)
+    buf, offs, slot = b.to_host()
+    o1, o2 = DeviceBuffer(engine.ctx, b.n), DeviceBuffer(engine.ctx, b.n)
+    engine.swipes(0, b, o1)
+    b.slot.from_host(slot + w.n_keys)           # second copy of the keys
+    engine.swipes_fixed(0, b, o2)
+    regs = engine.registers_all(2 * w.n_keys)
+    assert np.array_equal(o1.to_host(np.uint8, b.n), o2.to_host(np.uint8, b.n))
+    assert np.array_equal(regs[:w.n_keys], regs[w.n_keys:])
+    chain = orc.Chain(w.bf_capacity, w.bf_error)
+    mb = engine.members_batch(p, 0, w.n_members).to_host()
+    chain.madd_packed(mb[0], mb[1])
+    valid, oregs, _ = _oracle_swipes(orc, chain, w.n_keys, buf, offs, slot)
+    assert np.array_equal(o2.to_host(np.uint8, b.n), valid)
+    assert np.array_equal(regs[w.n_keys:], oregs)
