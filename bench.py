@@ -36,7 +36,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--tile", type=int, default=0, help="K1 swipes per thread in flight (1,2,4,8)")
-    ap.add_argument("--variant", type=int, default=-1, help="-1 auto, 0 global Bloom, 1 LDS Bloom")
+    ap.add_argument("--variant", type=int, default=-1,
+                    help="-1 auto, 0 global Bloom, 1 LDS Bloom, 2 XCD-partitioned Bloom")
     ap.add_argument("--max-batches", type=int, default=64)
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: K1 parts removed (bits)")
     ap.add_argument("--layout", default="offsets", choices=["offsets", "fixed"],
@@ -190,7 +191,7 @@ def main():
                    "hll_keys_per_gpu": w.n_keys, "invalid_frac": w.invalid_frac,
                    "bloom": {"error": w.bf_error, "capacity": w.bf_capacity},
                    "id_bytes": width, "parallelism": f"dp{world} (key-sharded, Bloom replicated)",
-                   "k1_variant": "lds-bloom" if engine.variant(0) else "global-bloom",
+                   "k1_variant": {0: "global-bloom", 1: "lds-bloom", 2: "xcd-regions"}[engine.variant(0)],
                    "tile": args.tile or 2, "layout": args.layout},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -206,6 +206,7 @@ ChainDev chain_dev(const Filter &F, size_t first = 0, size_t count = SIZE_MAX) {
         D.div = L.div;
         D.k = uint32_t(L.hashes);
         D.lds_off = lds;
+        D.rmul = uint32_t((uint64_t(kRegions) << 32) / L.bits);
         const uint64_t padded = (L.bytes + 15) & ~uint64_t(15);
         lds = (lds + padded > 0xffffffffu) ? 0xffffffffu : uint32_t(lds + padded);
     }
@@ -227,13 +228,27 @@ LinkDev link_dev(const Link &L) {
     D.div = L.div;
     D.k = uint32_t(L.hashes);
     D.lds_off = 0;
+    D.rmul = uint32_t((uint64_t(kRegions) << 32) / L.bits);
     return D;
 }
 
 bool use_lds(const ske_ctx *c, const ChainDev &ch) {
     if (!c->lds_ok || ch.nlinks == 0) return false;
-    if (c->variant == 0) return false;
+    if (c->variant == 0 || c->variant == 2) return false;
     return ch.lds_bytes <= lds_bloom_max();
+}
+
+// K1 variant for a chain: 1 LDS image (fits 152 KiB), 2 XCD-partitioned
+// (larger than ~2 L2s, every link <= 2^31 bits), else 0 global.
+constexpr uint64_t kXrMinBytes = 8ull << 20;
+int k1_variant(const ske_ctx *c, const ChainDev &ch) {
+    if (ch.nlinks == 0) return 0;
+    if (use_lds(c, ch)) return 1;
+    uint64_t total = 0;
+    for (int l = 0; l < ch.nlinks; l++) total += ch.link[l].div.d >> 3;
+    if (!xr_supported(ch) || c->variant == 0) return 0;
+    if (c->variant == 2 || total >= kXrMinBytes) return 2;
+    return 0;
 }
 
 Filter *get_filter(ske_ctx *c, uint32_t fid) {
@@ -286,6 +301,34 @@ int check_err_flag(ske_ctx *c, int code_if_set) {
     HIPCHK(c, hipMemcpyAsync(&h, c->err, 4, hipMemcpyDeviceToHost, c->st));
     HIPCHK(c, hipStreamSynchronize(c->st));
     return h ? code_if_set : SKE_OK;
+}
+
+// Enqueue K1 (mode swipes) with the variant the chain selects.
+int launch_k1(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32_t *offs,
+              uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *out) {
+    if (n == 0) return SKE_OK;
+    if (k1_variant(c, ch) == 2 && !c->ablate) {
+        hipError_t e = hipSuccess;
+        void *scr = scratch_get(c->scratch, 16, xr_scratch_bytes(n, ch.nlinks), &e);
+        if (e != hipSuccess) {
+            c->last_hip = hipGetErrorString(e);
+            return SKE_ENOMEM;
+        }
+        HIPCHK(c, launch_swipes_xr(ch, bytes, offs, fixed_w, slot, n, c->regs, c->nslots, out,
+                                   scr, c->err, c->cus, c->st));
+        return SKE_OK;
+    }
+    if (c->ablate) {
+        ChainDev cha = ch;
+        cha.ablate = c->ablate;
+        HIPCHK(c, launch_swipes(0, cha, use_lds(c, ch), c->pb, bytes, offs, fixed_w, slot, n,
+                                c->regs, c->nslots, out, (unsigned long long *)c->err, c->cus,
+                                c->st));
+        return SKE_OK;
+    }
+    HIPCHK(c, launch_swipes(0, ch, use_lds(c, ch), c->pb, bytes, offs, fixed_w, slot, n, c->regs,
+                            c->nslots, out, (unsigned long long *)c->err, c->cus, c->st));
+    return SKE_OK;
 }
 
 }  // namespace
@@ -412,7 +455,7 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
         return SKE_OK;
     }
     if (!strcmp(name, "variant")) {
-        if (value < -1 || value > 1) return SKE_EINVAL;
+        if (value < -1 || value > 2) return SKE_EINVAL;
         c->variant = int(value);
         return SKE_OK;
     }
@@ -720,9 +763,9 @@ int ske_swipes(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *by
         if (rc) return rc;
     }
     HIPCHK(c, hipMemsetAsync(c->err, 0, 4, c->st));
-    const ChainDev ch = F->exists ? chain_dev(*F) : ChainDev{};
-    HIPCHK(c, launch_swipes(0, ch, use_lds(c, ch), c->pb, s.bytes, s.offs, 0, dslot, n, c->regs,
-                            c->nslots, dout, (unsigned long long *)c->err, c->cus, c->st));
+    static const ChainDev empty{};
+    rc = launch_k1(c, F->exists ? cached_chain(*F) : empty, s.bytes, s.offs, 0, dslot, n, dout);
+    if (rc) return rc;
     if (out_valid && mem != SKE_MEM_DEVICE)
         HIPCHK(c, hipMemcpyAsync(out_valid, dout, n, hipMemcpyDeviceToHost, c->st));
     return check_err_flag(c, SKE_ERANGE);
@@ -734,17 +777,7 @@ int ske_swipes_async(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8
     Filter *F = get_filter(c, fid);
     if (!F) return SKE_EINVAL;
     static const ChainDev empty{};
-    const ChainDev &ch = F->exists ? cached_chain(*F) : empty;
-    if (c->ablate) {
-        ChainDev cha = ch;
-        cha.ablate = c->ablate;
-        HIPCHK(c, launch_swipes(0, cha, use_lds(c, ch), c->pb, bytes, offs, 0, slot, n, c->regs,
-                                c->nslots, out_valid, (unsigned long long *)c->err, c->cus, c->st));
-        return SKE_OK;
-    }
-    HIPCHK(c, launch_swipes(0, ch, use_lds(c, ch), c->pb, bytes, offs, 0, slot, n, c->regs,
-                            c->nslots, out_valid, (unsigned long long *)c->err, c->cus, c->st));
-    return SKE_OK;
+    return launch_k1(c, F->exists ? cached_chain(*F) : empty, bytes, offs, 0, slot, n, out_valid);
 }
 
 int ske_swipes_fixed_async(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *bytes,
@@ -753,10 +786,8 @@ int ske_swipes_fixed_async(ske_ctx *c, uint32_t fid, const uint32_t *slot, const
     Filter *F = get_filter(c, fid);
     if (!F) return SKE_EINVAL;
     static const ChainDev empty{};
-    const ChainDev &ch = F->exists ? cached_chain(*F) : empty;
-    HIPCHK(c, launch_swipes(0, ch, use_lds(c, ch), c->pb, bytes, nullptr, width, slot, n, c->regs,
-                            c->nslots, out_valid, (unsigned long long *)c->err, c->cus, c->st));
-    return SKE_OK;
+    return launch_k1(c, F->exists ? cached_chain(*F) : empty, bytes, nullptr, width, slot, n,
+                     out_valid);
 }
 
 int ske_swipes_fixed(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *bytes,
@@ -812,7 +843,7 @@ int ske_swipes_variant(ske_ctx *c, uint32_t fid) {
     Filter *F = c ? get_filter(c, fid) : nullptr;
     if (!F) return SKE_EINVAL;
     const ChainDev ch = F->exists ? chain_dev(*F) : ChainDev{};
-    return use_lds(c, ch) ? 1 : 0;
+    return k1_variant(c, ch);
 }
 
 static int pfcount_impl(ske_ctx *c, const uint8_t *regs, const uint32_t *slots,

@@ -205,7 +205,11 @@ struct LinkDev {
     Divisor div;
     uint32_t k;          // bloom->hashes
     uint32_t lds_off;    // byte offset of this link inside the LDS image
+    uint32_t rmul;       // XCD-region split: region(x) = umulhi(x, rmul) in [0, 8)
+    uint32_t pad_;
 };
+
+constexpr int kRegions = 8;  // one slice of every link per XCD
 
 // Diagnostic ablation bits (ske_set_option "ablate"; never set in production):
 // the timing of K1 with a part removed says what bounds it.

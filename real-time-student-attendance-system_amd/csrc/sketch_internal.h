@@ -29,6 +29,14 @@ hipError_t launch_gen_swipes(const GenDev &g, uint64_t start, uint64_t n, uint8_
 hipError_t launch_gen_members(const GenDev &g, uint64_t start, uint64_t n, uint8_t *bytes,
                               uint32_t *offs, int cus, hipStream_t st);
 
+// sketch_xr.hip -- XCD-partitioned K1 for chains larger than the LDS image
+bool xr_supported(const ChainDev &ch);
+uint64_t xr_scratch_bytes(uint64_t n, int nlinks);
+hipError_t launch_swipes_xr(const ChainDev &ch, const uint8_t *bytes, const uint32_t *offs,
+                            uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *regs,
+                            uint32_t nslots, uint8_t *out, void *scratch, unsigned int *err,
+                            int cus, hipStream_t st);
+
 // sketch_order.hip -- order-exact paths (replies that depend on item order)
 struct Scratch;  // growable device scratch, owned by the context
 void *scratch_get(Scratch *s, int slot, size_t bytes, hipError_t *err);

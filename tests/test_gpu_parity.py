@@ -227,7 +227,7 @@ def _oracle_swipes(orc, chain, nkeys, buf, offs, slot):
     return valid, regs, probes
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("pb", [1, 4, 8])
 def test_swipes_c2_shape_vs_oracle(engine, orc, variant, pb):
     """Fused BF.EXISTS + PFADD on a C2-shaped stream (7-digit ids, 10 %
@@ -254,12 +254,14 @@ def test_swipes_c2_shape_vs_oracle(engine, orc, variant, pb):
     assert np.array_equal(out.to_host(np.uint8, b.n), valid)
     assert np.array_equal(engine.registers_all(w.n_keys), regs)
     assert engine.swipes_stats(0, b) == (probes, int(valid.sum()))
-    assert engine.variant(0) == (1 if variant != 0 else 0)
+    assert engine.variant(0) == variant
 
 
-def test_swipes_facade_multilink_and_ragged(client, orc):
+@pytest.mark.parametrize("variant", [-1, 0, 2])
+def test_swipes_facade_multilink_and_ragged(client, orc, variant):
     """swipes() over a 4-link default chain with ragged ids (0..40 B), keys
-    created only when they receive a valid swipe."""
+    created only when they receive a valid swipe; every K1 variant."""
+    client.ctx.call("ske_set_option", b"variant", variant)
     rng = np.random.default_rng(8)
     members = _rand_items(rng, 1000, 40)
     client.execute_command("BF.MADD", "bf", *members)
@@ -373,7 +375,7 @@ def test_hll_get_set_interop(client, orc):
     assert client.pfcount("hll:b") == h.count()
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_swipes_fixed_width_equals_offsets(engine, orc, variant):
     """ske_swipes_fixed (ids at bytes + i*width, no offsets) == ske_swipes on
     the same batch == the oracle, registers and flags."""
