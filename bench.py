@@ -40,6 +40,8 @@ def parse():
                     help="-1 auto, 0 global Bloom, 1 LDS Bloom, 2 XCD-partitioned Bloom")
     ap.add_argument("--max-batches", type=int, default=64)
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: K1 parts removed (bits)")
+    ap.add_argument("--xr-u", type=int, default=0, help="XCD-partitioned K1: slice-pass tile")
+    ap.add_argument("--xr-fu", type=int, default=0, help="XCD-partitioned K1: finish-pass tile")
     ap.add_argument("--layout", default="offsets", choices=["offsets", "fixed"],
                     help="id batch layout: bytes + u32 offsets, or fixed-width ids")
     return ap.parse_args()
@@ -106,6 +108,10 @@ def main():
         engine.set_option("variant", args.variant)
     if args.ablate:
         engine.set_option("ablate", args.ablate)
+    if args.xr_u:
+        engine.set_option("xr_region_u", args.xr_u)
+    if args.xr_fu:
+        engine.set_option("xr_finish_u", args.xr_fu)
 
     # Bloom preload (replicated on every rank), HLL key shard of this rank
     engine.reserve(0, w.bf_error, w.bf_capacity)

@@ -73,6 +73,8 @@ struct ske_ctx {
     int pb = 2;           // K1 tile: swipes per thread in flight (1, 2, 4, 8)
     int variant = -1;     // -1 auto, 0 global, 1 LDS
     uint32_t ablate = 0;  // diagnostic only (kAblate* bits)
+    int xr_region_u = 2;  // XCD-partitioned K1: swipes per lane in the slice passes
+    int xr_finish_u = 1;  //   and in the finish pass
     bool lds_ok = false;
     std::string last_hip;
 };
@@ -315,7 +317,7 @@ int launch_k1(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32
             return SKE_ENOMEM;
         }
         HIPCHK(c, launch_swipes_xr(ch, bytes, offs, fixed_w, slot, n, c->regs, c->nslots, out,
-                                   scr, c->err, c->cus, c->st));
+                                   scr, c->err, c->cus, c->xr_region_u, c->xr_finish_u, c->st));
         return SKE_OK;
     }
     if (c->ablate) {
@@ -447,6 +449,11 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
     if (!strcmp(name, "tile")) {
         if (value != 1 && value != 2 && value != 4 && value != 8) return SKE_EINVAL;
         c->pb = int(value);
+        return SKE_OK;
+    }
+    if (!strcmp(name, "xr_region_u") || !strcmp(name, "xr_finish_u")) {
+        if (value != 1 && value != 2 && value != 4 && value != 8) return SKE_EINVAL;
+        (name[3] == 'r' ? c->xr_region_u : c->xr_finish_u) = int(value);
         return SKE_OK;
     }
     if (!strcmp(name, "ablate")) {

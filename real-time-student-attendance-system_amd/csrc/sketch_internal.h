@@ -35,7 +35,7 @@ uint64_t xr_scratch_bytes(uint64_t n, int nlinks);
 hipError_t launch_swipes_xr(const ChainDev &ch, const uint8_t *bytes, const uint32_t *offs,
                             uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *regs,
                             uint32_t nslots, uint8_t *out, void *scratch, unsigned int *err,
-                            int cus, hipStream_t st);
+                            int cus, int region_u, int finish_u, hipStream_t st);
 
 // sketch_order.hip -- order-exact paths (replies that depend on item order)
 struct Scratch;  // growable device scratch, owned by the context

@@ -93,8 +93,12 @@ __global__ void __launch_bounds__(256)
         const uint32_t slice = ((d + kRegions - 1) / kRegions + 1023) & ~1023u;
         const uint32_t lo = region * slice;
         const uint32_t len = lo >= d ? 0u : (d - lo < slice ? d - lo : slice);
+        // bit array through a buffer descriptor: 32-bit byte offsets, range
+        // checked by the hardware
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t *>(L.bf), 0, int(d >> 3), 0x00020000);
         for (uint64_t base = c0; base < c1; base += uint64_t(T) * U) {
-            uint32_t x[U], bm[U], wrap[U];
+            uint32_t x[U], inc0[U], inc1[U], wrap[U];
             bool ok[U], act[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {
@@ -102,26 +106,30 @@ __global__ void __launch_bounds__(256)
                 act[u] = i < c1;
                 ok[u] = act[u];
                 x[u] = act[u] ? st.x0[uint64_t(l) * n + i] : 0u;
-                bm[u] = act[u] ? st.bm[uint64_t(l) * n + i] : 0u;
+                inc0[u] = act[u] ? st.bm[uint64_t(l) * n + i] : 0u;
                 wrap[u] = act[u] ? st.wrap[uint64_t(l) * n + i] : 0u;
             }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                // the step that wraps a + i*b adds bm - (2^64 mod d) instead
+                const uint32_t m = inc0[u] - t;
+                inc1[u] = umin32(m, m + d);
+            }
             for (uint32_t j = 0; j < L.k; j++) {
-                uint8_t byte[U];
+                uint32_t byte[U];
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     const bool mine = ok[u] && (x[u] - lo) < len;
-                    byte[u] = mine ? L.bf[x[u] >> 3] : uint8_t(0xff);
+                    byte[u] = mine ? uint32_t(__builtin_amdgcn_raw_buffer_load_b8(rsrc, x[u] >> 3, 0, 0))
+                                   : 0xffu;
                 }
                 bool any = false;
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     ok[u] = ok[u] && ((byte[u] >> (x[u] & 7)) & 1);
                     any |= ok[u];
-                    // step j -> j+1 (x, bm < d <= 2^31)
-                    x[u] += bm[u];
+                    x[u] += ((wrap[u] >> (j + 1)) & 1) ? inc1[u] : inc0[u];
                     x[u] = umin32(x[u], x[u] - d);
-                    x[u] -= ((wrap[u] >> (j + 1)) & 1) ? t : 0u;
-                    x[u] = umin32(x[u], x[u] + d);
                 }
                 if (!__any(any)) break;
             }
@@ -138,35 +146,60 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+template <int U>
 __global__ void __launch_bounds__(256)
     k_xr_finish(const ChainDev ch, const uint32_t *__restrict__ slot, uint64_t n,
                 const uint32_t *__restrict__ hllw, uint8_t *__restrict__ regs, uint32_t nslots,
                 uint8_t *__restrict__ out, const unsigned long long *__restrict__ fail,
                 unsigned int *__restrict__ err) {
     const uint64_t nwaves = (n + 63) / 64;
-    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t w = i / 64;
-        const uint32_t lane = uint32_t(i & 63);
-        bool valid = false;
-        for (int l = 0; l < ch.nlinks && !valid; l++) {
-            unsigned long long f = 0;
+    const uint32_t T = blockDim.x, tid = threadIdx.x;
+    const uint64_t stride = uint64_t(gridDim.x) * T * U;
+    for (uint64_t base = uint64_t(blockIdx.x) * T * U; base < n; base += stride) {
+        bool valid[U];
+        uint8_t *reg[U];
+        uint32_t rank[U], cur[U];
 #pragma unroll
-            for (int r = 0; r < kRegions; r++) f |= fail[(uint64_t(r) * ch.nlinks + l) * nwaves + w];
-            valid = !((f >> lane) & 1);
-        }
-        if (valid) {
-            const uint32_t s = slot[i];
-            if (s >= nslots) {
-                atomicOr(err, 1u);
-            } else {
-                const uint32_t hv = hllw[i];
-                uint8_t *reg = regs + size_t(s) * kHllRegs + (hv & 0xffff);
-                const uint32_t rank = hv >> 16;
-                if (*reg < rank) xr_reg_max(reg, rank);
+        for (int u = 0; u < U; u++) {
+            const uint64_t i = base + uint64_t(u) * T + tid;
+            valid[u] = false;
+            reg[u] = nullptr;
+            rank[u] = 0;
+            if (i < n) {
+                const uint64_t w = i / 64;
+                const uint32_t lane = uint32_t(i & 63);
+                for (int l = 0; l < ch.nlinks && !valid[u]; l++) {
+                    unsigned long long f = 0;
+#pragma unroll
+                    for (int r = 0; r < kRegions; r++)
+                        f |= fail[(uint64_t(r) * ch.nlinks + l) * nwaves + w];
+                    valid[u] = !((f >> lane) & 1);
+                }
+                if (valid[u]) {
+                    const uint32_t s = slot[i];
+                    if (s >= nslots) {
+                        atomicOr(err, 1u);
+                    } else {
+                        const uint32_t hv = hllw[i];
+                        reg[u] = regs + size_t(s) * kHllRegs + (hv & 0xffff);
+                        rank[u] = hv >> 16;
+                    }
+                }
             }
         }
-        if (out) out[i] = valid;
+        // the U register pre-checks in flight together
+#pragma unroll
+        for (int u = 0; u < U; u++) cur[u] = reg[u] ? *reg[u] : 0xffu;
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (cur[u] < rank[u]) xr_reg_max(reg[u], rank[u]);
+        if (out) {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint64_t i = base + uint64_t(u) * T + tid;
+                if (i < n) out[i] = valid[u];
+            }
+        }
     }
 }
 
@@ -191,7 +224,7 @@ uint64_t xr_scratch_bytes(uint64_t n, int nlinks) {
 hipError_t launch_swipes_xr(const ChainDev &ch, const uint8_t *bytes, const uint32_t *offs,
                             uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *regs,
                             uint32_t nslots, uint8_t *out, void *scratch, unsigned int *err,
-                            int cus, hipStream_t st) {
+                            int cus, int region_u, int finish_u, hipStream_t st) {
     if (n == 0) return hipSuccess;
     auto *fail = reinterpret_cast<unsigned long long *>(scratch);
     uint32_t *p = reinterpret_cast<uint32_t *>(fail + uint64_t(kRegions) * ch.nlinks * ((n + 63) / 64));
@@ -202,16 +235,23 @@ hipError_t launch_swipes_xr(const ChainDev &ch, const uint8_t *bytes, const uint
     s.hll = p + 3 * uint64_t(ch.nlinks) * n;
     hipLaunchKernelGGL(k_xr_hash, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, ch, bytes, offs,
                        fixed_w, n, s);
-    constexpr int U = 2;
-    const uint64_t tile = 256 * U;
+    const int U = region_u >= 8 ? 8 : (region_u >= 4 ? 4 : (region_u >= 2 ? 2 : 1));
+    const uint64_t tile = 256 * uint64_t(U);
     uint64_t chunks = uint64_t(cus) * 8 / kRegions;  // 8 blocks per CU in total
     uint64_t chunk = (n + chunks - 1) / chunks;
     chunk = (chunk + tile - 1) / tile * tile;
     chunks = (n + chunk - 1) / chunk;
-    hipLaunchKernelGGL(k_xr_region<U>, dim3(unsigned(chunks * kRegions)), dim3(256), 0, st, ch, n,
-                       chunk, s, fail);
-    hipLaunchKernelGGL(k_xr_finish, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, ch, slot, n,
-                       s.hll, regs, nslots, out, fail, err);
+    const dim3 g(unsigned(chunks * kRegions));
+    if (U == 8) hipLaunchKernelGGL(k_xr_region<8>, g, dim3(256), 0, st, ch, n, chunk, s, fail);
+    else if (U == 4) hipLaunchKernelGGL(k_xr_region<4>, g, dim3(256), 0, st, ch, n, chunk, s, fail);
+    else if (U == 2) hipLaunchKernelGGL(k_xr_region<2>, g, dim3(256), 0, st, ch, n, chunk, s, fail);
+    else hipLaunchKernelGGL(k_xr_region<1>, g, dim3(256), 0, st, ch, n, chunk, s, fail);
+    if (finish_u >= 4)
+        hipLaunchKernelGGL(k_xr_finish<4>, dim3(grid_for(n, 256 * 4, cus * 8)), dim3(256), 0, st, ch,
+                           slot, n, s.hll, regs, nslots, out, fail, err);
+    else
+        hipLaunchKernelGGL(k_xr_finish<1>, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, ch,
+                           slot, n, s.hll, regs, nslots, out, fail, err);
     return hipGetLastError();
 }
 
