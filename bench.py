@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: K1 parts removed (bits)")
     ap.add_argument("--xr-u", type=int, default=0, help="XCD-partitioned K1: slice-pass tile")
     ap.add_argument("--xr-fu", type=int, default=0, help="XCD-partitioned K1: finish-pass tile")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="HIP streams the steps alternate over (launch tails overlap)")
     ap.add_argument("--layout", default="offsets", choices=["offsets", "fixed"],
                     help="id batch layout: bytes + u32 offsets, or fixed-width ids")
     return ap.parse_args()
@@ -127,8 +129,11 @@ def main():
     width = len(str(w.id_hi - 1))
 
     fixed = args.layout == "fixed"
+    streams = [stream] + [torch.cuda.Stream() for _ in range(max(0, args.streams - 1))]
 
     def step(j):
+        if len(streams) > 1:
+            engine.set_stream(streams[j % len(streams)].cuda_stream)
         if fixed:
             engine.swipes_fixed_async(0, batches[j % nb])
         else:
@@ -144,8 +149,12 @@ def main():
     e1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
+    for s_ in streams[1:]:
+        s_.wait_stream(stream)
     for j in range(args.steps):
         step(args.warmup + j)
+    for s_ in streams[1:]:
+        stream.wait_stream(s_)
     e1.record(stream)
     host_enqueue = time.perf_counter() - t0
     torch.cuda.synchronize()
@@ -198,7 +207,7 @@ def main():
                    "bloom": {"error": w.bf_error, "capacity": w.bf_capacity},
                    "id_bytes": width, "parallelism": f"dp{world} (key-sharded, Bloom replicated)",
                    "k1_variant": {0: "global-bloom", 1: "lds-bloom", 2: "xcd-regions"}[engine.variant(0)],
-                   "tile": args.tile or 2, "layout": args.layout},
+                   "tile": args.tile or 2, "layout": args.layout, "streams": args.streams},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src,

@@ -827,6 +827,15 @@ int ske_swipes_fixed(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8
     return check_err_flag(c, SKE_ERANGE);
 }
 
+#ifdef SKE_STAMPS
+// diagnostic build only: point the phase-stamp side buffer at dev_ptr
+int ske_diag_set_stamp_buffer(ske_ctx *c, void *dev_ptr) {
+    if (!c) return SKE_EINVAL;
+    HIPCHK(c, ske::set_stamp_buffer(dev_ptr));
+    return SKE_OK;
+}
+#endif
+
 int ske_swipes_stats(ske_ctx *c, uint32_t fid, const uint8_t *bytes, const uint32_t *offs,
                      uint64_t n, uint64_t *probes, uint64_t *nvalid) {
     if (!c || !probes || !nvalid) return SKE_EINVAL;

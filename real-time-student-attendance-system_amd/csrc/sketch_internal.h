@@ -11,6 +11,7 @@ hipError_t launch_swipes(int mode, const ChainDev &ch, bool lds, int tile, const
                          uint32_t nslots, uint8_t *out, unsigned long long *stats, int cus,
                          hipStream_t st);
 hipError_t lds_bloom_setup();
+hipError_t set_stamp_buffer(void *p);  // -DSKE_STAMPS diagnostic build only
 uint32_t lds_bloom_max();
 hipError_t launch_pfadd(const uint32_t *slot, const uint8_t *bytes, const uint32_t *offs,
                         uint64_t n, uint8_t *regs, uint32_t nslots, unsigned int *err, int cus,

@@ -43,6 +43,30 @@ __device__ __forceinline__ bool reg_max(uint8_t *reg, uint32_t rank) {
 
 enum SwipeMode { kModeSwipes = 0, kModeExists = 1, kModeStats = 2 };
 
+// Diagnostic phase stamps (tools/stamps: built only with -DSKE_STAMPS; the
+// product library has none).  Lane 0 of every wave records s_memtime at the
+// phase boundaries of its first two tiles into a side buffer that no output
+// depends on.
+#ifdef SKE_STAMPS
+__device__ unsigned long long *ske_stamp_buf;
+hipError_t set_stamp_buffer(void *p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(ske_stamp_buf), &p, sizeof(void *));
+}
+#define SKE_STAMP(tile, k)                                                                         \
+    do {                                                                                           \
+        __builtin_amdgcn_sched_barrier(0);                                                         \
+        unsigned long long t_;                                                                     \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
+        __builtin_amdgcn_sched_barrier(0);                                                         \
+        if ((threadIdx.x & 63) == 0 && (tile) < 2)                                                 \
+            ske_stamp_buf[((blockIdx.x * 16 + (threadIdx.x >> 6)) * 2 + (tile)) * 8 + (k)] = t_;   \
+    } while (0)
+#else
+#define SKE_STAMP(tile, k) \
+    do {                   \
+    } while (0)
+#endif
+
 constexpr int kLdsBloomMax = 152 * 1024;  // LDS image budget (160 KiB per CU)
 
 // Copy every link's bit array into the LDS image by LDS-DMA
@@ -160,7 +184,10 @@ __global__ void __launch_bounds__(kLds ? 1024 : 256)
     const bool ablate_probe = kMode == kModeSwipes && (ch.ablate & kAblateProbe);
     const bool do_hll = kMode == kModeSwipes && !(ch.ablate & kAblateHll);
     // a block with no work still joins the staging barrier below
-    for (uint64_t base = c0; base < c1 || !staged; base += uint64_t(T) * U) {
+    int tile_no = 0;
+    SKE_STAMP(0, 0);
+    for (uint64_t base = c0; base < c1 || !staged; base += uint64_t(T) * U, tile_no++) {
+        SKE_STAMP(tile_no, 1);
         Item it[U];
         uint32_t sl[U];
         bool act[U];
@@ -182,6 +209,7 @@ __global__ void __launch_bounds__(kLds ? 1024 : 256)
             __syncthreads();
             staged = true;
         }
+        SKE_STAMP(tile_no, 2);
         // ids of at most 8 bytes (every config's decimal student id) take the
         // short MurmurHash64A path, chosen per wave
         bool short_ids = true;
@@ -224,6 +252,7 @@ __global__ void __launch_bounds__(kLds ? 1024 : 256)
 #pragma unroll
             for (int u = 0; u < U; u++) cur[u] = reg[u] ? *reg[u] : 0xffu;
         }
+        SKE_STAMP(tile_no, 3);
         bool valid[U];
 #pragma unroll
         for (int u = 0; u < U; u++) valid[u] = ablate_probe && act[u];
@@ -238,6 +267,7 @@ __global__ void __launch_bounds__(kLds ? 1024 : 256)
                     link_probe<kLds, U, ProbeCursor>(L, lds_img, ha, hb, act, valid, probes);
             }
         }
+        SKE_STAMP(tile_no, 4);
         if constexpr (kMode == kModeSwipes) {
             if (do_hll) {
 #pragma unroll
@@ -255,6 +285,7 @@ __global__ void __launch_bounds__(kLds ? 1024 : 256)
                     }
                 }
             }
+            SKE_STAMP(tile_no, 5);
             if (out) {
 #pragma unroll
                 for (int u = 0; u < U; u++)

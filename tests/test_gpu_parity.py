@@ -402,3 +402,40 @@ def test_swipes_fixed_width_equals_offsets(engine, orc, variant):
     valid, oregs, _ = _oracle_swipes(orc, chain, w.n_keys, buf, offs, slot)
     assert np.array_equal(o2.to_host(np.uint8, b.n), valid)
     assert np.array_equal(regs[w.n_keys:], oregs)
+
+
+def test_swipes_c3_filter_xcd_regions_vs_oracle(engine, orc):
+    """The XCD-partitioned K1 at C3's real filter size (RESERVE 0.001 / 1e7:
+    19.8 MB, 158M bits, k = 11, slices of ~2.5 MB) on a 1.5M-swipe slice of
+    the C3 stream (Zipf keys), bit-exact vs the oracle; and equal to the
+    global-Bloom variant on the next slice."""
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import DeviceBuffer
+    w = synthetic.WORKLOADS["c3"]
+    engine.reserve(0, w.bf_error, w.bf_capacity)
+    p = engine.gen_params(w)
+    engine.preload(0, p, w.n_members)
+    assert engine.variant(0) == 2
+    keys = 2000  # the stream's first keys only: keep the oracle's slab small
+    w_small = synthetic.Workload(**{**w.__dict__, "n_keys": keys, "zipf_lectures": 20,
+                                    "zipf_days": 100})
+    ps = engine.gen_params(w_small)
+    engine.hll_reserve(2 * keys)
+    b = engine.swipe_batch(ps, 5_000_000, 1_500_000)
+    out = DeviceBuffer(engine.ctx, b.n)
+    engine.swipes(0, b, out)
+    buf, offs, slot = b.to_host()
+    mb = engine.members_batch(p, 0, w.n_members).to_host()
+    chain = orc.Chain(w.bf_capacity, w.bf_error)
+    chain.madd_packed(mb[0], mb[1])
+    assert np.array_equal(engine.bloom_bits(0, 0, chain.link_info(0)["bytes"]), chain.link_bits(0))
+    valid, regs, _ = _oracle_swipes(orc, chain, keys, buf, offs, slot)
+    assert np.array_equal(out.to_host(np.uint8, b.n), valid)
+    assert np.array_equal(engine.registers_all(keys), regs)
+    # global variant on the same batch into the second half of the slab
+    engine.set_option("variant", 0)
+    b.slot.from_host(slot + keys)
+    out2 = DeviceBuffer(engine.ctx, b.n)
+    engine.swipes(0, b, out2)
+    assert np.array_equal(out2.to_host(np.uint8, b.n), valid)
+    assert np.array_equal(engine.registers_all(2 * keys)[keys:], regs)
