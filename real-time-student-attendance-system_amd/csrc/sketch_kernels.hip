@@ -56,7 +56,7 @@ hipError_t set_stamp_buffer(void *p) {
     do {                                                                                           \
         __builtin_amdgcn_sched_barrier(0);                                                         \
         unsigned long long t_;                                                                     \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");           \
         __builtin_amdgcn_sched_barrier(0);                                                         \
         if ((threadIdx.x & 63) == 0 && (tile) < 2)                                                 \
             ske_stamp_buf[((blockIdx.x * 16 + (threadIdx.x >> 6)) * 2 + (tile)) * 8 + (k)] = t_;   \

@@ -1,11 +1,11 @@
 """Phase timeline of K1 (LDS variant, C2) from the stamped diagnostic build.
 
-Stamps per wave and tile (s_memtime ticks, lane 0):
+Stamps per wave and tile (s_memrealtime ticks at 100 MHz, lane 0):
   0 kernel entry   1 tile start   2 id/slot loads issued (+ Bloom staged, tile 0)
   3 hashes + HLL pre-check issued   4 probes done   5 HLL CAS done
-Prints median / p90 phase lengths in microseconds (100 MHz s_memrealtime is not
-used; s_memtime runs at the shader clock, so ticks are converted with the
-clock measured over the whole kernel: ticks(last stamp) / kernel wall time).
+Prints median / p90 phase lengths in microseconds.  The stamp buffer is zeroed
+before the measured launch, which runs asynchronously on its own stream
+between two events.
 """
 import ctypes as C
 import os
@@ -37,40 +37,43 @@ eng.preload(0, p, w.n_members)
 eng.hll_reserve(w.n_keys)
 batches = [eng.swipe_batch(p, j * w.step_swipes, w.step_swipes) for j in range(12)]
 nblocks, nwaves = 256, 16
-buf = DeviceBuffer(eng.ctx, nblocks * nwaves * 2 * 8 * 8)
+N = nblocks * nwaves * 2 * 8
+buf = DeviceBuffer(eng.ctx, N * 8)
 lib.ske_diag_set_stamp_buffer(eng.ctx.ptr, C.c_void_p(buf.ptr))
-for j in range(11):
-    eng.swipes(0, batches[j])
+for j in range(10):
+    eng.swipes_async(0, batches[j])
 torch.cuda.synchronize()
-s = buf.to_host(np.uint64, nblocks * nwaves * 2 * 8).reshape(nblocks, nwaves, 2, 8).astype(np.int64)
-t0 = s[:, :, 0, 0][s[:, :, 0, 0] > 0].min()
+buf.from_host(np.zeros(N, np.uint64))
+stream = torch.cuda.Stream()
+eng.set_stream(stream.cuda_stream)
 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-ev[0].record()
-eng.swipes(0, batches[11])
-ev[1].record()
+ev[0].record(stream)
+eng.swipes_async(0, batches[10])
+ev[1].record(stream)
 torch.cuda.synchronize()
 kern_us = ev[0].elapsed_time(ev[1]) * 1e3
-s = buf.to_host(np.uint64, nblocks * nwaves * 2 * 8).reshape(nblocks, nwaves, 2, 8).astype(np.int64)
+s = buf.to_host(np.uint64, N).reshape(nblocks, nwaves, 2, 8).astype(np.int64)
+TICK_US = 0.01  # s_memrealtime: 100 MHz
 valid = s[:, :, 0, 0] > 0
 start = s[:, :, 0, 0][valid].min()
-last = s[valid].max()
-ghz = (last - start) / (kern_us * 1e3)
-print(f"tile={tile} kernel {kern_us:.1f} us (events), stamped span {(last - start) / ghz / 1e3:.1f} us "
-      f"at {ghz:.2f} GHz-equivalent ticks")
-names = {(0, 1): "entry->tile0", (1, 2): "loads+stage", (2, 3): "hash+precheck issue",
-         (3, 4): "probes", (4, 5): "HLL wait+CAS"}
+print(f"tile={tile} kernel {kern_us:.1f} us (events); {valid.sum()} waves stamped")
+names = [(0, 1, "entry->tile0"), (1, 2, "loads(+stage)"), (2, 3, "hash+precheck issue"),
+         (3, 4, "probes"), (4, 5, "HLL wait+CAS")]
 for t in range(2):
-    for (a, b), nm in names.items():
-        if t == 1 and a == 0:
+    ok_t = valid & (s[:, :, t, 5] > 0)
+    for a_, b_, nm in names:
+        if t == 1 and a_ == 0:
             continue
-        d = (s[:, :, t, b] - s[:, :, t, a])[valid & (s[:, :, t, b] > 0)] / ghz / 1e3
+        d = (s[:, :, t, b_] - s[:, :, t, a_])[ok_t] * TICK_US
         if d.size:
-            print(f"  tile{t} {nm:22s} median {np.median(d):6.2f} us  p90 {np.percentile(d, 90):6.2f} us")
+            print(f"  tile{t} {nm:22s} median {np.median(d):6.2f} us  p90 {np.percentile(d, 90):6.2f} us  (n={d.size})")
     if t == 0:
-        d = (s[:, :, 1, 1] - s[:, :, 0, 5])[valid & (s[:, :, 1, 1] > 0)] / ghz / 1e3
+        ok1 = valid & (s[:, :, 1, 1] > 0)
+        d = (s[:, :, 1, 1] - s[:, :, 0, 5])[ok1] * TICK_US
         if d.size:
-            print(f"  out writes+loop        median {np.median(d):6.2f} us")
-ends = np.maximum(s[:, :, 0, 5], s[:, :, 1, 5])[valid]
-print(f"  wave end (last stamp) rel. to first entry: median {np.median(ends - start) / ghz / 1e3:.2f} us, "
-      f"max {(ends.max() - start) / ghz / 1e3:.2f} us; first entry spread "
-      f"{(s[:, :, 0, 0][valid].max() - start) / ghz / 1e3:.2f} us")
+            print(f"  out writes+loop          median {np.median(d):6.2f} us")
+entry = (s[:, :, 0, 0][valid] - start) * TICK_US
+last = np.where(s[:, :, 1, 5] > 0, s[:, :, 1, 5], s[:, :, 0, 5])[valid]
+print(f"  wave entry spread: median {np.median(entry):.2f} us, max {entry.max():.2f} us")
+print(f"  wave end rel. first entry: median {np.median((last - start) * TICK_US):.2f} us, "
+      f"max {(last.max() - start) * TICK_US:.2f} us")
