@@ -199,6 +199,29 @@ struct ProbeCursor32 {
     }
 };
 
+// The same walk with both increments precomputed: the step whose a + i*b
+// wraps 2^64 adds inc1 = (bm - 2^64 mod d) mod d, every other step inc0 = bm,
+// so a step is the 64-bit add (its carry selects the increment), one 32-bit
+// add and one conditional subtract.  d <= 2^31.
+struct ProbeWalk32 {
+    uint64_t v, b;
+    uint32_t x, inc0, inc1;
+    SKE_HD void init(uint64_t a, uint64_t b_, const Divisor &D) {
+        v = a;
+        b = b_;
+        x = uint32_t(fastmod(a, D));
+        inc0 = uint32_t(fastmod(b_, D));
+        const uint32_t m = inc0 - uint32_t(D.t);
+        inc1 = umin32(m, m + uint32_t(D.d));
+    }
+    SKE_HD void step(uint32_t d) {
+        const uint64_t vn = v + b;
+        x += vn < v ? inc1 : inc0;
+        v = vn;
+        x = umin32(x, x - d);
+    }
+};
+
 // One link of a RedisBloom scalable chain (SBLink.inner), device view.
 struct LinkDev {
     const uint8_t *bf;  // bit array (bytes multiple of 8; LSB-first bits)

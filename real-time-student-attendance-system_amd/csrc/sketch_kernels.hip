@@ -96,9 +96,9 @@ template <int U>
 __device__ __forceinline__ void link_probe_lds32(const LinkDev &L, const uint8_t *lds,
                                                  const uint64_t *ha, const uint64_t *hb,
                                                  const bool *act, bool *valid, uint32_t &probes) {
-    const uint32_t d = uint32_t(L.div.d), t = uint32_t(L.div.t);
+    const uint32_t d = uint32_t(L.div.d);
     const uint8_t *img = lds + L.lds_off;
-    ProbeCursor32 c[U];
+    ProbeWalk32 c[U];
     bool alive[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -115,7 +115,7 @@ __device__ __forceinline__ void link_probe_lds32(const LinkDev &L, const uint8_t
             probes += alive[u];
             alive[u] = alive[u] && ((byte[u] >> (c[u].x & 7)) & 1);
             any |= alive[u];
-            c[u].step(d, t);
+            c[u].step(d);
         }
         if (!__any(any)) break;
     }

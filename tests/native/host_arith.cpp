@@ -55,6 +55,16 @@ int main() {
                     }
                     c32.step(D);
                 }
+                ske::ProbeWalk32 w32;  // precomputed-increment walk (LDS K1)
+                w32.init(a, b, D);
+                for (uint64_t i = 0; i < 40; i++) {
+                    checks++;
+                    if (w32.x != (a + i * b) % d) {
+                        if (bad++ < 5) printf("walk32 mismatch d=%llu i=%llu\n", (unsigned long long)d, (unsigned long long)i);
+                        break;
+                    }
+                    w32.step(uint32_t(D.d));
+                }
             }
         }
     }
