@@ -1,11 +1,16 @@
 """Summarise rocprofv3 --pmc passes for one kernel into a JSON file.
 
-usage: python tools/pmc_summary.py <pmc_root_dir> <kernel-substring> <out.json> [skip]
+usage: python tools/pmc_summary.py [--launch] <pmc_root_dir> <kernel-substring> <out.json> [skip]
 
 Each sub-directory of <pmc_root_dir> is one rocprofv3 pass
 (<pass>/run_counter_collection.csv).  Per counter the value is averaged over
 the dispatches of the kernel, skipping the first `skip` (warm-up) ones.
 HBM-side bytes per dispatch: FETCH_SIZE and WRITE_SIZE are in KB.
+
+--launch: the substring matches several kernels that together make one
+launch of the path (the XCD-partitioned K1: hash, region and finish passes);
+each counter is then the sum over those kernels of their per-dispatch means,
+i.e. per launch, and the per-kernel means are kept under "per_kernel".
 """
 from __future__ import annotations
 
@@ -48,10 +53,34 @@ def summarise(root: str, kernel: str, skip: int = 3) -> dict:
     return out
 
 
+def summarise_launch(root: str, kernel: str, skip: int = 3) -> dict:
+    names = set()
+    for f in glob.glob(os.path.join(root, "*", "run_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if kernel in r["Kernel_Name"]:
+                names.add(r["Kernel_Name"])
+    per = {n: summarise(root, n, skip) for n in sorted(names)}
+    mean: dict[str, float] = collections.defaultdict(float)
+    for res in per.values():
+        for k, v in res["mean"].items():
+            mean[k] += v
+    out = {"kernels": sorted(names), "mean": dict(mean),
+           "per_kernel": {n: r["mean"] for n, r in per.items()}}
+    if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
+        out["hbm_bytes_per_dispatch"] = (mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024
+    if "TCC_HIT_sum" in mean and "TCC_MISS_sum" in mean:
+        out["l2_hit_rate"] = mean["TCC_HIT_sum"] / max(1.0, mean["TCC_HIT_sum"] + mean["TCC_MISS_sum"])
+    return out
+
+
 if __name__ == "__main__":
-    root, kern, path = sys.argv[1:4]
-    skip = int(sys.argv[4]) if len(sys.argv) > 4 else 3
-    res = summarise(root, kern, skip)
+    argv = sys.argv[1:]
+    launch = argv and argv[0] == "--launch"
+    if launch:
+        argv = argv[1:]
+    root, kern, path = argv[:3]
+    skip = int(argv[3]) if len(argv) > 3 else 3
+    res = (summarise_launch if launch else summarise)(root, kern, skip)
     with open(path, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res["mean"], indent=1))
