@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--xr-fu", type=int, default=0, help="XCD-partitioned K1: finish-pass tile")
     ap.add_argument("--streams", type=int, default=1,
                     help="HIP streams the steps alternate over (launch tails overlap)")
+    ap.add_argument("--k1-legacy", action="store_true",
+                    help="diagnostic: the generic LDS K1 instead of the short-id kernel")
     ap.add_argument("--layout", default="offsets", choices=["offsets", "fixed"],
                     help="id batch layout: bytes + u32 offsets, or fixed-width ids")
     return ap.parse_args()
@@ -110,6 +112,8 @@ def main():
         engine.set_option("variant", args.variant)
     if args.ablate:
         engine.set_option("ablate", args.ablate)
+    if args.k1_legacy:
+        engine.set_option("k1_legacy", 1)
     if args.xr_u:
         engine.set_option("xr_region_u", args.xr_u)
     if args.xr_fu:

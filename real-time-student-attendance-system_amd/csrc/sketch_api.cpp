@@ -76,6 +76,9 @@ struct ske_ctx {
     int xr_region_u = 2;  // XCD-partitioned K1: swipes per lane in the slice passes
     int xr_finish_u = 1;  //   and in the finish pass
     bool lds_ok = false;
+    bool k1_ok = false;       // short-id LDS K1 (sketch_k1.hip) usable
+    int k1_legacy = 0;        // 1: always the generic LDS kernel (A/B diagnostics)
+    uint8_t *zero16 = nullptr;  // 16 zero bytes on the device
     std::string last_hip;
 };
 
@@ -305,10 +308,36 @@ int check_err_flag(ske_ctx *c, int code_if_set) {
     return h ? code_if_set : SKE_OK;
 }
 
+// The short-id LDS kernel (sketch_k1.hip) when the chain, the batch and the
+// options allow it; false: use the generic kernels.
+bool k1_fast_args(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32_t *offs,
+                  uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *out, K1Args *A) {
+    if (!c->k1_ok || c->k1_legacy || c->ablate || !use_lds(c, ch)) return false;
+    if (n >= (uint64_t(1) << 31)) return false;
+    if (!offs && uint64_t(fixed_w) * n >= (uint64_t(1) << 32)) return false;
+    if (!k1_lds_plan(ch, A)) return false;
+    A->bytes = bytes;
+    A->offs = offs;
+    A->slot = slot;
+    A->regs = c->regs;
+    A->out = out;
+    A->err = c->err;
+    A->zero16 = c->zero16;
+    A->n = uint32_t(n);
+    A->nslots = c->nslots;
+    A->fixed_w = fixed_w;
+    return true;
+}
+
 // Enqueue K1 (mode swipes) with the variant the chain selects.
 int launch_k1(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32_t *offs,
               uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *out) {
     if (n == 0) return SKE_OK;
+    K1Args A;
+    if (k1_fast_args(c, ch, bytes, offs, fixed_w, slot, n, out, &A)) {
+        HIPCHK(c, launch_swipes_lds(A, true, c->pb, c->cus, c->st));
+        return SKE_OK;
+    }
     if (k1_variant(c, ch) == 2 && !c->ablate) {
         hipError_t e = hipSuccess;
         void *scr = scratch_get(c->scratch, 16, xr_scratch_bytes(n, ch.nlinks), &e);
@@ -383,6 +412,11 @@ int ske_open(int device, ske_ctx **out) {
         return SKE_ENOMEM;
     }
     c->lds_ok = lds_bloom_setup() == hipSuccess;
+    c->k1_ok = c->lds_ok && k1_lds_setup() == hipSuccess;
+    if (hipMalloc(&c->zero16, 64) != hipSuccess || hipMemset(c->zero16, 0, 64) != hipSuccess) {
+        ske_close(c);
+        return SKE_ENOMEM;
+    }
     *out = c;
     return SKE_OK;
 }
@@ -398,6 +432,7 @@ int ske_close(ske_ctx *c) {
     for (int i = 0; i < 8; i++)
         if (c->stg[i]) (void)hipFree(c->stg[i]);
     if (c->err) (void)hipFree(c->err);
+    if (c->zero16) (void)hipFree(c->zero16);
     if (c->stats) (void)hipFree(c->stats);
     if (c->scratch) scratch_delete(c->scratch);
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -459,6 +494,11 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
     if (!strcmp(name, "ablate")) {
         if (value < 0 || value > 7) return SKE_EINVAL;
         c->ablate = uint32_t(value);
+        return SKE_OK;
+    }
+    if (!strcmp(name, "k1_legacy")) {
+        if (value < 0 || value > 1) return SKE_EINVAL;
+        c->k1_legacy = int(value);
         return SKE_OK;
     }
     if (!strcmp(name, "variant")) {
@@ -591,8 +631,12 @@ int ske_bf_mexists(ske_ctx *c, uint32_t fid, const uint8_t *bytes, const uint32_
         if (rc) return rc;
     }
     const ChainDev ch = chain_dev(*F);
-    HIPCHK(c, launch_swipes(1, ch, use_lds(c, ch), c->pb, s.bytes, s.offs, 0, nullptr, n, nullptr, 0,
-                            dout, nullptr, c->cus, c->st));
+    K1Args A;
+    if (k1_fast_args(c, ch, s.bytes, s.offs, 0, nullptr, n, dout, &A))
+        HIPCHK(c, launch_swipes_lds(A, false, c->pb, c->cus, c->st));
+    else
+        HIPCHK(c, launch_swipes(1, ch, use_lds(c, ch), c->pb, s.bytes, s.offs, 0, nullptr, n, nullptr,
+                                0, dout, nullptr, c->cus, c->st));
     if (mem != SKE_MEM_DEVICE) HIPCHK(c, hipMemcpyAsync(out, dout, n, hipMemcpyDeviceToHost, c->st));
     HIPCHK(c, hipStreamSynchronize(c->st));
     return SKE_OK;

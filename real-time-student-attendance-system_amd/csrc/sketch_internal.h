@@ -30,6 +30,38 @@ hipError_t launch_gen_swipes(const GenDev &g, uint64_t start, uint64_t n, uint8_
 hipError_t launch_gen_members(const GenDev &g, uint64_t start, uint64_t n, uint8_t *bytes,
                               uint32_t *offs, int cus, hipStream_t st);
 
+// sketch_k1.hip -- K1 for chains that fit the LDS image, short-id fast path
+constexpr int kK1MaxLinks = 8;
+constexpr int kLdsBloomMaxBytes = 152 * 1024;  // LDS image budget (160 KiB per CU)
+
+struct K1Link {
+    const uint8_t *bf;   // device bit array (readable to nbytes16)
+    uint64_t m;          // Granlund-Montgomery magic of d
+    uint32_t d;          // bloom->bits (<= 2^31)
+    uint32_t t;          // 2^64 mod d
+    uint32_t sh;         // l - 1 of the magic
+    uint32_t k;          // bloom->hashes
+    uint32_t nbytes16;   // bloom->bytes rounded up to 16
+    uint32_t piece0;     // first 1 KiB LDS piece of the link (LDS offset piece0 * 1024)
+};
+
+struct K1Args {
+    const uint8_t *bytes;
+    const uint32_t *offs;   // nullptr: fixed-width ids (fixed_w bytes each)
+    const uint32_t *slot;
+    uint8_t *regs;
+    uint8_t *out;           // may be nullptr
+    unsigned int *err;      // set when a valid swipe names a slot >= nslots
+    const uint8_t *zero16;  // 16 readable zero bytes (load address of empty ids)
+    uint32_t n, nslots, fixed_w, nlinks, npieces;
+    K1Link link[kK1MaxLinks];
+};
+
+// fills A's chain fields; false when the chain does not fit this variant
+bool k1_lds_plan(const ChainDev &ch, K1Args *A);
+hipError_t launch_swipes_lds(const K1Args &A, bool hll, int tile, int cus, hipStream_t st);
+hipError_t k1_lds_setup();
+
 // sketch_xr.hip -- XCD-partitioned K1 for chains larger than the LDS image
 bool xr_supported(const ChainDev &ch);
 uint64_t xr_scratch_bytes(uint64_t n, int nlinks);

@@ -1,0 +1,332 @@
+// sketch_k1.hip -- K1 for Bloom chains that fit one CU's LDS (C1/C2/C4: the
+// 137 848 B RESERVE 0.01 / 1e5 filter, the reference's 4-link default chain).
+//
+// Same answers as k_swipes (sketch_kernels.hip): per swipe, BF.EXISTS
+// (SBChain_Check: links newest -> oldest, each "present" iff all k probe bits
+// are set, probes in RedisBloom's order (a + i*b) mod 2^64 mod bits) and, if
+// present, PFADD (hllPatLen -> register max) -- attendance_processor.py:109-113
+// and :127-129.  What differs is how it is laid out for gfx950, measured on
+// C2 (1M swipes per launch): the launch is VALU-issue bound at the margin and
+// carries a fixed per-launch cost, so this variant
+//   - issues the LDS image copy (LDS-DMA, one 1 KiB piece per wave-instruction,
+//     a compile-time count per wave) right after the first tile's loads and
+//     hashes that tile while the copy lands -- the hashing no longer waits for
+//     the image;
+//   - loads an id of at most 8 bytes branch-free: the one or two aligned
+//     64-bit words that hold it (an empty id reads a 16-byte zero buffer), a
+//     funnel shift and a length mask;
+//   - hashes MurmurHash64A of a short id in closed form: h = ((seed ^ len*m) ^
+//     t) * m then the finaliser, t = the id word (len < 8) or its mixed block
+//     (len == 8, mixed once for all three hashes);
+//   - walks the probes with the precomputed-increment 32-bit walk
+//     (ProbeWalk32) and reads the image with ds_read_u8;
+//   - keeps 32-bit swipe indices (n < 2^31; the host falls back otherwise).
+// Ids longer than 8 bytes are hashed by the generic routines (murmur_item) on a
+// wave-uniform branch that short-id batches never take.
+#include "sketch_common.h"
+#include "sketch_internal.h"
+
+namespace ske {
+
+constexpr uint32_t kK1Block = 1024;     // threads per block, one block per CU
+constexpr uint32_t kK1Waves = kK1Block / 64;
+constexpr int kK1MaxPieces = 10;        // 1 KiB LDS pieces per wave (152 KiB / 16 waves)
+
+__device__ __forceinline__ uint64_t mul_m(uint64_t x) { return x * kMurmurM; }
+
+__device__ __forceinline__ uint64_t bytes_of(uint64_t w0, uint64_t w1, uint32_t s8, uint32_t len) {
+    // bytes s8 .. s8+len-1 of the 16-byte little-endian word pair w1:w0
+    const uint32_t sh = s8 * 8;
+    const bool hi = sh >= 32;
+    const uint32_t a = hi ? uint32_t(w0 >> 32) : uint32_t(w0);
+    const uint32_t b = hi ? uint32_t(w1) : uint32_t(w0 >> 32);
+    const uint32_t c = hi ? uint32_t(w1 >> 32) : uint32_t(w1);
+    uint32_t lo = __builtin_amdgcn_alignbit(b, a, sh & 31);
+    uint32_t up = __builtin_amdgcn_alignbit(c, b, sh & 31);
+    // keep len bytes (len <= 8)
+    const uint32_t lbits = len * 8;
+    lo &= lbits >= 32 ? 0xffffffffu : ((1u << lbits) - 1u);
+    up &= lbits >= 64 ? 0xffffffffu : (lbits <= 32 ? 0u : ((1u << (lbits - 32)) - 1u));
+    return (uint64_t(up) << 32) | lo;
+}
+
+// Copy this wave's P pieces of the LDS image: piece p of the flat piece list
+// (links in order, each padded to whole 1 KiB pieces) lands at img + p*1024.
+// Pieces past the end repeat the last one (same bytes, same place), so every
+// wave issues exactly P LDS-DMA instructions and the compiler can wait for the
+// tile's own loads with vmcnt(P) while the image is still in flight.  Bytes past
+// a link's 16-byte-padded end read as zero (buffer range check).
+template <int P>
+__device__ __forceinline__ void k1_stage(const K1Args &A, uint8_t *img, uint32_t wave, uint32_t lane) {
+#pragma unroll
+    for (int j = 0; j < P; j++) {
+        uint32_t p = wave + kK1Waves * uint32_t(j);
+        p = p < A.npieces ? p : A.npieces - 1;
+        uint32_t l = 0;
+        while (l + 1 < A.nlinks && p >= A.link[l + 1].piece0) l++;
+        const K1Link &L = A.link[l];
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t *>(L.bf), 0, int(L.nbytes16), 0x00020000);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            r, (__attribute__((address_space(3))) void *)(img + p * 1024), 16,
+            int((p - L.piece0) * 1024 + lane * 16), 0, 0, 0);
+    }
+}
+
+__device__ __forceinline__ bool k1_reg_max(uint8_t *reg, uint32_t rank) {
+    const uint32_t b = uint32_t(reinterpret_cast<uintptr_t>(reg) & 3);
+    uint32_t *w = reinterpret_cast<uint32_t *>(reg - b);
+    const uint32_t sh = b * 8;
+    uint32_t old = *w;
+    while (((old >> sh) & 0xffu) < rank) {
+        const uint32_t prev = atomicCAS(w, old, (old & ~(0xffu << sh)) | (rank << sh));
+        if (prev == old) return true;
+        old = prev;
+    }
+    return false;
+}
+
+// One tile: U swipes per thread (swipe base + u*1024 + tid).  kFirst: the
+// block's first tile, which also stages the LDS image and ends the staging
+// with the block barrier (peeled out of the loop so the wait for the tile's
+// own loads can leave the P image pieces in flight).
+template <bool kHll, int U, int P, bool kFirst>
+__device__ __forceinline__ void k1_tile(const K1Args &A, uint8_t *img, uint32_t base, uint32_t c1) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
+    uint32_t idx[U], len[U], s8[U], sl[U];
+    bool act[U];
+    uint64_t w0[U], w1[U];
+    // ---- loads: ids (offsets, then the 1-2 aligned words), key slots
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint32_t i = base + uint32_t(u) * kK1Block + tid;
+        act[u] = i < c1;
+        idx[u] = act[u] ? i : A.n - 1;  // clamped: every load stays in bounds
+        uint32_t b, e;
+        if (A.offs) {
+            b = A.offs[idx[u]];
+            e = A.offs[idx[u] + 1];
+        } else {
+            b = idx[u] * A.fixed_w;
+            e = b + A.fixed_w;
+        }
+        len[u] = e - b;
+        s8[u] = b & 7;
+        sl[u] = kHll ? A.slot[idx[u]] : 0u;
+        const uint8_t *p0 = len[u] ? A.bytes + (b & ~7u) : A.zero16;
+        const uint8_t *p1 = (s8[u] + len[u] > 8 && len[u] <= 8) ? p0 + 8 : p0;
+        w0[u] = *reinterpret_cast<const uint64_t *>(p0);
+        w1[u] = *reinterpret_cast<const uint64_t *>(p1);
+        idx[u] = i;
+    }
+    if constexpr (kFirst) {
+        __builtin_amdgcn_sched_barrier(0);
+        k1_stage<P>(A, img, wave, lane);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- hashes (a = H(x, bloom seed), b = H(x, a), h = H(x, hll seed))
+    uint64_t ha[U], hb[U], hh[U];
+    bool long_ids = false;
+#pragma unroll
+    for (int u = 0; u < U; u++) long_ids |= act[u] && len[u] > 8;
+    if (__any(long_ids)) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t i = act[u] ? idx[u] : A.n - 1;
+            const uint32_t b = A.offs ? A.offs[i] : i * A.fixed_w;
+            const Item it = load_item(A.bytes, b, b + len[u]);
+            ha[u] = murmur_item(it, kBloomSeed);
+            hb[u] = murmur_item(it, ha[u]);
+            hh[u] = kHll ? murmur_item(it, kHllSeed) : 0;
+        }
+    } else {
+        uint64_t tw[U];
+        bool any8 = false;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            tw[u] = bytes_of(w0[u], w1[u], s8[u], len[u]);
+            any8 |= len[u] == 8;
+        }
+        if (__any(any8)) {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                uint64_t k = mul_m(tw[u]);
+                k ^= k >> 47;
+                k = mul_m(k);
+                tw[u] = len[u] == 8 ? k : tw[u];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t t = tw[u] ^ (uint64_t(len[u]) * kMurmurM);
+            const bool nz = len[u] != 0;
+            ha[u] = mm_final(nz ? mul_m(kBloomSeed ^ t) : kBloomSeed);
+            hb[u] = mm_final(nz ? mul_m(ha[u] ^ t) : ha[u]);
+            if (kHll) hh[u] = mm_final(nz ? mul_m(kHllSeed ^ t) : kHllSeed);
+        }
+    }
+    // ---- HLL: register and rank; the pre-check load flies over the probes
+    uint8_t *reg[U];
+    uint32_t rank[U], cur[U];
+    if constexpr (kHll) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            uint32_t ridx;
+            hll_patlen(hh[u], ridx, rank[u]);
+            const bool ok = act[u] && sl[u] < A.nslots;
+            reg[u] = ok ? A.regs + (uint64_t(sl[u]) << kHllP) + ridx : const_cast<uint8_t *>(A.zero16);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) cur[u] = *reg[u];
+    }
+    // ---- Bloom: newest link first, stop at the first link that has the id
+    const int top = int(A.nlinks) - 1;
+    ProbeWalk32 wk[U];
+    {
+        const K1Link &L = A.link[top];
+        const Divisor D{L.d, L.m, L.t, L.sh, 0};
+#pragma unroll
+        for (int u = 0; u < U; u++) wk[u].init(ha[u], hb[u], D);
+    }
+    if constexpr (kFirst) __syncthreads();  // the image has landed
+    bool valid[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) valid[u] = false;
+    for (int l = top; l >= 0; --l) {
+        const K1Link &L = A.link[l];
+        if (l != top) {
+            const Divisor D{L.d, L.m, L.t, L.sh, 0};
+#pragma unroll
+            for (int u = 0; u < U; u++) wk[u].init(ha[u], hb[u], D);
+        }
+        const uint8_t *limg = img + L.piece0 * 1024;
+        bool alive[U];
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            alive[u] = act[u] && !valid[u];
+            any |= alive[u];
+        }
+        if (!__any(any)) break;
+        for (uint32_t j = 0; j < L.k; j++) {
+            uint32_t byte[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) byte[u] = limg[wk[u].x >> 3];
+            any = false;
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                alive[u] = alive[u] && ((byte[u] >> (wk[u].x & 7)) & 1);
+                any |= alive[u];
+                wk[u].step(L.d);
+            }
+            if (!__any(any)) break;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) valid[u] |= alive[u];
+    }
+    // ---- PFADD of the valid swipes, answers
+    if constexpr (kHll) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (!valid[u]) continue;
+            if (sl[u] >= A.nslots)
+                atomicOr(A.err, 1u);
+            else if (cur[u] < rank[u])  // the pre-check may be stale, never too high
+                k1_reg_max(reg[u], rank[u]);
+        }
+    }
+    if (A.out) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (act[u]) A.out[idx[u]] = valid[u];
+    }
+}
+
+// Each block owns one contiguous chunk of the batch; its first tile (always
+// run, even by a block without swipes) stages the image.
+template <bool kHll, int U, int P>
+__global__ void __launch_bounds__(kK1Block) k_swipes_lds(const K1Args A) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t img[];
+    const uint32_t per_block = (A.n + gridDim.x - 1) / gridDim.x;
+    const uint32_t c0 = blockIdx.x * per_block;
+    const uint32_t c1 = c0 + per_block < A.n ? c0 + per_block : A.n;
+    k1_tile<kHll, U, P, true>(A, img, c0, c1);
+    for (uint32_t base = c0 + kK1Block * U; base < c1; base += kK1Block * U)
+        k1_tile<kHll, U, P, false>(A, img, base, c1);
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+bool k1_lds_plan(const ChainDev &ch, K1Args *A) {
+    if (ch.nlinks < 1 || ch.nlinks > kK1MaxLinks) return false;
+    uint32_t pieces = 0;
+    for (int l = 0; l < ch.nlinks; l++) {
+        const LinkDev &L = ch.link[l];
+        if (L.div.d > (uint64_t(1) << 31) || L.div.d < 64) return false;
+        const uint64_t nb16 = (((L.div.d >> 3) + 15) >> 4) << 4;
+        K1Link &K = A->link[l];
+        K.bf = L.bf;
+        K.m = L.div.m;
+        K.d = uint32_t(L.div.d);
+        K.t = uint32_t(L.div.t);
+        K.sh = L.div.sh;
+        K.k = L.k;
+        K.nbytes16 = uint32_t(nb16);
+        K.piece0 = pieces;
+        pieces += uint32_t((nb16 + 1023) / 1024);
+    }
+    if (pieces * 1024 > lds_bloom_max() || pieces > kK1Waves * kK1MaxPieces) return false;
+    A->nlinks = uint32_t(ch.nlinks);
+    A->npieces = pieces;
+    return true;
+}
+
+template <bool kHll, int U>
+static hipError_t k1_launch_p(const K1Args &A, unsigned grid, hipStream_t st) {
+    const int P = int((A.npieces + kK1Waves - 1) / kK1Waves);
+    const size_t lds = size_t(A.npieces) * 1024;
+#define SKE_P(PP)                                                                                  \
+    case PP:                                                                                       \
+        hipLaunchKernelGGL((k_swipes_lds<kHll, U, PP>), dim3(grid), dim3(kK1Block), lds, st, A);   \
+        break;
+    switch (P) {
+        SKE_P(1) SKE_P(2) SKE_P(3) SKE_P(4) SKE_P(5) SKE_P(6) SKE_P(7) SKE_P(8) SKE_P(9) SKE_P(10)
+    default: return hipErrorInvalidValue;
+    }
+#undef SKE_P
+    return hipGetLastError();
+}
+
+hipError_t launch_swipes_lds(const K1Args &A, bool hll, int tile, int cus, hipStream_t st) {
+    if (A.n == 0) return hipSuccess;
+    const int U = tile >= 4 ? 4 : (tile >= 2 ? 2 : 1);
+    uint64_t g = (uint64_t(A.n) + uint64_t(kK1Block) * U - 1) / (uint64_t(kK1Block) * U);
+    const unsigned grid = unsigned(g < uint64_t(cus) ? (g ? g : 1) : uint64_t(cus));
+    if (hll) {
+        if (U == 4) return k1_launch_p<true, 4>(A, grid, st);
+        if (U == 2) return k1_launch_p<true, 2>(A, grid, st);
+        return k1_launch_p<true, 1>(A, grid, st);
+    }
+    if (U == 4) return k1_launch_p<false, 4>(A, grid, st);
+    if (U == 2) return k1_launch_p<false, 2>(A, grid, st);
+    return k1_launch_p<false, 1>(A, grid, st);
+}
+
+hipError_t k1_lds_setup() {
+    hipError_t e = hipSuccess;
+#define SKE_A(H, UU, PP)                                                                            \
+    e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_swipes_lds<H, UU, PP>),               \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBloomMaxBytes);         \
+    if (e != hipSuccess) return e;
+#define SKE_AP(H, UU)                                                                               \
+    SKE_A(H, UU, 1) SKE_A(H, UU, 2) SKE_A(H, UU, 3) SKE_A(H, UU, 4) SKE_A(H, UU, 5)                 \
+    SKE_A(H, UU, 6) SKE_A(H, UU, 7) SKE_A(H, UU, 8) SKE_A(H, UU, 9) SKE_A(H, UU, 10)
+    SKE_AP(true, 1) SKE_AP(true, 2) SKE_AP(true, 4) SKE_AP(false, 1) SKE_AP(false, 2) SKE_AP(false, 4)
+#undef SKE_AP
+#undef SKE_A
+    return e;
+}
+
+}  // namespace ske

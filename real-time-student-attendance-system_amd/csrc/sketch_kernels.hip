@@ -67,7 +67,7 @@ hipError_t set_stamp_buffer(void *p) {
     } while (0)
 #endif
 
-constexpr int kLdsBloomMax = 152 * 1024;  // LDS image budget (160 KiB per CU)
+constexpr int kLdsBloomMax = kLdsBloomMaxBytes;
 
 // Copy every link's bit array into the LDS image by LDS-DMA
 // (global_load_lds_dwordx4: one wave-instruction moves 1 KiB straight into
