@@ -46,6 +46,10 @@ def parse():
                     help="HIP streams the steps alternate over (launch tails overlap)")
     ap.add_argument("--k1-legacy", action="store_true",
                     help="diagnostic: the generic LDS K1 instead of the short-id kernel")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="1: the K timed steps are recorded once into a HIP graph (one K1 "
+                         "launch per step, each over its own resident batch) and replayed; "
+                         "0: launched one by one from the host")
     ap.add_argument("--layout", default="offsets", choices=["offsets", "fixed"],
                     help="id batch layout: bytes + u32 offsets, or fixed-width ids")
     return ap.parse_args()
@@ -146,6 +150,10 @@ def main():
     for j in range(args.warmup):
         step(j)
     torch.cuda.synchronize()
+    graph = None
+    if args.graph and len(streams) == 1:
+        # the timed steps, recorded (not run) into one uploaded graph
+        graph = engine.capture(lambda: [step(args.warmup + j) for j in range(args.steps)])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -153,12 +161,15 @@ def main():
     e1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
-    for s_ in streams[1:]:
-        s_.wait_stream(stream)
-    for j in range(args.steps):
-        step(args.warmup + j)
-    for s_ in streams[1:]:
-        stream.wait_stream(s_)
+    if graph is not None:
+        graph.launch()
+    else:
+        for s_ in streams[1:]:
+            s_.wait_stream(stream)
+        for j in range(args.steps):
+            step(args.warmup + j)
+        for s_ in streams[1:]:
+            stream.wait_stream(s_)
     e1.record(stream)
     host_enqueue = time.perf_counter() - t0
     torch.cuda.synchronize()
@@ -191,6 +202,9 @@ def main():
         traffic = pmc.get("hbm_bytes_per_dispatch")
         traffic_src = os.path.relpath(pmc_path, ROOT)
     alg_bytes = n * s_io + 64 * probes + 128 * nvalid
+    variant = engine.variant(0)
+    kernel_name = {0: "k_swipes", 1: "k_swipes" if args.k1_legacy else "k_swipes_lds",
+                   2: "k_xr_hash+k_xr_region+k_xr_finish"}[variant]
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     line = {
         "metric": METRIC,
@@ -210,12 +224,13 @@ def main():
                    "hll_keys_per_gpu": w.n_keys, "invalid_frac": w.invalid_frac,
                    "bloom": {"error": w.bf_error, "capacity": w.bf_capacity},
                    "id_bytes": width, "parallelism": f"dp{world} (key-sharded, Bloom replicated)",
-                   "k1_variant": {0: "global-bloom", 1: "lds-bloom", 2: "xcd-regions"}[engine.variant(0)],
-                   "tile": args.tile or 2, "layout": args.layout, "streams": args.streams},
+                   "k1_variant": {0: "global-bloom", 1: "lds-bloom", 2: "xcd-regions"}[variant],
+                   "tile": args.tile or 2, "layout": args.layout, "streams": args.streams,
+                   "launch": "hip-graph" if graph is not None else "host"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "kernel": "k_swipes", "kernel_ms": kern_ms,
+                     "kernel": kernel_name, "kernel_ms": kern_ms,
                      "alg_bytes_per_swipe": alg_bytes / n,
                      "probes_per_swipe": probes / n, "valid_frac": nvalid / n},
         "preload_s": preload_s,
@@ -225,6 +240,8 @@ def main():
         line["cpu_baseline"] = cpu_baseline(engine, pkg, w, p, batches[0], args.cpu_seconds)
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if graph is not None:
+        graph.free()
     for b in batches:
         b.free()
     if world > 1:

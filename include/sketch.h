@@ -190,6 +190,19 @@ int ske_swipes_stats(ske_ctx *ctx, uint32_t fid, const uint8_t *bytes, const uin
 int ske_swipes_variant(ske_ctx *ctx, uint32_t fid);
 int ske_set_option(ske_ctx *ctx, const char *name, int64_t value);
 
+/* ---- stream capture (HIP graphs) ----
+ * Record the device work of the calls made between begin and end on the
+ * context stream (only enqueue-only calls: ske_swipes_async,
+ * ske_swipes_fixed_async) into an executable graph, uploaded to the device;
+ * each ske_graph_launch replays it on the context stream.  A consumer that
+ * processes a ring of fixed device batch slots replays one graph per turn of
+ * the ring instead of one launch per batch (SURVEY.md §8a-1's processor loop at
+ * batch granularity).  The graph keeps the pointers it was recorded with. */
+int ske_capture_begin(ske_ctx *ctx);
+int ske_capture_end(ske_ctx *ctx, void **graph_out);
+int ske_graph_launch(ske_ctx *ctx, void *graph);
+int ske_graph_free(ske_ctx *ctx, void *graph);
+
 /* ---- synthetic stream (device buffers) ---- */
 int ske_gen_members(ske_ctx *ctx, const ske_gen_params_t *p, uint64_t start, uint64_t n,
                     uint8_t *bytes_dev, uint32_t *offs_dev);

@@ -108,6 +108,10 @@ SIGNATURES = {
                                    C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "ske_swipes_variant": (C.c_int, [_CTX, C.c_uint32]),
     "ske_set_option": (C.c_int, [_CTX, C.c_char_p, C.c_int64]),
+    "ske_capture_begin": (C.c_int, [_CTX]),
+    "ske_capture_end": (C.c_int, [_CTX, C.POINTER(C.c_void_p)]),
+    "ske_graph_launch": (C.c_int, [_CTX, _vp]),
+    "ske_graph_free": (C.c_int, [_CTX, _vp]),
     "ske_gen_members": (C.c_int, [_CTX, C.POINTER(GenParams), C.c_uint64, C.c_uint64, _u8p, _u32p]),
     "ske_gen_swipes": (C.c_int, [_CTX, C.POINTER(GenParams), C.c_uint64, C.c_uint64, _u8p, _u32p,
                                  _u32p]),

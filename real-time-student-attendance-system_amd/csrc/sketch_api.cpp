@@ -1076,6 +1076,48 @@ int ske_hll_slab(ske_ctx *c, void **p, uint64_t *bytes) {
     return SKE_OK;
 }
 
+// ------------------------------------------------------------------ graphs
+int ske_capture_begin(ske_ctx *c) {
+    if (!c) return SKE_EINVAL;
+    HIPCHK(c, hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
+    return SKE_OK;
+}
+
+int ske_capture_end(ske_ctx *c, void **graph_out) {
+    if (!c || !graph_out) return SKE_EINVAL;
+    *graph_out = nullptr;
+    hipGraph_t g = nullptr;
+    HIPCHK(c, hipStreamEndCapture(c->st, &g));
+    hipGraphExec_t ge = nullptr;
+    hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) {
+        c->last_hip = std::string("hipGraphInstantiate: ") + hipGetErrorString(e);
+        return SKE_EHIP;
+    }
+    e = hipGraphUpload(ge, c->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+    if (e != hipSuccess) {
+        (void)hipGraphExecDestroy(ge);
+        c->last_hip = std::string("hipGraphUpload: ") + hipGetErrorString(e);
+        return SKE_EHIP;
+    }
+    *graph_out = ge;
+    return SKE_OK;
+}
+
+int ske_graph_launch(ske_ctx *c, void *graph) {
+    if (!c || !graph) return SKE_EINVAL;
+    HIPCHK(c, hipGraphLaunch(hipGraphExec_t(graph), c->st));
+    return SKE_OK;
+}
+
+int ske_graph_free(ske_ctx *c, void *graph) {
+    if (!c) return SKE_EINVAL;
+    if (graph) HIPCHK(c, hipGraphExecDestroy(hipGraphExec_t(graph)));
+    return SKE_OK;
+}
+
 // ------------------------------------------------------------------ generator
 int ske_gen_id_width(const ske_gen_params_t *p) {
     if (!p || p->id_hi <= p->id_lo) return SKE_EINVAL;

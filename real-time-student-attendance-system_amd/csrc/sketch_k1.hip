@@ -32,6 +32,8 @@ constexpr uint32_t kK1Block = 1024;     // threads per block, one block per CU
 constexpr uint32_t kK1Waves = kK1Block / 64;
 constexpr int kK1MaxPieces = 10;        // 1 KiB LDS pieces per wave (152 KiB / 16 waves)
 
+typedef __attribute__((address_space(3))) uint8_t lds_u8;  // an LDS byte
+
 __device__ __forceinline__ uint64_t mul_m(uint64_t x) { return x * kMurmurM; }
 
 __device__ __forceinline__ uint64_t bytes_of(uint64_t w0, uint64_t w1, uint32_t s8, uint32_t len) {
@@ -51,19 +53,19 @@ __device__ __forceinline__ uint64_t bytes_of(uint64_t w0, uint64_t w1, uint32_t 
 }
 
 // Copy this wave's P pieces of the LDS image: piece p of the flat piece list
-// (links in order, each padded to whole 1 KiB pieces) lands at img + p*1024.
+// (links newest first, each padded to whole 1 KiB pieces) lands at img + p*1024.
 // Pieces past the end repeat the last one (same bytes, same place), so every
 // wave issues exactly P LDS-DMA instructions and the compiler can wait for the
 // tile's own loads with vmcnt(P) while the image is still in flight.  Bytes past
 // a link's 16-byte-padded end read as zero (buffer range check).
 template <int P>
-__device__ __forceinline__ void k1_stage(const K1Args &A, uint8_t *img, uint32_t wave, uint32_t lane) {
+__device__ __forceinline__ void k1_stage(const K1Args &A, lds_u8 *img, uint32_t wave, uint32_t lane) {
 #pragma unroll
     for (int j = 0; j < P; j++) {
         uint32_t p = wave + kK1Waves * uint32_t(j);
         p = p < A.npieces ? p : A.npieces - 1;
-        uint32_t l = 0;
-        while (l + 1 < A.nlinks && p >= A.link[l + 1].piece0) l++;
+        uint32_t l = A.nlinks - 1;  // pieces run newest link first
+        while (l > 0 && p >= A.link[l - 1].piece0) l--;
         const K1Link &L = A.link[l];
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint8_t *>(L.bf), 0, int(L.nbytes16), 0x00020000);
@@ -86,14 +88,53 @@ __device__ __forceinline__ bool k1_reg_max(uint8_t *reg, uint32_t rank) {
     return false;
 }
 
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t k1_rsrc(const void *p, uint32_t nbytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, int(nbytes), 0x00020000);
+}
+
+// Probe rounds of one link for U swipes in lock step.  Every swipe keeps
+// RedisBloom's sequential order: `alive` drops at its first unset bit and a
+// dead swipe's later probes are ignored (the bit array is read-only, so the
+// answer and the register updates are exactly the sequential ones).  The
+// rounds carry no wave-level exit: at 90 % members nearly every wave needs
+// all k rounds, and the exit test costs more than the rounds it saves.
+// kTop: the newest link, placed at LDS offset 0.
+template <int U, bool kTop>
+__device__ __forceinline__ void k1_probe_link(const K1Link &L, const lds_u8 *img, ProbeWalk32 *wk,
+                                              uint32_t *alive) {
+    const lds_u8 *limg = kTop ? img : img + L.piece0 * 1024;
+    const uint32_t d = L.d;
+#pragma unroll 4
+    for (uint32_t j = 0; j < L.k; j++) {
+        uint32_t byte[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) byte[u] = limg[wk[u].x >> 3];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            alive[u] &= __builtin_amdgcn_ubfe(byte[u], wk[u].x & 7, 1);
+            // x_{j+1}: the 64-bit running sum's carry selects the increment
+            unsigned c1, c2;
+            const uint32_t lo = __builtin_addc(uint32_t(wk[u].v), uint32_t(wk[u].b), 0u, &c1);
+            const uint32_t hi = __builtin_addc(uint32_t(wk[u].v >> 32), uint32_t(wk[u].b >> 32), c1, &c2);
+            wk[u].v = (uint64_t(hi) << 32) | lo;
+            const uint32_t xn = wk[u].x + (c2 ? wk[u].inc1 : wk[u].inc0);
+            wk[u].x = umin32(xn, xn - d);
+        }
+    }
+}
+
 // One tile: U swipes per thread (swipe base + u*1024 + tid).  kFirst: the
 // block's first tile, which also stages the LDS image and ends the staging
 // with the block barrier (peeled out of the loop so the wait for the tile's
 // own loads can leave the P image pieces in flight).
 template <bool kHll, int U, int P, bool kFirst>
-__device__ __forceinline__ void k1_tile(const K1Args &A, uint8_t *img, uint32_t base, uint32_t c1) {
+__device__ __forceinline__ void k1_tile(const K1Args &A, lds_u8 *img, uint32_t base, uint32_t c1) {
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
+    // 32-bit offsets into the batch buffers (the ids stay below 4 GiB: u32 offsets)
+    const __amdgpu_buffer_rsrc_t r_offs = k1_rsrc(A.offs, 0xfffffff0u);
+    const __amdgpu_buffer_rsrc_t r_slot = k1_rsrc(A.slot, 0xfffffff0u);
+    const __amdgpu_buffer_rsrc_t r_bytes = k1_rsrc(A.bytes, 0xfffffff0u);
     uint32_t idx[U], len[U], s8[U], sl[U];
     bool act[U];
     uint64_t w0[U], w1[U];
@@ -102,22 +143,24 @@ __device__ __forceinline__ void k1_tile(const K1Args &A, uint8_t *img, uint32_t 
     for (int u = 0; u < U; u++) {
         const uint32_t i = base + uint32_t(u) * kK1Block + tid;
         act[u] = i < c1;
-        idx[u] = act[u] ? i : A.n - 1;  // clamped: every load stays in bounds
+        const uint32_t ic = act[u] ? i : A.n - 1;  // clamped: every load stays in bounds
         uint32_t b, e;
         if (A.offs) {
-            b = A.offs[idx[u]];
-            e = A.offs[idx[u] + 1];
+            b = __builtin_amdgcn_raw_buffer_load_b32(r_offs, ic * 4, 0, 0);
+            e = __builtin_amdgcn_raw_buffer_load_b32(r_offs, ic * 4 + 4, 0, 0);
         } else {
-            b = idx[u] * A.fixed_w;
+            b = ic * A.fixed_w;
             e = b + A.fixed_w;
         }
         len[u] = e - b;
         s8[u] = b & 7;
-        sl[u] = kHll ? A.slot[idx[u]] : 0u;
-        const uint8_t *p0 = len[u] ? A.bytes + (b & ~7u) : A.zero16;
-        const uint8_t *p1 = (s8[u] + len[u] > 8 && len[u] <= 8) ? p0 + 8 : p0;
-        w0[u] = *reinterpret_cast<const uint64_t *>(p0);
-        w1[u] = *reinterpret_cast<const uint64_t *>(p1);
+        sl[u] = kHll ? __builtin_amdgcn_raw_buffer_load_b32(r_slot, ic * 4, 0, 0) : 0u;
+        // an empty id reads past the range (zero); a second word only when the
+        // id crosses an 8-byte boundary (else the first word again)
+        const uint32_t o0 = len[u] ? (b & ~7u) : 0xfffffff8u;
+        const uint32_t o1 = (s8[u] + len[u] > 8 && len[u] <= 8) ? o0 + 8 : o0;
+        w0[u] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r_bytes, o0, 0, 0));
+        w1[u] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r_bytes, o1, 0, 0));
         idx[u] = i;
     }
     if constexpr (kFirst) {
@@ -145,7 +188,17 @@ __device__ __forceinline__ void k1_tile(const K1Args &A, uint8_t *img, uint32_t 
         bool any8 = false;
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            tw[u] = bytes_of(w0[u], w1[u], s8[u], len[u]);
+            // bytes s8 .. s8+len-1 of w1:w0, then only the low len bytes kept
+            // (len == 0 never reads t below)
+            const uint32_t sh = s8[u] * 8;
+            const bool hi = sh >= 32;
+            const uint32_t a = hi ? uint32_t(w0[u] >> 32) : uint32_t(w0[u]);
+            const uint32_t bb = hi ? uint32_t(w1[u]) : uint32_t(w0[u] >> 32);
+            const uint32_t c = hi ? uint32_t(w1[u] >> 32) : uint32_t(w1[u]);
+            const uint64_t v = (uint64_t(__builtin_amdgcn_alignbit(c, bb, sh & 31)) << 32) |
+                               __builtin_amdgcn_alignbit(bb, a, sh & 31);
+            const uint32_t drop = (64 - len[u] * 8) & 63;
+            tw[u] = (v << drop) >> drop;
             any8 |= len[u] == 8;
         }
         if (__any(any8)) {
@@ -190,38 +243,25 @@ __device__ __forceinline__ void k1_tile(const K1Args &A, uint8_t *img, uint32_t 
         for (int u = 0; u < U; u++) wk[u].init(ha[u], hb[u], D);
     }
     if constexpr (kFirst) __syncthreads();  // the image has landed
-    bool valid[U];
+    uint32_t alive[U], valid[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) valid[u] = false;
-    for (int l = top; l >= 0; --l) {
-        const K1Link &L = A.link[l];
-        if (l != top) {
-            const Divisor D{L.d, L.m, L.t, L.sh, 0};
+    for (int u = 0; u < U; u++) alive[u] = act[u];
+    k1_probe_link<U, true>(A.link[top], img, wk, alive);
 #pragma unroll
-            for (int u = 0; u < U; u++) wk[u].init(ha[u], hb[u], D);
-        }
-        const uint8_t *limg = img + L.piece0 * 1024;
-        bool alive[U];
+    for (int u = 0; u < U; u++) valid[u] = alive[u];
+    for (int l = top - 1; l >= 0; --l) {
         bool any = false;
 #pragma unroll
         for (int u = 0; u < U; u++) {
             alive[u] = act[u] && !valid[u];
-            any |= alive[u];
+            any |= alive[u] != 0;
         }
         if (!__any(any)) break;
-        for (uint32_t j = 0; j < L.k; j++) {
-            uint32_t byte[U];
+        const K1Link &L = A.link[l];
+        const Divisor D{L.d, L.m, L.t, L.sh, 0};
 #pragma unroll
-            for (int u = 0; u < U; u++) byte[u] = limg[wk[u].x >> 3];
-            any = false;
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                alive[u] = alive[u] && ((byte[u] >> (wk[u].x & 7)) & 1);
-                any |= alive[u];
-                wk[u].step(L.d);
-            }
-            if (!__any(any)) break;
-        }
+        for (int u = 0; u < U; u++) wk[u].init(ha[u], hb[u], D);
+        k1_probe_link<U, false>(L, img, wk, alive);
 #pragma unroll
         for (int u = 0; u < U; u++) valid[u] |= alive[u];
     }
@@ -237,9 +277,10 @@ __device__ __forceinline__ void k1_tile(const K1Args &A, uint8_t *img, uint32_t 
         }
     }
     if (A.out) {
+        const __amdgpu_buffer_rsrc_t r_out = k1_rsrc(A.out, A.n);
 #pragma unroll
-        for (int u = 0; u < U; u++)
-            if (act[u]) A.out[idx[u]] = valid[u];
+        for (int u = 0; u < U; u++)  // lanes past the chunk store out of range (dropped)
+            __builtin_amdgcn_raw_buffer_store_b8(uint8_t(valid[u]), r_out, act[u] ? idx[u] : 0xffffffffu, 0, 0);
     }
 }
 
@@ -247,7 +288,10 @@ __device__ __forceinline__ void k1_tile(const K1Args &A, uint8_t *img, uint32_t 
 // run, even by a block without swipes) stages the image.
 template <bool kHll, int U, int P>
 __global__ void __launch_bounds__(kK1Block) k_swipes_lds(const K1Args A) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t img[];
+    // a static image (not dynamic LDS): its address folds to 0 in the probe
+    // address arithmetic (one VALU op per probe less)
+    __shared__ __attribute__((aligned(16))) uint8_t img_[kLdsBloomMaxBytes];
+    lds_u8 *img = (lds_u8 *)img_;
     const uint32_t per_block = (A.n + gridDim.x - 1) / gridDim.x;
     const uint32_t c0 = blockIdx.x * per_block;
     const uint32_t c1 = c0 + per_block < A.n ? c0 + per_block : A.n;
@@ -262,7 +306,7 @@ __global__ void __launch_bounds__(kK1Block) k_swipes_lds(const K1Args A) {
 bool k1_lds_plan(const ChainDev &ch, K1Args *A) {
     if (ch.nlinks < 1 || ch.nlinks > kK1MaxLinks) return false;
     uint32_t pieces = 0;
-    for (int l = 0; l < ch.nlinks; l++) {
+    for (int l = ch.nlinks - 1; l >= 0; l--) {  // the newest link (probed first) at LDS offset 0
         const LinkDev &L = ch.link[l];
         if (L.div.d > (uint64_t(1) << 31) || L.div.d < 64) return false;
         const uint64_t nb16 = (((L.div.d >> 3) + 15) >> 4) << 4;
@@ -286,10 +330,9 @@ bool k1_lds_plan(const ChainDev &ch, K1Args *A) {
 template <bool kHll, int U>
 static hipError_t k1_launch_p(const K1Args &A, unsigned grid, hipStream_t st) {
     const int P = int((A.npieces + kK1Waves - 1) / kK1Waves);
-    const size_t lds = size_t(A.npieces) * 1024;
 #define SKE_P(PP)                                                                                  \
     case PP:                                                                                       \
-        hipLaunchKernelGGL((k_swipes_lds<kHll, U, PP>), dim3(grid), dim3(kK1Block), lds, st, A);   \
+        hipLaunchKernelGGL((k_swipes_lds<kHll, U, PP>), dim3(grid), dim3(kK1Block), 0, st, A);     \
         break;
     switch (P) {
         SKE_P(1) SKE_P(2) SKE_P(3) SKE_P(4) SKE_P(5) SKE_P(6) SKE_P(7) SKE_P(8) SKE_P(9) SKE_P(10)
@@ -314,19 +357,6 @@ hipError_t launch_swipes_lds(const K1Args &A, bool hll, int tile, int cus, hipSt
     return k1_launch_p<false, 1>(A, grid, st);
 }
 
-hipError_t k1_lds_setup() {
-    hipError_t e = hipSuccess;
-#define SKE_A(H, UU, PP)                                                                            \
-    e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_swipes_lds<H, UU, PP>),               \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBloomMaxBytes);         \
-    if (e != hipSuccess) return e;
-#define SKE_AP(H, UU)                                                                               \
-    SKE_A(H, UU, 1) SKE_A(H, UU, 2) SKE_A(H, UU, 3) SKE_A(H, UU, 4) SKE_A(H, UU, 5)                 \
-    SKE_A(H, UU, 6) SKE_A(H, UU, 7) SKE_A(H, UU, 8) SKE_A(H, UU, 9) SKE_A(H, UU, 10)
-    SKE_AP(true, 1) SKE_AP(true, 2) SKE_AP(true, 4) SKE_AP(false, 1) SKE_AP(false, 2) SKE_AP(false, 4)
-#undef SKE_AP
-#undef SKE_A
-    return e;
-}
+hipError_t k1_lds_setup() { return hipSuccess; }  // static LDS: nothing to raise
 
 }  // namespace ske

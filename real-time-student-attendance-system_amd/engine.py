@@ -76,6 +76,21 @@ class DeviceBatch:
             b.free()
 
 
+class Graph:
+    """An executable HIP graph of recorded sketch calls (ske_capture_end)."""
+
+    def __init__(self, ctx: Context, ptr: int):
+        self.ctx, self.ptr = ctx, ptr
+
+    def launch(self):
+        self.ctx.call("ske_graph_launch", C.c_void_p(self.ptr))
+
+    def free(self):
+        if self.ptr:
+            self.ctx.call("ske_graph_free", C.c_void_p(self.ptr))
+            self.ptr = None
+
+
 class SketchEngine:
     """Device-pointer driver over one libsketch context."""
 
@@ -169,6 +184,18 @@ class SketchEngine:
 
     def sync(self):
         self.ctx.call("ske_sync")
+
+    # ---- HIP graphs: record enqueue-only calls once, replay many times
+    def capture(self, fn) -> "Graph":
+        """Record the device work `fn()` enqueues on the context stream (only
+        *_async calls) into an uploaded executable graph."""
+        self.ctx.call("ske_capture_begin")
+        try:
+            fn()
+        finally:
+            g = C.c_void_p()
+            self.ctx.call("ske_capture_end", C.byref(g))
+        return Graph(self.ctx, g.value)
 
     # ---- HLL reads
     def registers(self, slot: int) -> np.ndarray:

@@ -439,3 +439,34 @@ def test_swipes_c3_filter_xcd_regions_vs_oracle(engine, orc):
     engine.swipes(0, b, out2)
     assert np.array_equal(out2.to_host(np.uint8, b.n), valid)
     assert np.array_equal(engine.registers_all(2 * keys)[keys:], regs)
+
+
+def test_graph_replay_equals_eager(engine):
+    """K1 recorded into a HIP graph (ske_capture_begin/end) and replayed over
+    four resident batches gives the same registers and answers as the same
+    launches made one by one."""
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import DeviceBuffer
+    w = synthetic.WORKLOADS["c2"]
+    engine.reserve(0, w.bf_error, w.bf_capacity)
+    p = engine.gen_params(w)
+    engine.preload(0, p, w.n_members)
+    engine.hll_reserve(2 * w.n_keys)
+    bs = [engine.swipe_batch(p, j * 200_000, 200_000) for j in range(4)]
+    outs = [DeviceBuffer(engine.ctx, b.n) for b in bs]
+    for b, o in zip(bs, outs):
+        engine.swipes_async(0, b, o)
+    engine.sync()
+    eager = engine.registers_all(w.n_keys).copy()
+    answers = [o.to_host(np.uint8, b.n) for b, o in zip(bs, outs)]
+    for b in bs:
+        b.slot.from_host(b.slot.to_host(np.uint32, b.n) + w.n_keys)
+    g = engine.capture(lambda: [engine.swipes_async(0, b, o) for b, o in zip(bs, outs)])
+    for o in outs:
+        o.from_host(np.full(o.nbytes, 7, np.uint8))
+    g.launch()
+    engine.sync()
+    g.free()
+    assert np.array_equal(engine.registers_all(2 * w.n_keys)[w.n_keys:], eager)
+    for a, b, o in zip(answers, bs, outs):
+        assert np.array_equal(o.to_host(np.uint8, b.n), a)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes (one counter group per rocprofv3 run, --pmc only) over the
 # default bench; summary of K1 into gpurun_out/pmc_<tag>.json.
-# usage: TAG=r01 BENCH_ARGS="..." bash tools/gpu_pmc.sh
+# usage: TAG=r01 BENCH_ARGS="..." KERNEL="k_swipes_lds<true" bash tools/gpu_pmc.sh
 mkdir -p gpurun_out/pmc_$TAG
 export TMPDIR=/tmp
 GROUPS_=("FETCH_SIZE" "WRITE_SIZE" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum"
@@ -11,6 +11,6 @@ for c in "${GROUPS_[@]}"; do
   tag=$(echo $c | tr ' ' '_')
   timeout -k 10 300 rocprofv3 --pmc $c -d gpurun_out/pmc_$TAG/$tag -o run --output-format csv -- python bench.py --steps 12 --warmup 3 --no-cpu $BENCH_ARGS > gpurun_out/pmc_$TAG/$tag.log 2>&1; rc=$?
   echo "pmc [$c] rc=$rc"
-  if [ $rc -ne 0 ]; then tail -3 gpurun_out/pmc_$TAG/$tag.log; fi
+  if [ $rc -ne 0 ]; then tail -3 gpurun_out/pmc_$TAG/$tag.log; exit $rc; fi
 done
-python tools/pmc_summary.py gpurun_out/pmc_$TAG "k_swipes<0" gpurun_out/pmc_$TAG.json 3 > /dev/null && echo "summary written"
+python tools/pmc_summary.py gpurun_out/pmc_$TAG "${KERNEL:-k_swipes_lds<true}" gpurun_out/pmc_$TAG.json 3 > /dev/null && echo "summary written"
