@@ -123,64 +123,90 @@ __device__ __forceinline__ void k1_probe_link(const K1Link &L, const lds_u8 *img
     }
 }
 
-// One tile: U swipes per thread (swipe base + u*1024 + tid).  kFirst: the
-// block's first tile, which also stages the LDS image and ends the staging
-// with the block barrier (peeled out of the loop so the wait for the tile's
-// own loads can leave the P image pieces in flight).
-template <bool kHll, int U, int P, bool kFirst>
-__device__ __forceinline__ void k1_tile(const K1Args &A, lds_u8 *img, uint32_t base, uint32_t c1) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
-    // 32-bit offsets into the batch buffers (the ids stay below 4 GiB: u32 offsets)
-    const __amdgpu_buffer_rsrc_t r_offs = k1_rsrc(A.offs, 0xfffffff0u);
-    const __amdgpu_buffer_rsrc_t r_slot = k1_rsrc(A.slot, 0xfffffff0u);
-    const __amdgpu_buffer_rsrc_t r_bytes = k1_rsrc(A.bytes, 0xfffffff0u);
-    uint32_t idx[U], len[U], s8[U], sl[U];
+// A tile: U swipes per thread (swipe base + u*1024 + tid).  The block runs
+// its tiles as a two-stage software pipeline: the next tile's offsets and key
+// slots are loaded while the current tile probes, its id words while the
+// current tile updates registers, so no tile but the first waits for HBM.
+// Loads of a tile past the block's chunk are still issued (clamped to the last
+// swipe: one cache line) so that the number of memory operations in flight
+// does not depend on the branch taken, and the compiler's waits stay exact.
+template <int U>
+struct K1In {  // a tile's loads in flight
+    uint32_t idx[U], b[U], e[U], sl[U];
     bool act[U];
     uint64_t w0[U], w1[U];
-    // ---- loads: ids (offsets, then the 1-2 aligned words), key slots
+};
+
+template <int U>
+struct K1Hot {  // a hashed tile
+    uint32_t idx[U], sl[U], rank[U], cur[U];
+    bool act[U];
+    uint64_t ha[U], hb[U];
+    uint8_t *reg[U];
+    ProbeWalk32 wk[U];
+};
+
+struct K1Rsrc {
+    __amdgpu_buffer_rsrc_t offs, slot, bytes;
+};
+
+template <bool kHll, int U>
+__device__ __forceinline__ void k1_issue_a(const K1Args &A, const K1Rsrc &R, uint32_t base,
+                                           uint32_t c1, K1In<U> &in) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        const uint32_t i = base + uint32_t(u) * kK1Block + tid;
-        act[u] = i < c1;
-        const uint32_t ic = act[u] ? i : A.n - 1;  // clamped: every load stays in bounds
-        uint32_t b, e;
+        const uint32_t i = base + uint32_t(u) * kK1Block + threadIdx.x;
+        in.act[u] = i < c1;
+        in.idx[u] = i;
+        const uint32_t ic = in.act[u] ? i : A.n - 1;  // clamped: every load stays in bounds
         if (A.offs) {
-            b = __builtin_amdgcn_raw_buffer_load_b32(r_offs, ic * 4, 0, 0);
-            e = __builtin_amdgcn_raw_buffer_load_b32(r_offs, ic * 4 + 4, 0, 0);
+            in.b[u] = __builtin_amdgcn_raw_buffer_load_b32(R.offs, ic * 4, 0, 0);
+            in.e[u] = __builtin_amdgcn_raw_buffer_load_b32(R.offs, ic * 4 + 4, 0, 0);
         } else {
-            b = ic * A.fixed_w;
-            e = b + A.fixed_w;
+            in.b[u] = ic * A.fixed_w;
+            in.e[u] = in.b[u] + A.fixed_w;
         }
-        len[u] = e - b;
-        s8[u] = b & 7;
-        sl[u] = kHll ? __builtin_amdgcn_raw_buffer_load_b32(r_slot, ic * 4, 0, 0) : 0u;
+        in.sl[u] = kHll ? __builtin_amdgcn_raw_buffer_load_b32(R.slot, ic * 4, 0, 0) : 0u;
+    }
+}
+
+template <int U>
+__device__ __forceinline__ void k1_issue_b(const K1Rsrc &R, K1In<U> &in) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
         // an empty id reads past the range (zero); a second word only when the
         // id crosses an 8-byte boundary (else the first word again)
-        const uint32_t o0 = len[u] ? (b & ~7u) : 0xfffffff8u;
-        const uint32_t o1 = (s8[u] + len[u] > 8 && len[u] <= 8) ? o0 + 8 : o0;
-        w0[u] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r_bytes, o0, 0, 0));
-        w1[u] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r_bytes, o1, 0, 0));
-        idx[u] = i;
+        const uint32_t len = in.e[u] - in.b[u], s8 = in.b[u] & 7;
+        const uint32_t o0 = len ? (in.b[u] & ~7u) : 0xfffffff8u;
+        const uint32_t o1 = (s8 + len > 8 && len <= 8) ? o0 + 8 : o0;
+        in.w0[u] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(R.bytes, o0, 0, 0));
+        in.w1[u] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(R.bytes, o1, 0, 0));
     }
-    if constexpr (kFirst) {
-        __builtin_amdgcn_sched_barrier(0);
-        k1_stage<P>(A, img, wave, lane);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    // ---- hashes (a = H(x, bloom seed), b = H(x, a), h = H(x, hll seed))
-    uint64_t ha[U], hb[U], hh[U];
+}
+
+// hashes (a = H(x, bloom seed), b = H(x, a), h = H(x, hll seed)), the HLL
+// register and rank with its pre-check load, and the newest link's walk
+template <bool kHll, int U>
+__device__ __forceinline__ void k1_hash(const K1Args &A, const K1In<U> &in, K1Hot<U> &h) {
+    uint32_t len[U];
+    uint64_t hh[U];
     bool long_ids = false;
 #pragma unroll
-    for (int u = 0; u < U; u++) long_ids |= act[u] && len[u] > 8;
+    for (int u = 0; u < U; u++) {
+        len[u] = in.e[u] - in.b[u];
+        h.idx[u] = in.idx[u];
+        h.act[u] = in.act[u];
+        h.sl[u] = in.sl[u];
+        long_ids |= in.act[u] && len[u] > 8;
+    }
     if (__any(long_ids)) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t i = act[u] ? idx[u] : A.n - 1;
+            const uint32_t i = in.act[u] ? in.idx[u] : A.n - 1;
             const uint32_t b = A.offs ? A.offs[i] : i * A.fixed_w;
             const Item it = load_item(A.bytes, b, b + len[u]);
-            ha[u] = murmur_item(it, kBloomSeed);
-            hb[u] = murmur_item(it, ha[u]);
+            h.ha[u] = murmur_item(it, kBloomSeed);
+            h.hb[u] = murmur_item(it, h.ha[u]);
             hh[u] = kHll ? murmur_item(it, kHllSeed) : 0;
         }
     } else {
@@ -190,11 +216,11 @@ __device__ __forceinline__ void k1_tile(const K1Args &A, lds_u8 *img, uint32_t b
         for (int u = 0; u < U; u++) {
             // bytes s8 .. s8+len-1 of w1:w0, then only the low len bytes kept
             // (len == 0 never reads t below)
-            const uint32_t sh = s8[u] * 8;
+            const uint32_t sh = (in.b[u] & 7) * 8;
             const bool hi = sh >= 32;
-            const uint32_t a = hi ? uint32_t(w0[u] >> 32) : uint32_t(w0[u]);
-            const uint32_t bb = hi ? uint32_t(w1[u]) : uint32_t(w0[u] >> 32);
-            const uint32_t c = hi ? uint32_t(w1[u] >> 32) : uint32_t(w1[u]);
+            const uint32_t a = hi ? uint32_t(in.w0[u] >> 32) : uint32_t(in.w0[u]);
+            const uint32_t bb = hi ? uint32_t(in.w1[u]) : uint32_t(in.w0[u] >> 32);
+            const uint32_t c = hi ? uint32_t(in.w1[u] >> 32) : uint32_t(in.w1[u]);
             const uint64_t v = (uint64_t(__builtin_amdgcn_alignbit(c, bb, sh & 31)) << 32) |
                                __builtin_amdgcn_alignbit(bb, a, sh & 31);
             const uint32_t drop = (64 - len[u] * 8) & 63;
@@ -214,78 +240,84 @@ __device__ __forceinline__ void k1_tile(const K1Args &A, lds_u8 *img, uint32_t b
         for (int u = 0; u < U; u++) {
             const uint64_t t = tw[u] ^ (uint64_t(len[u]) * kMurmurM);
             const bool nz = len[u] != 0;
-            ha[u] = mm_final(nz ? mul_m(kBloomSeed ^ t) : kBloomSeed);
-            hb[u] = mm_final(nz ? mul_m(ha[u] ^ t) : ha[u]);
+            h.ha[u] = mm_final(nz ? mul_m(kBloomSeed ^ t) : kBloomSeed);
+            h.hb[u] = mm_final(nz ? mul_m(h.ha[u] ^ t) : h.ha[u]);
             if (kHll) hh[u] = mm_final(nz ? mul_m(kHllSeed ^ t) : kHllSeed);
         }
     }
-    // ---- HLL: register and rank; the pre-check load flies over the probes
-    uint8_t *reg[U];
-    uint32_t rank[U], cur[U];
     if constexpr (kHll) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             uint32_t ridx;
-            hll_patlen(hh[u], ridx, rank[u]);
-            const bool ok = act[u] && sl[u] < A.nslots;
-            reg[u] = ok ? A.regs + (uint64_t(sl[u]) << kHllP) + ridx : const_cast<uint8_t *>(A.zero16);
+            hll_patlen(hh[u], ridx, h.rank[u]);
+            const bool ok = in.act[u] && in.sl[u] < A.nslots;
+            h.reg[u] = ok ? A.regs + (uint64_t(in.sl[u]) << kHllP) + ridx : const_cast<uint8_t *>(A.zero16);
         }
+        // the pre-check load flies over the probes
 #pragma unroll
-        for (int u = 0; u < U; u++) cur[u] = *reg[u];
+        for (int u = 0; u < U; u++) h.cur[u] = *h.reg[u];
     }
-    // ---- Bloom: newest link first, stop at the first link that has the id
+    const K1Link &L = A.link[A.nlinks - 1];
+    const Divisor D{L.d, L.m, L.t, L.sh, 0};
+#pragma unroll
+    for (int u = 0; u < U; u++) h.wk[u].init(h.ha[u], h.hb[u], D);
+}
+
+// Bloom: newest link first, stop at the first link that has the id
+template <int U>
+__device__ __forceinline__ void k1_probe(const K1Args &A, const lds_u8 *img, K1Hot<U> &h,
+                                         uint32_t *valid) {
     const int top = int(A.nlinks) - 1;
-    ProbeWalk32 wk[U];
-    {
-        const K1Link &L = A.link[top];
-        const Divisor D{L.d, L.m, L.t, L.sh, 0};
+    uint32_t alive[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) wk[u].init(ha[u], hb[u], D);
-    }
-    if constexpr (kFirst) __syncthreads();  // the image has landed
-    uint32_t alive[U], valid[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) alive[u] = act[u];
-    k1_probe_link<U, true>(A.link[top], img, wk, alive);
+    for (int u = 0; u < U; u++) alive[u] = h.act[u];
+    k1_probe_link<U, true>(A.link[top], img, h.wk, alive);
 #pragma unroll
     for (int u = 0; u < U; u++) valid[u] = alive[u];
     for (int l = top - 1; l >= 0; --l) {
         bool any = false;
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            alive[u] = act[u] && !valid[u];
+            alive[u] = h.act[u] && !valid[u];
             any |= alive[u] != 0;
         }
         if (!__any(any)) break;
         const K1Link &L = A.link[l];
         const Divisor D{L.d, L.m, L.t, L.sh, 0};
 #pragma unroll
-        for (int u = 0; u < U; u++) wk[u].init(ha[u], hb[u], D);
-        k1_probe_link<U, false>(L, img, wk, alive);
+        for (int u = 0; u < U; u++) h.wk[u].init(h.ha[u], h.hb[u], D);
+        k1_probe_link<U, false>(L, img, h.wk, alive);
 #pragma unroll
         for (int u = 0; u < U; u++) valid[u] |= alive[u];
     }
-    // ---- PFADD of the valid swipes, answers
+}
+
+// PFADD of the valid swipes, answers
+template <bool kHll, int U>
+__device__ __forceinline__ void k1_commit(const K1Args &A, const K1Hot<U> &h, const uint32_t *valid) {
     if constexpr (kHll) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             if (!valid[u]) continue;
-            if (sl[u] >= A.nslots)
+            if (h.sl[u] >= A.nslots)
                 atomicOr(A.err, 1u);
-            else if (cur[u] < rank[u])  // the pre-check may be stale, never too high
-                k1_reg_max(reg[u], rank[u]);
+            else if (h.cur[u] < h.rank[u])  // the pre-check may be stale, never too high
+                k1_reg_max(h.reg[u], h.rank[u]);
         }
     }
     if (A.out) {
         const __amdgpu_buffer_rsrc_t r_out = k1_rsrc(A.out, A.n);
 #pragma unroll
         for (int u = 0; u < U; u++)  // lanes past the chunk store out of range (dropped)
-            __builtin_amdgcn_raw_buffer_store_b8(uint8_t(valid[u]), r_out, act[u] ? idx[u] : 0xffffffffu, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8(uint8_t(valid[u]), r_out, h.act[u] ? h.idx[u] : 0xffffffffu,
+                                                 0, 0);
     }
 }
 
-// Each block owns one contiguous chunk of the batch; its first tile (always
-// run, even by a block without swipes) stages the image.
+// Each block owns one contiguous chunk of the batch.  Its first tile is
+// loaded, the LDS image copy issued behind it (P LDS-DMA pieces per wave) and
+// the tile hashed while the copy lands; then the pipelined tile loop.  A block
+// without swipes still stages and joins the barrier.
 template <bool kHll, int U, int P>
 __global__ void __launch_bounds__(kK1Block) k_swipes_lds(const K1Args A) {
     // a static image (not dynamic LDS): its address folds to 0 in the probe
@@ -295,9 +327,32 @@ __global__ void __launch_bounds__(kK1Block) k_swipes_lds(const K1Args A) {
     const uint32_t per_block = (A.n + gridDim.x - 1) / gridDim.x;
     const uint32_t c0 = blockIdx.x * per_block;
     const uint32_t c1 = c0 + per_block < A.n ? c0 + per_block : A.n;
-    k1_tile<kHll, U, P, true>(A, img, c0, c1);
-    for (uint32_t base = c0 + kK1Block * U; base < c1; base += kK1Block * U)
-        k1_tile<kHll, U, P, false>(A, img, base, c1);
+    // 32-bit offsets into the batch buffers (u32 offsets keep the ids below 4 GiB)
+    K1Rsrc R;
+    R.offs = k1_rsrc(A.offs, 0xfffffff0u);
+    R.slot = k1_rsrc(A.slot, 0xfffffff0u);
+    R.bytes = k1_rsrc(A.bytes, 0xfffffff0u);
+    K1In<U> in;
+    K1Hot<U> hot;
+    k1_issue_a<kHll, U>(A, R, c0, c1, in);
+    k1_issue_b<U>(R, in);
+    __builtin_amdgcn_sched_barrier(0);
+    k1_stage<P>(A, img, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x & 63);
+    __builtin_amdgcn_sched_barrier(0);
+    k1_hash<kHll, U>(A, in, hot);
+    __syncthreads();  // the image has landed
+    for (uint32_t base = c0;;) {
+        const uint32_t next = base + kK1Block * U;
+        const bool more = next < c1;  // block-uniform
+        k1_issue_a<kHll, U>(A, R, next, c1, in);
+        uint32_t valid[U];
+        k1_probe<U>(A, img, hot, valid);
+        k1_issue_b<U>(R, in);
+        k1_commit<kHll, U>(A, hot, valid);
+        if (!more) break;
+        k1_hash<kHll, U>(A, in, hot);
+        base = next;
+    }
 }
 
 // ---------------------------------------------------------------------------
