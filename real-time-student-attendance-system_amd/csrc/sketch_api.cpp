@@ -878,6 +878,11 @@ int ske_diag_set_stamp_buffer(ske_ctx *c, void *dev_ptr) {
     HIPCHK(c, ske::set_stamp_buffer(dev_ptr));
     return SKE_OK;
 }
+int ske_diag_set_k1_stamp_buffer(ske_ctx *c, void *dev_ptr) {
+    if (!c) return SKE_EINVAL;
+    HIPCHK(c, ske::set_k1_stamp_buffer(dev_ptr));
+    return SKE_OK;
+}
 #endif
 
 int ske_swipes_stats(ske_ctx *c, uint32_t fid, const uint8_t *bytes, const uint32_t *offs,

@@ -61,6 +61,7 @@ struct K1Args {
 bool k1_lds_plan(const ChainDev &ch, K1Args *A);
 hipError_t launch_swipes_lds(const K1Args &A, bool hll, int tile, int cus, hipStream_t st);
 hipError_t k1_lds_setup();
+hipError_t set_k1_stamp_buffer(void *p);  // -DSKE_STAMPS diagnostic build only
 
 // sketch_xr.hip -- XCD-partitioned K1 for chains larger than the LDS image
 bool xr_supported(const ChainDev &ch);

@@ -34,6 +34,28 @@ constexpr int kK1MaxPieces = 10;        // 1 KiB LDS pieces per wave (152 KiB / 
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;  // an LDS byte
 
+// Diagnostic phase stamps (tools/stamps, built only with -DSKE_STAMPS; the
+// product library has none): lane 0 of every wave records s_memtime at fixed
+// points of its first two tiles into a side buffer no output depends on.
+#ifdef SKE_STAMPS
+__device__ unsigned long long *ske_k1_stamp_buf;
+hipError_t set_k1_stamp_buffer(void *p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(ske_k1_stamp_buf), &p, sizeof(void *));
+}
+#define K1_STAMP(k)                                                                                \
+    do {                                                                                           \
+        __builtin_amdgcn_sched_barrier(0);                                                         \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                \
+        __builtin_amdgcn_sched_barrier(0);                                                         \
+        if ((threadIdx.x & 63) == 0 && (k) < 16)                                                   \
+            ske_k1_stamp_buf[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 16 + (k)] = t_;              \
+    } while (0)
+#else
+#define K1_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
+
 __device__ __forceinline__ uint64_t mul_m(uint64_t x) { return x * kMurmurM; }
 
 __device__ __forceinline__ uint64_t bytes_of(uint64_t w0, uint64_t w1, uint32_t s8, uint32_t len) {
@@ -334,25 +356,37 @@ __global__ void __launch_bounds__(kK1Block) k_swipes_lds(const K1Args A) {
     R.bytes = k1_rsrc(A.bytes, 0xfffffff0u);
     K1In<U> in;
     K1Hot<U> hot;
+    K1_STAMP(0);
+    // the tile's loads first, then the image copy behind them: the hash waits
+    // for its own loads only (vmcnt(P)) while the P pieces land.  (Copy first,
+    // loads behind: measured 3 % slower at 524k swipes.)
     k1_issue_a<kHll, U>(A, R, c0, c1, in);
     k1_issue_b<U>(R, in);
     __builtin_amdgcn_sched_barrier(0);
     k1_stage<P>(A, img, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x & 63);
     __builtin_amdgcn_sched_barrier(0);
+    K1_STAMP(1);
     k1_hash<kHll, U>(A, in, hot);
+    K1_STAMP(2);
     __syncthreads();  // the image has landed
-    for (uint32_t base = c0;;) {
+    K1_STAMP(3);
+    [[maybe_unused]] int it = 0;  // stamp index only
+    for (uint32_t base = c0;; it++) {
         const uint32_t next = base + kK1Block * U;
         const bool more = next < c1;  // block-uniform
         k1_issue_a<kHll, U>(A, R, next, c1, in);
         uint32_t valid[U];
         k1_probe<U>(A, img, hot, valid);
+        K1_STAMP(4 + 3 * it);
         k1_issue_b<U>(R, in);
         k1_commit<kHll, U>(A, hot, valid);
+        K1_STAMP(5 + 3 * it);
         if (!more) break;
         k1_hash<kHll, U>(A, in, hot);
+        K1_STAMP(6 + 3 * it);
         base = next;
     }
+    K1_STAMP(15);
 }
 
 // ---------------------------------------------------------------------------
