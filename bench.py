@@ -5,9 +5,14 @@ One step = one K1 launch over one resident batch of synthetic swipes (C2: 1M
 swipes, 7-digit ids from a 100k-student population, 10 % invalid, 50
 lecture-day HLL keys, Bloom RESERVE 0.01 / 100k preloaded).  Inputs are
 generated on the GPU and resident in HBM before timing; each step consumes a
-distinct batch of the stream.  N>1: one process per GPU (torchrun), each rank
-runs its own stream over its own key shard with the Bloom replicated
-(no data-path collective; weak scaling).
+distinct batch of the stream.  The K timed steps are recorded once into a HIP
+graph and replayed (one K1 launch per step, back to back on one stream), so
+the kernel's average duration is the per-step device time that rocprofv3
+reports.  (--streams 2 alternates the steps over two streams, so one batch's
+launch tail overlaps the next batch's head: about 6 % more swipes/s at C2, but
+overlapping launches have no single duration.)  N>1: one process per GPU
+(torchrun), each rank runs its own stream over its own key shard with the
+Bloom replicated (no data-path collective; weak scaling).
 
 Prints ONE JSON line on rank 0.
 """
@@ -29,8 +34,8 @@ METRIC = "swipes/sec (fused BF.EXISTS+PFADD) at 1/2/4/8 GPUs; % of HBM peak"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--batch", type=int, default=0, help="swipes per step (default: config)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -46,10 +51,13 @@ def parse():
                     help="HIP streams the steps alternate over (launch tails overlap)")
     ap.add_argument("--k1-legacy", action="store_true",
                     help="diagnostic: the generic LDS K1 instead of the short-id kernel")
+    ap.add_argument("--k1-grid", type=int, default=0,
+                    help="blocks of the short-id LDS K1 (0: one per CU); with --streams S > 1 "
+                         "consecutive steps run side by side on disjoint CUs")
     ap.add_argument("--graph", type=int, default=1,
-                    help="1: the K timed steps are recorded once into a HIP graph (one K1 "
-                         "launch per step, each over its own resident batch) and replayed; "
-                         "0: launched one by one from the host")
+                    help="with --streams 1: 1 = the K timed steps are recorded once into a "
+                         "HIP graph (one K1 launch per step, each over its own resident batch) "
+                         "and replayed; 0 = launched one by one from the host")
     ap.add_argument("--layout", default="offsets", choices=["offsets", "fixed"],
                     help="id batch layout: bytes + u32 offsets, or fixed-width ids")
     return ap.parse_args()
@@ -116,6 +124,8 @@ def main():
         engine.set_option("variant", args.variant)
     if args.ablate:
         engine.set_option("ablate", args.ablate)
+    if args.k1_grid:
+        engine.set_option("k1_grid", args.k1_grid)
     if args.k1_legacy:
         engine.set_option("k1_legacy", 1)
     if args.xr_u:
@@ -159,6 +169,11 @@ def main():
     torch.cuda.synchronize()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
+    # several streams: every launch is bracketed by its own event pair on the
+    # stream it runs on, so the kernel's average duration is measured even
+    # though consecutive launches overlap
+    per = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)] if len(streams) > 1 else []
     t0 = time.perf_counter()
     e0.record(stream)
     if graph is not None:
@@ -167,7 +182,11 @@ def main():
         for s_ in streams[1:]:
             s_.wait_stream(stream)
         for j in range(args.steps):
+            if per:
+                per[j][0].record(streams[(args.warmup + j) % len(streams)])
             step(args.warmup + j)
+            if per:
+                per[j][1].record(streams[(args.warmup + j) % len(streams)])
         for s_ in streams[1:]:
             stream.wait_stream(s_)
     e1.record(stream)
@@ -177,13 +196,15 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     torch.cuda.synchronize()
-    # average launch duration of K1 on its stream (HIP events around the K
-    # back-to-back launches; includes the inter-kernel gaps, so an upper bound)
-    kern_ms = e0.elapsed_time(e1) / args.steps
+    # average launch duration of K1: one stream -- HIP events around the K
+    # back-to-back launches (includes the inter-kernel gaps, so an upper
+    # bound); several streams -- the mean of the per-launch event pairs
+    step_ms = e0.elapsed_time(e1) / args.steps
+    kern_ms = sum(a.elapsed_time(b) for a, b in per) / len(per) if per else step_ms
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, kern_ms, step_ms], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+        elapsed, kern_ms, step_ms = float(t[0]), float(t[1]), float(t[2])
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * n * args.steps / elapsed
@@ -231,6 +252,8 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src,
                      "kernel": kernel_name, "kernel_ms": kern_ms,
+                     "device_ms_per_step": step_ms,
+                     "achieved_per_step": alg_bytes / (step_ms * 1e-3) / 1e9,
                      "alg_bytes_per_swipe": alg_bytes / n,
                      "probes_per_swipe": probes / n, "valid_frac": nvalid / n},
         "preload_s": preload_s,

@@ -78,7 +78,12 @@ struct ske_ctx {
     bool lds_ok = false;
     bool k1_ok = false;       // short-id LDS K1 (sketch_k1.hip) usable
     int k1_legacy = 0;        // 1: always the generic LDS kernel (A/B diagnostics)
+    int k1_grid = 0;          // blocks of the short-id LDS K1 (0: one per CU)
     uint8_t *zero16 = nullptr;  // 16 zero bytes on the device
+    // the XCD-partitioned K1 keeps per-launch state in the context scratch:
+    // a launch on another stream first waits for the previous one
+    hipEvent_t xr_done = nullptr;
+    hipStream_t xr_stream = nullptr;
     std::string last_hip;
 };
 
@@ -335,7 +340,7 @@ int launch_k1(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32
     if (n == 0) return SKE_OK;
     K1Args A;
     if (k1_fast_args(c, ch, bytes, offs, fixed_w, slot, n, out, &A)) {
-        HIPCHK(c, launch_swipes_lds(A, true, c->pb, c->cus, c->st));
+        HIPCHK(c, launch_swipes_lds(A, true, c->pb, c->k1_grid ? c->k1_grid : c->cus, c->st));
         return SKE_OK;
     }
     if (k1_variant(c, ch) == 2 && !c->ablate) {
@@ -345,8 +350,12 @@ int launch_k1(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32
             c->last_hip = hipGetErrorString(e);
             return SKE_ENOMEM;
         }
+        if (!c->xr_done) HIPCHK(c, hipEventCreateWithFlags(&c->xr_done, hipEventDisableTiming));
+        if (c->xr_stream && c->xr_stream != c->st) HIPCHK(c, hipStreamWaitEvent(c->st, c->xr_done, 0));
         HIPCHK(c, launch_swipes_xr(ch, bytes, offs, fixed_w, slot, n, c->regs, c->nslots, out,
                                    scr, c->err, c->cus, c->xr_region_u, c->xr_finish_u, c->st));
+        HIPCHK(c, hipEventRecord(c->xr_done, c->st));
+        c->xr_stream = c->st;
         return SKE_OK;
     }
     if (c->ablate) {
@@ -433,6 +442,7 @@ int ske_close(ske_ctx *c) {
         if (c->stg[i]) (void)hipFree(c->stg[i]);
     if (c->err) (void)hipFree(c->err);
     if (c->zero16) (void)hipFree(c->zero16);
+    if (c->xr_done) (void)hipEventDestroy(c->xr_done);
     if (c->stats) (void)hipFree(c->stats);
     if (c->scratch) scratch_delete(c->scratch);
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -494,6 +504,11 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
     if (!strcmp(name, "ablate")) {
         if (value < 0 || value > 7) return SKE_EINVAL;
         c->ablate = uint32_t(value);
+        return SKE_OK;
+    }
+    if (!strcmp(name, "k1_grid")) {
+        if (value < 0 || value > 65535) return SKE_EINVAL;
+        c->k1_grid = int(value);
         return SKE_OK;
     }
     if (!strcmp(name, "k1_legacy")) {

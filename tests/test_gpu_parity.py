@@ -470,3 +470,38 @@ def test_graph_replay_equals_eager(engine):
     assert np.array_equal(engine.registers_all(2 * w.n_keys)[w.n_keys:], eager)
     for a, b, o in zip(answers, bs, outs):
         assert np.array_equal(o.to_host(np.uint8, b.n), a)
+
+
+@pytest.mark.parametrize("variant", [-1, 2])
+def test_two_streams_equal_one_stream(engine, variant):
+    """Launches alternating over two HIP streams (overlapping K1 kernels; the
+    XCD-partitioned variant serialises on its scratch) leave the same
+    registers and answers as the same launches on one stream."""
+    import torch
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import DeviceBuffer
+    w = synthetic.WORKLOADS["c2"]
+    engine.set_option("variant", variant)
+    engine.reserve(0, w.bf_error, w.bf_capacity)
+    p = engine.gen_params(w)
+    engine.preload(0, p, w.n_members)
+    engine.hll_reserve(2 * w.n_keys)
+    bs = [engine.swipe_batch(p, j * 150_000, 150_000) for j in range(6)]
+    outs = [DeviceBuffer(engine.ctx, b.n) for b in bs]
+    for b, o in zip(bs, outs):
+        engine.swipes_async(0, b, o)
+    engine.sync()
+    one = engine.registers_all(w.n_keys).copy()
+    answers = [o.to_host(np.uint8, b.n) for b, o in zip(bs, outs)]
+    for b in bs:
+        b.slot.from_host(b.slot.to_host(np.uint32, b.n) + w.n_keys)
+    st = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    for j, (b, o) in enumerate(zip(bs, outs)):
+        engine.set_stream(st[j % 2].cuda_stream)
+        engine.swipes_async(0, b, o)
+    torch.cuda.synchronize()
+    engine.set_stream(None)
+    assert np.array_equal(engine.registers_all(2 * w.n_keys)[w.n_keys:], one)
+    for a, b, o in zip(answers, bs, outs):
+        assert np.array_equal(o.to_host(np.uint8, b.n), a)
