@@ -497,7 +497,9 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
         return SKE_OK;
     }
     if (!strcmp(name, "xr_region_u") || !strcmp(name, "xr_finish_u")) {
-        if (value != 1 && value != 2 && value != 4 && value != 8) return SKE_EINVAL;
+        // xr_region_u < 0: the per-step slice loop instead of the batched one
+        const int64_t a = (name[3] == 'r' && value < 0) ? -value : value;
+        if (a != 1 && a != 2 && a != 4 && a != 8) return SKE_EINVAL;
         (name[3] == 'r' ? c->xr_region_u : c->xr_finish_u) = int(value);
         return SKE_OK;
     }

@@ -146,6 +146,80 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// The slice pass with every probe of a tile in flight at once (k <= 16): the
+// walk for all k steps is computed first and each in-slice probe issued as a
+// buffer load, then the bits are tested.  No wave-level exit between steps: a
+// member (90 % of the swipes) is alive in every slice through all k steps, so
+// a per-step exit test only serialises k memory round trips (the loop above
+// waits for every probe before taking the next step).
+constexpr int kXrBatchK = 16;
+
+template <int U>
+__global__ void __launch_bounds__(256)
+    k_xr_region_b(const ChainDev ch, uint64_t n, uint64_t chunk, XrState st,
+                  unsigned long long *__restrict__ fail) {
+    const uint32_t T = blockDim.x, tid = threadIdx.x;
+    const uint32_t region = blockIdx.x % kRegions;
+    const uint64_t c0 = uint64_t(blockIdx.x / kRegions) * chunk;
+    const uint64_t c1 = c0 + chunk < n ? c0 + chunk : n;
+    const uint64_t nwaves = (n + 63) / 64;
+    for (int l = ch.nlinks - 1; l >= 0; --l) {
+        const LinkDev &L = ch.link[l];
+        const uint32_t d = uint32_t(L.div.d), t = uint32_t(L.div.t), k = L.k;
+        const uint32_t slice = ((d + kRegions - 1) / kRegions + 1023) & ~1023u;
+        const uint32_t lo = region * slice;
+        const uint32_t len = lo >= d ? 0u : (d - lo < slice ? d - lo : slice);
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t *>(L.bf), 0, int(d >> 3), 0x00020000);
+        for (uint64_t base = c0; base < c1; base += uint64_t(T) * U) {
+            uint32_t x[U], inc0[U], inc1[U], wrap[U], ok[U];
+            bool act[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint64_t i = base + uint64_t(u) * T + tid;
+                act[u] = i < c1;
+                const uint64_t ic = act[u] ? i : c0;
+                x[u] = st.x0[uint64_t(l) * n + ic];
+                inc0[u] = st.bm[uint64_t(l) * n + ic];
+                wrap[u] = st.wrap[uint64_t(l) * n + ic];
+            }
+            uint32_t byte[U][kXrBatchK], pos[U][kXrBatchK];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t m = inc0[u] - t;
+                inc1[u] = umin32(m, m + d);
+#pragma unroll
+                for (int j = 0; j < kXrBatchK; j++) {
+                    // a probe outside the slice (or past k) reads out of range: 0,
+                    // and is not tested below
+                    const bool mine = uint32_t(j) < k && (x[u] - lo) < len;
+                    pos[u][j] = x[u];
+                    byte[u][j] = __builtin_amdgcn_raw_buffer_load_b8(
+                        rsrc, mine ? (x[u] >> 3) : 0x80000000u, 0, 0);
+                    x[u] += ((wrap[u] >> (j + 1)) & 1) ? inc1[u] : inc0[u];
+                    x[u] = umin32(x[u], x[u] - d);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                ok[u] = act[u];
+#pragma unroll
+                for (int j = 0; j < kXrBatchK; j++) {
+                    const bool mine = uint32_t(j) < k && (pos[u][j] - lo) < len;
+                    ok[u] &= mine ? __builtin_amdgcn_ubfe(byte[u][j], pos[u][j] & 7, 1) : 1u;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const unsigned long long m = __ballot(act[u] && !ok[u]);
+                const uint64_t first = base + uint64_t(u) * T + (tid & ~63u);
+                if ((tid & 63) == 0 && first < c1)
+                    fail[(uint64_t(region) * ch.nlinks + l) * nwaves + first / 64] = m;
+            }
+        }
+    }
+}
+
 template <int U>
 __global__ void __launch_bounds__(256)
     k_xr_finish(const ChainDev ch, const uint32_t *__restrict__ slot, uint64_t n,
@@ -235,14 +309,20 @@ hipError_t launch_swipes_xr(const ChainDev &ch, const uint8_t *bytes, const uint
     s.hll = p + 3 * uint64_t(ch.nlinks) * n;
     hipLaunchKernelGGL(k_xr_hash, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, ch, bytes, offs,
                        fixed_w, n, s);
-    const int U = region_u >= 8 ? 8 : (region_u >= 4 ? 4 : (region_u >= 2 ? 2 : 1));
+    const int ru = region_u < 0 ? -region_u : region_u;
+    const int U = ru >= 8 ? 8 : (ru >= 4 ? 4 : (ru >= 2 ? 2 : 1));
     const uint64_t tile = 256 * uint64_t(U);
     uint64_t chunks = uint64_t(cus) * 8 / kRegions;  // 8 blocks per CU in total
     uint64_t chunk = (n + chunks - 1) / chunks;
     chunk = (chunk + tile - 1) / tile * tile;
     chunks = (n + chunk - 1) / chunk;
     const dim3 g(unsigned(chunks * kRegions));
-    if (U == 8) hipLaunchKernelGGL(k_xr_region<8>, g, dim3(256), 0, st, ch, n, chunk, s, fail);
+    bool batch = region_u > 0;  // region_u < 0: the per-step loop (A/B diagnostics)
+    for (int l = 0; l < ch.nlinks; l++) batch &= ch.link[l].k <= uint32_t(kXrBatchK);
+    if (batch) {
+        if (U >= 2) hipLaunchKernelGGL(k_xr_region_b<2>, g, dim3(256), 0, st, ch, n, chunk, s, fail);
+        else hipLaunchKernelGGL(k_xr_region_b<1>, g, dim3(256), 0, st, ch, n, chunk, s, fail);
+    } else if (U == 8) hipLaunchKernelGGL(k_xr_region<8>, g, dim3(256), 0, st, ch, n, chunk, s, fail);
     else if (U == 4) hipLaunchKernelGGL(k_xr_region<4>, g, dim3(256), 0, st, ch, n, chunk, s, fail);
     else if (U == 2) hipLaunchKernelGGL(k_xr_region<2>, g, dim3(256), 0, st, ch, n, chunk, s, fail);
     else hipLaunchKernelGGL(k_xr_region<1>, g, dim3(256), 0, st, ch, n, chunk, s, fail);
