@@ -131,6 +131,17 @@ int ske_bf_link_info(ske_ctx *ctx, uint32_t fid, uint32_t link, ske_bf_link_t *o
 int ske_bf_export_link(ske_ctx *ctx, uint32_t fid, uint32_t link, uint8_t *out, uint64_t cap);
 int ske_bf_import_link(ske_ctx *ctx, uint32_t fid, uint32_t link, const uint8_t *in,
                        uint64_t nbytes);
+/* BF.LOADCHUNK key <iter> <data>: bytes [offset, offset + nbytes) of one link's
+ * bit array (SBChain_LoadEncodedChunk); the range must lie inside the link. */
+int ske_bf_link_write(ske_ctx *ctx, uint32_t fid, uint32_t link, uint64_t offset,
+                      const uint8_t *in, uint64_t nbytes);
+/* BF.LOADCHUNK key 1 <header>: a chain with exactly the given links (geometry
+ * and sizes as dumped by BF.SCANDUMP's header chunk, zeroed bit arrays; the
+ * data chunks then go in through ske_bf_import_link / the facade).  Each
+ * link needs bits == bytes * 8, 1 <= hashes <= 64.  SKE_EEXISTS if fid exists.
+ *   replaces: SB_NewChainFromHeader (RedisBloom src/sb.c) behind BF.LOADCHUNK */
+int ske_bf_load_header(ske_ctx *ctx, uint32_t fid, const ske_bf_link_t *links, uint32_t nlinks,
+                       uint64_t inserted, uint32_t expansion, int nonscaling);
 
 /* ---- HyperLogLog register slab (Redis p=14, one byte per register) ---- */
 int ske_hll_reserve(ske_ctx *ctx, uint32_t nslots);  /* grow the slab to >= nslots keys */

@@ -83,6 +83,9 @@ SIGNATURES = {
     "ske_bf_link_info": (C.c_int, [_CTX, C.c_uint32, C.c_uint32, C.POINTER(BfLink)]),
     "ske_bf_export_link": (C.c_int, [_CTX, C.c_uint32, C.c_uint32, _u8p, C.c_uint64]),
     "ske_bf_import_link": (C.c_int, [_CTX, C.c_uint32, C.c_uint32, _u8p, C.c_uint64]),
+    "ske_bf_link_write": (C.c_int, [_CTX, C.c_uint32, C.c_uint32, C.c_uint64, _u8p, C.c_uint64]),
+    "ske_bf_load_header": (C.c_int, [_CTX, C.c_uint32, C.POINTER(BfLink), C.c_uint32, C.c_uint64,
+                                     C.c_uint32, C.c_int]),
     "ske_hll_reserve": (C.c_int, [_CTX, C.c_uint32]),
     "ske_hll_capacity": (C.c_uint32, [_CTX]),
     "ske_hll_clear": (C.c_int, [_CTX, C.c_uint32]),

@@ -265,6 +265,76 @@ class SketchClient:
         self.ctx.call("ske_bf_export_link", self.keys.fid[key], link, _ptr(out), out.size)
         return out
 
+    # ---- BF.SCANDUMP / BF.LOADCHUNK (RedisBloom rebloom.c BFScanDump /
+    # BFLoadChunk, src/sb.c SBChain_GetEncodedHeader / GetEncodedChunk /
+    # LoadEncodedChunk; [recall], unconfirmed on a Redis box).  Iterator 0
+    # returns the header chunk with iterator 1; iterator i > 0 returns the bytes
+    # at offset i - 1 of the links' bit arrays laid end to end, at most one link
+    # and MAX_SCANDUMP_SIZE bytes per chunk, with the next iterator i + len;
+    # past the end it returns (0, empty).  LOADCHUNK takes the iterator that
+    # SCANDUMP returned with the chunk (offset = iter - 1 - len).
+    MAX_SCANDUMP_SIZE = 10 * 1024 * 1024
+
+    def bf_scandump(self, key, it: int) -> tuple[int, bytes]:
+        key = encode(key)
+        if not self.keys.expect(key, "bf"):
+            raise ResponseError("ERR not found")
+        it = int(it)
+        links = self.bf_links(key)
+        if it == 0:
+            info = BfInfo()
+            self.ctx.call("ske_bf_info", self.keys.fid[key], C.byref(info))
+            hdr = formats.bf_dump_header(info.inserted, links, info.expansion, bool(info.nonscaling))
+            return 1, hdr
+        off = it - 1
+        for i, L in enumerate(links):
+            if off < L["bytes"]:
+                n = min(L["bytes"] - off, self.MAX_SCANDUMP_SIZE)
+                bits = self.bf_link_bits(key, i)
+                return it + n, bits[off:off + n].tobytes()
+            off -= L["bytes"]
+        return 0, b""
+
+    def bf_loadchunk(self, key, it: int, data: bytes) -> bool:
+        key = encode(key)
+        it, data = int(it), bytes(encode(data))
+        if it == 1:
+            try:
+                h = formats.bf_parse_header(data)
+            except Exception:
+                raise ResponseError("ERR received bad data")
+            if self.keys.type_of(key) is not None:
+                raise ResponseError("ERR item exists")
+            if h["options"] & formats.BLOOM_OPT_FORCE64 == 0 or not h["links"]:
+                raise ResponseError("ERR received bad data")
+            arr = (BfLink * len(h["links"]))()
+            for i, L in enumerate(h["links"]):
+                arr[i].entries, arr[i].bytes, arr[i].bits = L["entries"], L["bytes"], L["bits"]
+                arr[i].size, arr[i].error, arr[i].bpe, arr[i].hashes = (
+                    L["size"], L["error"], L["bpe"], L["hashes"])
+            fid = self.keys.new_fid(key)
+            try:
+                self.ctx.call("ske_bf_load_header", fid, arr, len(h["links"]), h["size"],
+                              h["growth"], 1 if h["nonscaling"] else 0)
+            except SketchLibError as e:
+                self.keys.drop(key)
+                raise ResponseError("ERR received bad data") from e
+            return True
+        if not self.keys.expect(key, "bf"):
+            raise ResponseError("ERR not found")
+        off = it - 1 - len(data)
+        if off < 0:
+            raise ResponseError("ERR invalid offset - no link found")
+        for i, L in enumerate(self.bf_links(key)):
+            if off < L["bytes"]:
+                if off + len(data) > L["bytes"]:
+                    raise ResponseError("ERR invalid chunk - Too big for current filter")
+                buf = np.frombuffer(data, np.uint8)
+                self.ctx.call("ske_bf_link_write", self.keys.fid[key], i, off, _ptr(buf), buf.size)
+                return True
+            off -= L["bytes"]
+        raise ResponseError("ERR invalid offset - no link found")
+
     def bf(self) -> "BloomCommands":
         return BloomCommands(self)
 
@@ -549,6 +619,14 @@ class SketchClient:
             for k, v in info.items():
                 flat += [self._s(k), v]
             return flat
+        if cmd == "BF.SCANDUMP":
+            need(2, 2)
+            it, chunk = self.bf_scandump(a[0], a[1])
+            return [it, chunk]
+        if cmd == "BF.LOADCHUNK":
+            need(3, 3)
+            self.bf_loadchunk(a[0], a[1], a[2])
+            return self._ok()
         if cmd == "BF.CARD":
             need(1, 1)
             k = encode(a[0])

@@ -624,6 +624,63 @@ int ske_bf_import_link(ske_ctx *c, uint32_t fid, uint32_t link, const uint8_t *i
     return SKE_OK;
 }
 
+int ske_bf_link_write(ske_ctx *c, uint32_t fid, uint32_t link, uint64_t offset, const uint8_t *in,
+                      uint64_t nbytes) {
+    Filter *F = c ? get_filter(c, fid) : nullptr;
+    if (!F || (!in && nbytes)) return SKE_EINVAL;
+    if (!F->exists) return SKE_ENOFILTER;
+    if (link >= F->links.size()) return SKE_EINVAL;
+    const Link &L = F->links[link];
+    if (offset > L.bytes || nbytes > L.bytes - offset) return SKE_EINVAL;
+    if (nbytes) {
+        HIPCHK(c, hipMemcpyAsync(L.bf + offset, in, nbytes, hipMemcpyHostToDevice, c->st));
+        HIPCHK(c, hipStreamSynchronize(c->st));
+    }
+    return SKE_OK;
+}
+
+int ske_bf_load_header(ske_ctx *c, uint32_t fid, const ske_bf_link_t *links, uint32_t nlinks,
+                       uint64_t inserted, uint32_t expansion, int nonscaling) {
+    Filter *F = c ? get_filter(c, fid) : nullptr;
+    if (!F || (!links && nlinks)) return SKE_EINVAL;
+    if (F->exists) return SKE_EEXISTS;
+    if (nlinks == 0 || nlinks > SKE_MAX_LINKS) return SKE_EINVAL;
+    Filter nf;
+    nf.growth = expansion;
+    nf.nonscaling = nonscaling != 0;
+    for (uint32_t i = 0; i < nlinks; i++) {
+        const ske_bf_link_t &H = links[i];
+        if (H.bytes == 0 || H.bits != H.bytes * 8 || H.bits >= (uint64_t(1) << 62) || H.hashes < 1 ||
+            H.hashes > 64) {
+            free_filter(nf);
+            return SKE_EINVAL;
+        }
+        Link L;
+        L.entries = H.entries;
+        L.bytes = H.bytes;
+        L.bits = H.bits;
+        L.size = H.size;
+        L.error = H.error;
+        L.bpe = H.bpe;
+        L.hashes = H.hashes;
+        L.div = make_divisor(L.bits);
+        hipError_t e = hipMalloc(&L.bf, (L.bytes + 15) & ~uint64_t(15));
+        if (e == hipSuccess) e = hipMemsetAsync(L.bf, 0, (L.bytes + 15) & ~uint64_t(15), c->st);
+        if (e != hipSuccess) {
+            if (L.bf) (void)hipFree(L.bf);
+            free_filter(nf);
+            c->last_hip = std::string("load header: ") + hipGetErrorString(e);
+            return SKE_ENOMEM;
+        }
+        nf.links.push_back(L);
+    }
+    nf.size = inserted;
+    nf.exists = true;
+    *F = nf;
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
 int ske_bf_mexists(ske_ctx *c, uint32_t fid, const uint8_t *bytes, const uint32_t *offs,
                    uint64_t n, uint8_t *out, int mem) {
     if (!c || !out) return SKE_EINVAL;

@@ -505,3 +505,37 @@ def test_two_streams_equal_one_stream(engine, variant):
     assert np.array_equal(engine.registers_all(2 * w.n_keys)[w.n_keys:], one)
     for a, b, o in zip(answers, bs, outs):
         assert np.array_equal(o.to_host(np.uint8, b.n), a)
+
+
+@pytest.mark.parametrize("shape", ["default-chain", "c3-filter"])
+def test_bf_scandump_loadchunk_round_trip(client, orc, shape):
+    """BF.SCANDUMP of a chain (header chunk, then bit-array chunks of at most
+    MAX_SCANDUMP_SIZE bytes, then (0, b'')) replayed by BF.LOADCHUNK into
+    another key gives the same links, bit arrays, BF.INFO and answers."""
+    rng = np.random.default_rng(11)
+    if shape == "default-chain":
+        ids = [int(x) for x in rng.choice(np.arange(10000, 99999), 1000, replace=False)]
+        client.execute_command("BF.MADD", "src", *ids)   # auto-created, grows to 4 links
+    else:
+        client.execute_command("BF.RESERVE", "src", 0.001, 10_000_000)  # 19.8 MB: 2 chunks
+        ids = [int(x) for x in rng.integers(10**7, 10**8, 200_000)]
+        client.bf_madd_packed("src", *client_pack(ids))
+    chunks, it = [], 0
+    while True:
+        it, data = client.execute_command("BF.SCANDUMP", "src", it)
+        if it == 0:
+            assert data == b""
+            break
+        chunks.append((it, data))
+    assert all(len(d) <= client.MAX_SCANDUMP_SIZE for _, d in chunks[1:])
+    for it, data in chunks:
+        assert client.execute_command("BF.LOADCHUNK", "dst", it, data) == "OK"
+    assert client.bf_links("dst") == client.bf_links("src")
+    assert client.bf_info("dst") == client.bf_info("src")
+    for i in range(len(client.bf_links("src"))):
+        assert np.array_equal(client.bf_link_bits("dst", i), client.bf_link_bits("src", i))
+    probe = ids[:5000] + [int(x) for x in rng.integers(10**7, 10**8, 5000)]
+    assert client.execute_command("BF.MEXISTS", "dst", *probe) == \
+        client.execute_command("BF.MEXISTS", "src", *probe)
+    with pytest.raises(Exception, match="item exists"):
+        client.execute_command("BF.LOADCHUNK", "dst", 1, chunks[0][1])
