@@ -156,7 +156,8 @@ int ske_hll_pfadd(ske_ctx *ctx, const uint32_t *slot, const uint8_t *bytes,
 /* PFCOUNT key [key ...] (union), one answer.  attendance_processor.py:152 */
 int ske_hll_pfcount(ske_ctx *ctx, const uint32_t *slots, uint32_t nkeys, uint64_t *out);
 /* PFCOUNT of each key separately (rankings, attendance_analysis.py:87-97 as
- * README.md:179 describes); group form: union over slots[goffs[g]..goffs[g+1]). */
+ * README.md:179 describes); slots == NULL: keys 0..nkeys-1 of the slab.
+ * Group form: union over slots[goffs[g]..goffs[g+1]). */
 int ske_hll_pfcount_each(ske_ctx *ctx, const uint32_t *slots, uint32_t nkeys, uint64_t *out,
                          int mem);
 int ske_hll_pfcount_groups(ske_ctx *ctx, const uint32_t *slots, const uint32_t *goffs,

@@ -1025,7 +1025,7 @@ int ske_hll_pfcount_each(ske_ctx *c, const uint32_t *slots, uint32_t nkeys, uint
                          int mem) {
     if (!c || !out) return SKE_EINVAL;
     if (nkeys == 0) return SKE_OK;
-    if (mem != SKE_MEM_DEVICE) {
+    if (mem != SKE_MEM_DEVICE && slots) {
         int rc = check_slots_host(c, slots, nkeys);
         if (rc) return rc;
     }
@@ -1099,7 +1099,20 @@ int ske_hll_pfmerge(ske_ctx *c, uint32_t dst, const uint32_t *srcs, uint32_t n) 
     const uint32_t *ds;
     rc = stage_u32(c, srcs, n, SKE_MEM_HOST, 6, &ds);
     if (rc) return rc;
-    HIPCHK(c, launch_pfmerge(c->regs, dst, ds, n, c->st));
+    if (n <= 256) {
+        HIPCHK(c, launch_pfmerge(c->regs, dst, ds, n, c->st));
+    } else {
+        // campus-wide merges (C5: 1.8M day keys): a two-level parallel max
+        uint32_t per = 0;
+        const uint32_t P = pfmerge_partitions(n, c->cus, &per);
+        hipError_t e = hipSuccess;
+        uint8_t *partial = (uint8_t *)scratch_get(c->scratch, 17, size_t(P) * SKE_HLL_REGISTERS, &e);
+        if (e != hipSuccess) {
+            c->last_hip = hipGetErrorString(e);
+            return SKE_ENOMEM;
+        }
+        HIPCHK(c, launch_pfmerge_wide(c->regs, dst, ds, n, partial, per, P, c->st));
+    }
     HIPCHK(c, hipStreamSynchronize(c->st));
     return SKE_OK;
 }

@@ -347,6 +347,27 @@ __device__ __forceinline__ uint4 max_u8x16(uint4 a, uint4 b) {
     return make_uint4(av[0], av[1], av[2], av[3]);
 }
 
+// Max over the 16-B chunk `chunk` of the keys srcs[s0..s1) (slots index the
+// slab; srcs == nullptr: keys s0..s1), four loads in flight per step.
+__device__ __forceinline__ uint4 max_keys(const uint8_t *__restrict__ regs, const uint32_t *srcs,
+                                          uint32_t s0, uint32_t s1, uint32_t chunk, uint4 v) {
+    uint32_t s = s0;
+    for (; s + 4 <= s1; s += 4) {
+        uint4 r[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t key = srcs ? srcs[s + q] : s + q;
+            r[q] = reinterpret_cast<const uint4 *>(regs + size_t(key) * kHllRegs)[chunk];
+        }
+        v = max_u8x16(max_u8x16(v, r[0]), max_u8x16(max_u8x16(r[1], r[2]), r[3]));
+    }
+    for (; s < s1; s++) {
+        const uint32_t key = srcs ? srcs[s] : s;
+        v = max_u8x16(v, reinterpret_cast<const uint4 *>(regs + size_t(key) * kHllRegs)[chunk]);
+    }
+    return v;
+}
+
 __device__ __forceinline__ uint64_t hll_estimate_dev(const uint32_t *h, const double *tau_tab,
                                                      const double *sig_tab) {
     double z = tau_tab[h[kHllQ + 1]];
@@ -379,12 +400,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
         for (int c = 0; c < 4; c++) {
             const uint32_t chunk = c * 256 + tid;  // 1024 chunks of 16 B
-            uint4 v = make_uint4(0, 0, 0, 0);
-            for (uint32_t s = s0; s < s1; s++) {
-                const uint32_t key = slots ? slots[s] : s;
-                const uint4 r = reinterpret_cast<const uint4 *>(regs + size_t(key) * kHllRegs)[chunk];
-                v = (s == s0) ? r : max_u8x16(v, r);
-            }
+            const uint4 v = max_keys(regs, slots, s0, s1, chunk, make_uint4(0, 0, 0, 0));
             const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int q = 0; q < 4; q++)
@@ -399,6 +415,62 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// K2 for one key per group (PFCOUNT of every lecture-day key, the C5
+// rankings): one wave per key, four keys per block in flight.  Each lane bins
+// its 256 registers into a lane-private column of packed counters in LDS
+// (word w of lane l holds bins 2w and 2w+1 as two 16-bit counts, at
+// (w*64 + l)*4: every lane a different bank, no contention even when all
+// registers share a value, which the block-per-group kernel's shared bins
+// serialise on); 32 lanes then sum the columns and lane 0 runs hllCount().
+// A wave's LDS operations complete in order; wave_sync() keeps the compiler
+// from reordering across the cross-lane hand-offs and drains lgkmcnt.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ void __launch_bounds__(256)
+    k_pfcount_wave(const uint8_t *__restrict__ regs, const uint32_t *__restrict__ slots,
+                   uint32_t nkeys, const double *__restrict__ tau_tab,
+                   const double *__restrict__ sig_tab, uint64_t *__restrict__ out) {
+    __shared__ uint32_t cols[4][32 * 64];
+    __shared__ uint32_t hist[4][64];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t *col = cols[wave];
+    for (uint32_t g = blockIdx.x * 4 + wave; g < nkeys; g += gridDim.x * 4) {
+        const uint32_t key = slots ? slots[g] : g;
+        const uint4 *src = reinterpret_cast<const uint4 *>(regs + size_t(key) * kHllRegs);
+        uint4 v[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) v[q] = src[q * 64 + lane];  // coalesced 1 KiB per step
+#pragma unroll
+        for (int w = 0; w < 32; w++) col[w * 64 + lane] = 0;
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const uint32_t wd[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+#pragma unroll
+                for (int b = 0; b < 32; b += 8) {
+                    const uint32_t r = (wd[e] >> b) & 63;
+                    atomicAdd(&col[(r >> 1) * 64 + lane], 1u << ((r & 1) * 16));
+                }
+        }
+        wave_sync();
+        if (lane < 32) {
+            uint32_t sum = 0;
+#pragma unroll 8
+            for (int l = 0; l < 64; l++) sum += col[lane * 64 + l];
+            hist[wave][2 * lane] = sum & 0xffffu;
+            hist[wave][2 * lane + 1] = sum >> 16;
+        }
+        wave_sync();
+        if (lane == 0) out[g] = hll_estimate_dev(hist[wave], tau_tab, sig_tab);
+        wave_sync();
+    }
+}
+
 // Register histogram of one key (for the oracle cross-check of K2's bins).
 __global__ void __launch_bounds__(256)
     k_histogram(const uint8_t *__restrict__ regs, uint32_t *__restrict__ out64) {
@@ -410,6 +482,29 @@ __global__ void __launch_bounds__(256)
     if (threadIdx.x < 64) out64[threadIdx.x] = hist[threadIdx.x];
 }
 
+// K3 for many sources, pass 1: partition p of the sources (`per` consecutive
+// entries of srcs) max-merged into partial row p; block = (partition, quarter
+// of the 1024 chunks).
+__global__ void __launch_bounds__(256)
+    k_pfmerge_part(const uint8_t *__restrict__ regs, const uint32_t *__restrict__ srcs, uint32_t n,
+                   uint32_t per, uint8_t *__restrict__ partial) {
+    const uint32_t chunk = threadIdx.x + (blockIdx.x & 3) * 256;
+    const uint32_t p = blockIdx.x >> 2;
+    const uint32_t s0 = p * per, s1 = s0 + per < n ? s0 + per : n;
+    const uint4 v = max_keys(regs, srcs, s0, s1, chunk, make_uint4(0, 0, 0, 0));
+    reinterpret_cast<uint4 *>(partial + size_t(p) * kHllRegs)[chunk] = v;
+}
+
+// pass 2: dst = max(dst, partial rows 0..P)
+__global__ void __launch_bounds__(256)
+    k_pfmerge_rows(uint8_t *__restrict__ regs, uint32_t dst, const uint8_t *__restrict__ partial,
+                   uint32_t P) {
+    const uint32_t chunk = blockIdx.x * blockDim.x + threadIdx.x;
+    if (chunk >= kHllRegs / 16) return;
+    uint4 *d = reinterpret_cast<uint4 *>(regs + size_t(dst) * kHllRegs) + chunk;
+    *d = max_keys(partial, nullptr, 0, P, chunk, *d);
+}
+
 // K3: PFMERGE dst = max(dst, srcs...)
 __global__ void __launch_bounds__(256)
     k_pfmerge(uint8_t *__restrict__ regs, uint32_t dst, const uint32_t *__restrict__ srcs,
@@ -417,10 +512,7 @@ __global__ void __launch_bounds__(256)
     const uint32_t chunk = blockIdx.x * blockDim.x + threadIdx.x;
     if (chunk >= kHllRegs / 16) return;
     uint4 *d = reinterpret_cast<uint4 *>(regs + size_t(dst) * kHllRegs) + chunk;
-    uint4 v = *d;
-    for (uint32_t s = 0; s < n; s++)
-        v = max_u8x16(v, reinterpret_cast<const uint4 *>(regs + size_t(srcs[s]) * kHllRegs)[chunk]);
-    *d = v;
+    *d = max_keys(regs, srcs, 0, n, chunk, *d);
 }
 
 // K3 into an external buffer: dst[g] = max over the group's slots
@@ -429,9 +521,7 @@ __global__ void __launch_bounds__(256)
                    const uint32_t *__restrict__ goffs, uint32_t ngroups, uint8_t *__restrict__ dst) {
     const uint32_t chunk = threadIdx.x + (blockIdx.x & 3) * 256;  // 1024 x 16 B per key
     for (uint32_t g = blockIdx.x >> 2; g < ngroups; g += gridDim.x >> 2) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        for (uint32_t s = goffs[g]; s < goffs[g + 1]; s++)
-            v = max_u8x16(v, reinterpret_cast<const uint4 *>(regs + size_t(slots[s]) * kHllRegs)[chunk]);
+        const uint4 v = max_keys(regs, slots, goffs[g], goffs[g + 1], chunk, make_uint4(0, 0, 0, 0));
         reinterpret_cast<uint4 *>(dst + size_t(g) * kHllRegs)[chunk] = v;
     }
 }
@@ -612,6 +702,12 @@ hipError_t launch_pfcount(const uint8_t *regs, const uint32_t *slots, const uint
                           uint32_t ngroups, const double *tau, const double *sig, uint64_t *out,
                           int cus, hipStream_t st) {
     if (ngroups == 0) return hipSuccess;
+    if (!goffs) {  // one key per group
+        const unsigned want = (ngroups + 3) / 4, cap = unsigned(cus) * 8;
+        hipLaunchKernelGGL(k_pfcount_wave, dim3(want < cap ? want : cap), dim3(256), 0, st, regs,
+                           slots, ngroups, tau, sig, out);
+        return hipGetLastError();
+    }
     const unsigned grid = ngroups < unsigned(cus) * 8 ? ngroups : unsigned(cus) * 8;
     hipLaunchKernelGGL(k_pfcount, dim3(grid), dim3(256), 0, st, regs, slots, goffs, ngroups, tau,
                        sig, out);
@@ -626,6 +722,23 @@ hipError_t launch_histogram(const uint8_t *regs, uint32_t *out64, hipStream_t st
 hipError_t launch_pfmerge(uint8_t *regs, uint32_t dst, const uint32_t *srcs, uint32_t n,
                           hipStream_t st) {
     hipLaunchKernelGGL(k_pfmerge, dim3(kHllRegs / 16 / 256), dim3(256), 0, st, regs, dst, srcs, n);
+    return hipGetLastError();
+}
+
+// PFMERGE of many sources: partitions of `per` sources reduced in parallel
+// into partial rows (P <= 4 per CU), then one pass over the rows.
+uint32_t pfmerge_partitions(uint32_t n, int cus, uint32_t *per) {
+    const uint32_t maxp = uint32_t(cus) * 4;
+    uint32_t pp = (n + maxp - 1) / maxp;
+    *per = pp < 16 ? 16 : pp;
+    return (n + *per - 1) / *per;
+}
+
+hipError_t launch_pfmerge_wide(uint8_t *regs, uint32_t dst, const uint32_t *srcs, uint32_t n,
+                               uint8_t *partial, uint32_t per, uint32_t P, hipStream_t st) {
+    hipLaunchKernelGGL(k_pfmerge_part, dim3(P * 4), dim3(256), 0, st, regs, srcs, n, per, partial);
+    hipLaunchKernelGGL(k_pfmerge_rows, dim3(kHllRegs / 16 / 256), dim3(256), 0, st, regs, dst,
+                       partial, P);
     return hipGetLastError();
 }
 

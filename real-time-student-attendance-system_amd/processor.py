@@ -115,18 +115,40 @@ class AttendanceProcessor:
         return {"unique_attendees": self.redis_client.pfcount(key)}
 
 
+def rank_top_bottom(counts: np.ndarray, keys: Sequence[str], k: int) -> tuple[list, list]:
+    """Indices of the first k and the last k keys of the order (count
+    descending, key ascending), without sorting every key: only the keys tied
+    with or beyond the k-th count (np.partition) are ordered (np.lexsort).
+    Returns (head, tail), tail in that order as ``.tail(k)`` lists it."""
+    n = len(keys)
+    k = min(max(int(k), 0), n)
+    if k == 0:
+        return [], []
+    c = np.asarray(counts, dtype=np.int64)
+    karr = np.asarray(keys)
+
+    def ordered(idx):
+        return idx[np.lexsort((karr[idx], -c[idx]))]
+
+    hi = np.partition(c, n - k)[n - k]      # k-th largest count
+    head = ordered(np.nonzero(c >= hi)[0])[:k]
+    lo = np.partition(c, k - 1)[k - 1]      # k-th smallest count
+    tail = ordered(np.nonzero(c <= lo)[0])[-k:]
+    return head.tolist(), tail.tolist()
+
+
 def lecture_rankings(client: SketchClient, keys: Sequence[str], k: int = 3) -> dict:
     """Most / least attended lecture-day keys by PFCOUNT (one K2 launch).
 
     Order: count descending, then key ascending (the reference's pandas
     ``sort_values(ascending=False)`` leaves ties in quicksort order; a total
     order is used here so results are reproducible).  ``least_attended`` is
-    the tail of the same order, as ``.tail(3)`` (attendance_analysis.py:95)."""
+    the tail of the same order, as ``.tail(3)`` (attendance_analysis.py:95).
+    At C5 scale (1.8M lecture-day keys) only the tie sets at the two ends are
+    ordered (``rank_top_bottom``)."""
     keys = list(keys)
     counts = client.pfcount_each(keys).astype(np.int64)
-    order = sorted(range(len(keys)), key=lambda i: (-counts[i], keys[i]))
-    head = order[:k]
-    tail = order[-k:] if k else []
+    head, tail = rank_top_bottom(counts, keys, k)
     return {"most_attended": {keys[i]: int(counts[i]) for i in head},
             "least_attended": {keys[i]: int(counts[i]) for i in tail}}
 

@@ -539,3 +539,27 @@ def test_bf_scandump_loadchunk_round_trip(client, orc, shape):
         client.execute_command("BF.MEXISTS", "src", *probe)
     with pytest.raises(Exception, match="item exists"):
         client.execute_command("BF.LOADCHUNK", "dst", 1, chunks[0][1])
+
+
+def test_pfmerge_many_sources_two_level(client):
+    """PFMERGE of 3000 keys (the two-level parallel merge used past 256
+    sources) == the register-wise max, dst's own registers included; and
+    PFCOUNT of every key with a null slot list (keys 0..n-1)."""
+    rng = np.random.default_rng(12)
+    arrays = rng.integers(0, 20, (3000, 16384)).astype(np.uint8)
+    arrays[rng.random(arrays.shape) < 0.9] = 0
+    arrays[17, 5] = 51
+    for i, a in enumerate(arrays):
+        client.hll_load_registers(f"day{i}", a)
+    dst_own = rng.integers(0, 3, 16384).astype(np.uint8)
+    dst_own[9] = 50
+    client.hll_load_registers("campus", dst_own)
+    assert client.pfmerge("campus", *[f"day{i}" for i in range(3000)]) is True
+    want = np.maximum(arrays.max(axis=0), dst_own)
+    assert np.array_equal(client.hll_registers("campus"), want)
+    import ctypes as C
+    n = client.ctx.lib.ske_hll_capacity(client.ctx.ptr)
+    out = np.zeros(n, np.uint64)
+    client.ctx.call("ske_hll_pfcount_each", None, n, out.ctypes.data_as(C.c_void_p), 0)
+    slots = [client.keys.slot[f"day{i}".encode()] for i in range(0, 3000, 250)]
+    assert [int(out[s]) for s in slots] == client.pfcount_each([f"day{i}" for i in range(0, 3000, 250)]).tolist()

@@ -142,3 +142,20 @@ def test_processor_end_to_end_on_device(pkg, orc):
     for k in keys:
         u.merge(ref.hlls[k])
     assert roll["per_lecture"]["all"] == u.count() == roll["campus_unique"]
+
+
+def test_rank_top_bottom_matches_full_sort(pkg):
+    """rank_top_bottom == the first / last k of sorted(keys, (-count, key)),
+    with heavy ties (few distinct counts), k larger than n, and k = 0."""
+    from rtsas_amd.processor import rank_top_bottom
+    rng = np.random.default_rng(4)
+    for n, distinct, k in [(1, 1, 3), (5, 2, 3), (200, 3, 3), (5000, 40, 7), (50, 50, 60), (9, 4, 0)]:
+        keys = [f"hll:unique:L{int(x):05d}:2025-{int(y):02d}-01" for x, y in
+                zip(rng.integers(0, 10 * n, n), rng.integers(1, 13, n))]
+        keys = list(dict.fromkeys(keys))
+        counts = rng.integers(0, distinct, len(keys))
+        order = sorted(range(len(keys)), key=lambda i: (-counts[i], keys[i]))
+        head, tail = rank_top_bottom(counts, keys, k)
+        kk = min(k, len(keys))
+        assert head == order[:kk]
+        assert tail == (order[-kk:] if kk else [])
