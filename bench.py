@@ -58,6 +58,9 @@ def parse():
                     help="with --streams 1: 1 = the K timed steps are recorded once into a "
                          "HIP graph (one K1 launch per step, each over its own resident batch) "
                          "and replayed; 0 = launched one by one from the host")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group for N>1 (nccl = RCCL over xGMI; gloo only to rehearse "
+                         "several ranks on a one-GPU box)")
     ap.add_argument("--layout", default="offsets", choices=["offsets", "fixed"],
                     help="id batch layout: bytes + u32 offsets, or fixed-width ids")
     return ap.parse_args()
@@ -104,11 +107,16 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one GPU per rank; the modulo only matters for a rehearsal of several
+    # ranks on a one-GPU box (--dist-backend gloo), never on a full node
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":  # RCCL
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     w_all = synthetic.WORKLOADS[args.config]
     w = synthetic.shard(w_all, world)
@@ -202,7 +210,8 @@ def main():
     step_ms = e0.elapsed_time(e1) / args.steps
     kern_ms = sum(a.elapsed_time(b) for a, b in per) / len(per) if per else step_ms
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms, step_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, kern_ms, step_ms], dtype=torch.float64,
+                         device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms, step_ms = float(t[0]), float(t[1]), float(t[2])
 
