@@ -202,6 +202,38 @@ int ske_swipes_stats(ske_ctx *ctx, uint32_t fid, const uint8_t *bytes, const uin
 int ske_swipes_variant(ske_ctx *ctx, uint32_t fid);
 int ske_set_option(ske_ctx *ctx, const char *name, int64_t value);
 
+/* ---- ingest: JSON event decode + key-slot resolution ----
+ * The reference decodes each Pulsar payload on the CPU (attendance_processor.py
+ * :103-106) and builds the HLL key from lecture_id (:128; README.md:105-106
+ * adds the UTC day).  ske_ingest_parse decodes a batch of messages on the
+ * device: for each message, status 0 = decoded (the fast JSON / ISO-8601 path,
+ * see sketch_ingest.hip), 1 = left for the host (Python semantics), and for a
+ * decoded one the spans of student_id / lecture_id / timestamp inside msgs,
+ * the UTC day number and a 128-bit key hash.  The context's key table maps
+ * key hashes to HLL slots; the host inserts a key the first time it misses.
+ * All column pointers are device pointers owned by the caller (n entries,
+ * kh 2n); msgs must stay readable to the next 8-byte boundary. */
+typedef struct {
+    uint8_t *status;
+    uint32_t *id_start, *id_len, *lec_start, *lec_len, *ts_start, *ts_len;
+    int32_t *day;
+    uint64_t *kh;
+} ske_ingest_cols_t;
+int ske_ingest_parse(ske_ctx *ctx, const uint8_t *msgs, const uint32_t *moffs, uint64_t n,
+                     int day_form, const ske_ingest_cols_t *cols);
+/* slot_dev[i] = the slot of message i's key, 0xffffffff when not in the table
+ * (or not decoded); *nmiss = decoded messages whose key missed */
+int ske_keytab_lookup(ske_ctx *ctx, const ske_ingest_cols_t *cols, uint64_t n, uint32_t *slot_dev,
+                      uint64_t *nmiss);
+int ske_keytab_insert(ske_ctx *ctx, const uint64_t *kh_host, const uint32_t *slots_host, uint64_t n);
+int ske_keytab_clear(ske_ctx *ctx);
+/* the fused path (K1) over the decoded messages whose key is in the table:
+ * valid_dev[i] = BF.EXISTS of message i's id (0 for the others); PFADD of the
+ * valid ones.  *ntaken = messages that went through K1. */
+int ske_ingest_swipes(ske_ctx *ctx, uint32_t fid, const uint8_t *msgs,
+                      const ske_ingest_cols_t *cols, uint64_t n, uint8_t *valid_dev,
+                      uint64_t *ntaken);
+
 /* ---- stream capture (HIP graphs) ----
  * Record the device work of the calls made between begin and end on the
  * context stream (only enqueue-only calls: ske_swipes_async,

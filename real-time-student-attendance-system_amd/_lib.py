@@ -52,6 +52,12 @@ class BfLink(C.Structure):
                 ("hashes", C.c_int32), ("pad_", C.c_int32)]
 
 
+class IngestCols(C.Structure):
+    _fields_ = [("status", C.c_void_p), ("id_start", C.c_void_p), ("id_len", C.c_void_p),
+                ("lec_start", C.c_void_p), ("lec_len", C.c_void_p), ("ts_start", C.c_void_p),
+                ("ts_len", C.c_void_p), ("day", C.c_void_p), ("kh", C.c_void_p)]
+
+
 class GenParams(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("id_lo", C.c_uint64), ("id_hi", C.c_uint64),
                 ("n_members", C.c_uint64), ("perm_mul", C.c_uint64), ("perm_add", C.c_uint64),
@@ -111,6 +117,13 @@ SIGNATURES = {
                                    C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "ske_swipes_variant": (C.c_int, [_CTX, C.c_uint32]),
     "ske_set_option": (C.c_int, [_CTX, C.c_char_p, C.c_int64]),
+    "ske_ingest_parse": (C.c_int, [_CTX, _u8p, _u32p, C.c_uint64, C.c_int, C.POINTER(IngestCols)]),
+    "ske_keytab_lookup": (C.c_int, [_CTX, C.POINTER(IngestCols), C.c_uint64, _u32p,
+                                    C.POINTER(C.c_uint64)]),
+    "ske_keytab_insert": (C.c_int, [_CTX, _u64p, _u32p, C.c_uint64]),
+    "ske_keytab_clear": (C.c_int, [_CTX]),
+    "ske_ingest_swipes": (C.c_int, [_CTX, C.c_uint32, _u8p, C.POINTER(IngestCols), C.c_uint64, _u8p,
+                                    C.POINTER(C.c_uint64)]),
     "ske_capture_begin": (C.c_int, [_CTX]),
     "ske_capture_end": (C.c_int, [_CTX, C.POINTER(C.c_void_p)]),
     "ske_graph_launch": (C.c_int, [_CTX, _vp]),

@@ -68,6 +68,7 @@ class KeySpace:
         self._free_fids = list(range(_lib.SKE_MAX_FILTERS - 1, -1, -1))
         self._free_slots: list[int] = []
         self._next_slot = 0
+        self.slots_released = 0  # bumps whenever an HLL slot is freed (ingest key table)
 
     def type_of(self, key: bytes) -> str | None:
         return self.kind.get(key)
@@ -112,6 +113,7 @@ class KeySpace:
             s = self.slot.pop(key)
             self.ctx.call("ske_hll_clear", s)  # a reused slot starts empty
             self._free_slots.append(s)
+            self.slots_released += 1
         return k is not None
 
     def release_unused_slot(self, key: bytes) -> None:
@@ -120,6 +122,7 @@ class KeySpace:
         s = self.slot.pop(key)
         del self.kind[key]
         self._free_slots.append(s)
+        self.slots_released += 1
 
 
 class SketchClient:
@@ -134,6 +137,8 @@ class SketchClient:
         self.host, self.port, self.db = host, port, db
 
     # ------------------------------------------------------------ helpers
+    _kt_state = None  # (slots released, key form, prefix) the device key table was built under
+
     def _ok(self):
         return "OK" if self.decode_responses else b"OK"
 
@@ -571,6 +576,135 @@ class SketchClient:
             self.ctx.call("ske_swipes", self.keys.fid[bkey], _ptr(s), _ptr(buf), _ptr(offs), n,
                           _ptr(valid), SKE_MEM_HOST)
         return valid.astype(bool)
+
+    # ------------------------------------------------------------ ingest (§8f row 3)
+    def ingest(self, bf_key, messages: Sequence, hll_key_prefix: str = "hll:unique:",
+               key_form: str = "readme") -> tuple[np.ndarray, np.ndarray]:
+        """The processor loop of attendance_processor.py:100-137 over raw
+        message payloads: decode (json.loads, :103-106), BF.EXISTS of the
+        student id (:109-113) and, if valid, PFADD into the lecture key (:128;
+        README.md:105-106 form ``<prefix><lecture_id>:<YYYY-MM-DD>`` with the
+        UTC day, or ``key_form="code"``: ``<prefix><lecture_id>``).
+
+        Messages are decoded on the device (sketch_ingest.hip); those outside
+        its fast JSON / ISO-8601 path go through Python's json / datetime here,
+        so every message gets exactly the reference's treatment.  Returns
+        ``(valid, status)``: per message the BF.EXISTS answer and 0 decoded on
+        the device, 1 decoded on the host, -1 not decodable (the reference's
+        negative_acknowledge, :134-136)."""
+        import json
+        from datetime import datetime, timezone
+        from ._lib import IngestCols
+        n = len(messages)
+        valid = np.zeros(n, bool)
+        status = np.zeros(n, np.int8)
+        if n == 0:
+            return valid, status
+        day_form = 1 if key_form == "readme" else 0
+        prefix = str(hll_key_prefix)
+        raw = [m if isinstance(m, (bytes, bytearray, memoryview)) else str(m).encode() for m in messages]
+        lens = np.fromiter((len(m) for m in raw), np.uint32, count=n)
+        moffs = np.zeros(n + 1, np.uint32)
+        np.cumsum(lens, out=moffs[1:])
+        blob = np.frombuffer(b"".join(raw), np.uint8)
+        B = self._ingest_buffers(n, blob.size)
+        if blob.size:
+            self.ctx.call("ske_memcpy", C.c_void_p(B["msgs"].ptr), _ptr(blob), blob.size, 0)
+        self.ctx.call("ske_memcpy", C.c_void_p(B["moffs"].ptr), _ptr(moffs), moffs.nbytes, 0)
+        cols = IngestCols(*[C.c_void_p(B[k].ptr) for k in
+                            ("status", "id_start", "id_len", "lec_start", "lec_len", "ts_start",
+                             "ts_len", "day", "kh")])
+        self.ctx.call("ske_ingest_parse", C.c_void_p(B["msgs"].ptr), C.c_void_p(B["moffs"].ptr), n,
+                      day_form, C.byref(cols))
+        if self._kt_state != (self.keys.slots_released, day_form, prefix):
+            self.ctx.call("ske_keytab_clear")  # a freed slot may be reused: start over
+            self._kt_state = (self.keys.slots_released, day_form, prefix)
+        nmiss = C.c_uint64()
+        self.ctx.call("ske_keytab_lookup", C.byref(cols), n, C.c_void_p(B["slot"].ptr), C.byref(nmiss))
+        dev_status = B["status"].to_host(np.uint8, n)
+
+        def key_name(data) -> bytes:
+            lecture_id = data["lecture_id"]
+            ts = datetime.fromisoformat(data["timestamp"])
+            if key_form == "code":
+                return encode(f"{prefix}{lecture_id}")
+            if ts.tzinfo is not None:
+                ts = ts.astimezone(timezone.utc)
+            return encode(f"{prefix}{lecture_id}:{ts.date().isoformat()}")
+
+        tentative = []
+        if nmiss.value:
+            # keys seen for the first time: one Python decode per new key
+            slot = B["slot"].to_host(np.uint32, n)
+            kh = B["kh"].to_host(np.uint64, 2 * n).reshape(n, 2)
+            miss = np.nonzero((dev_status == 0) & (slot == 0xFFFFFFFF))[0]
+            uk, first = np.unique(kh[miss], axis=0, return_index=True)
+            new_slots = np.zeros(len(uk), np.uint32)
+            for j, m in enumerate(miss[first]):
+                name = key_name(json.loads(bytes(raw[m]).decode()))
+                self.keys.expect(name, "hll")
+                if name not in self.keys.slot:
+                    tentative.append(name)
+                    new_slots[j] = self.keys.new_slot(name)
+                else:
+                    new_slots[j] = self.keys.slot[name]
+            ukc = np.ascontiguousarray(uk, np.uint64)
+            self.ctx.call("ske_keytab_insert", ukc.ctypes.data_as(C.c_void_p), _ptr(new_slots), len(uk))
+        bkey = encode(bf_key)
+        has_bf = self.keys.expect(bkey, "bf")
+        taken = C.c_uint64()
+        if has_bf:
+            self.ctx.call("ske_ingest_swipes", self.keys.fid[bkey], C.c_void_p(B["msgs"].ptr),
+                          C.byref(cols), n, C.c_void_p(B["valid"].ptr), C.byref(taken))
+            valid[:] = B["valid"].to_host(np.uint8, n).astype(bool)
+        # the rest: Python's json / datetime semantics
+        host = np.nonzero(dev_status != 0)[0]
+        ids, keys, at = [], [], []
+        for m in host:
+            try:
+                data = json.loads(bytes(raw[m]).decode())
+                sid = encode(data["student_id"])
+                name = key_name(data)
+            except Exception:
+                status[m] = -1
+                continue
+            status[m] = 1
+            ids.append(sid)
+            keys.append(name)
+            at.append(m)
+        if at:
+            valid[np.asarray(at)] = self.swipes(bkey, keys, ids)
+        if tentative:
+            # keys created for this batch that no valid swipe reached are not
+            # created (as in the per-event loop)
+            hit = set()
+            if has_bf:
+                self.ctx.call("ske_keytab_lookup", C.byref(cols), n, C.c_void_p(B["slot"].ptr), None)
+                slot = B["slot"].to_host(np.uint32, n)
+                hit = set(np.unique(slot[valid & (dev_status == 0)]).tolist())
+                hit |= {self.keys.slot[k] for k, m in zip(keys, at) if valid[m] and k in self.keys.slot}
+            for name in tentative:
+                if name in self.keys.slot and self.keys.slot[name] not in hit:
+                    self.keys.release_unused_slot(name)
+        return valid, status
+
+    def _ingest_buffers(self, n: int, nbytes: int) -> dict:
+        from .engine import DeviceBuffer
+        B = getattr(self, "_ingest_bufs", None)
+        if B is None or B["n"] < n or B["nbytes"] < nbytes:
+            if B is not None:
+                for k, v in B.items():
+                    if k not in ("n", "nbytes"):
+                        v.free()
+            cn, cb = max(n, 1024), max(nbytes, 1 << 16)
+            B = {"n": cn, "nbytes": cb, "msgs": DeviceBuffer(self.ctx, cb + 64),
+                 "moffs": DeviceBuffer(self.ctx, (cn + 1) * 4), "status": DeviceBuffer(self.ctx, cn),
+                 "day": DeviceBuffer(self.ctx, cn * 4), "kh": DeviceBuffer(self.ctx, cn * 16),
+                 "slot": DeviceBuffer(self.ctx, cn * 4), "valid": DeviceBuffer(self.ctx, cn)}
+            for k in ("id_start", "id_len", "lec_start", "lec_len", "ts_start", "ts_len"):
+                B[k] = DeviceBuffer(self.ctx, cn * 4)
+            self._ingest_bufs = B
+        return B
 
     # ------------------------------------------------------------ command dispatch
     def execute_command(self, *args, **options):

@@ -84,6 +84,10 @@ struct ske_ctx {
     // a launch on another stream first waits for the previous one
     hipEvent_t xr_done = nullptr;
     hipStream_t xr_stream = nullptr;
+    // ingest key table (open addressing on the 128-bit key hash)
+    uint64_t *kt_key = nullptr;  // 2 per entry, kh0 == 0: empty
+    uint32_t *kt_slot = nullptr;
+    uint64_t kt_cap = 0, kt_count = 0;
     std::string last_hip;
 };
 
@@ -443,6 +447,8 @@ int ske_close(ske_ctx *c) {
     if (c->err) (void)hipFree(c->err);
     if (c->zero16) (void)hipFree(c->zero16);
     if (c->xr_done) (void)hipEventDestroy(c->xr_done);
+    if (c->kt_key) (void)hipFree(c->kt_key);
+    if (c->kt_slot) (void)hipFree(c->kt_slot);
     if (c->stats) (void)hipFree(c->stats);
     if (c->scratch) scratch_delete(c->scratch);
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -1166,6 +1172,177 @@ int ske_hll_slab(ske_ctx *c, void **p, uint64_t *bytes) {
     *p = c->regs;
     *bytes = uint64_t(c->nslots) * SKE_HLL_REGISTERS;
     return SKE_OK;
+}
+
+// ------------------------------------------------------------------ ingest
+static IngestCols ingest_cols(const ske_ingest_cols_t *c) {
+    IngestCols k;
+    k.status = c->status;
+    k.id_start = c->id_start;
+    k.id_len = c->id_len;
+    k.lec_start = c->lec_start;
+    k.lec_len = c->lec_len;
+    k.ts_start = c->ts_start;
+    k.ts_len = c->ts_len;
+    k.day = c->day;
+    k.kh = c->kh;
+    return k;
+}
+
+int ske_ingest_parse(ske_ctx *c, const uint8_t *msgs, const uint32_t *moffs, uint64_t n,
+                     int day_form, const ske_ingest_cols_t *cols) {
+    if (!c || !cols || (n && (!msgs || !moffs))) return SKE_EINVAL;
+    HIPCHK(c, launch_ingest_parse(msgs, moffs, n, day_form, ingest_cols(cols), c->cus, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SKE_OK;
+}
+
+static int keytab_lookup(ske_ctx *c, const ske_ingest_cols_t *cols, uint64_t n, uint32_t *slot,
+                         uint32_t **flag, uint32_t **mlen) {
+    hipError_t e = hipSuccess;
+    *flag = (uint32_t *)scratch_get(c->scratch, 18, n * 4, &e);
+    *mlen = (uint32_t *)scratch_get(c->scratch, 19, n * 4, &e);
+    if (e != hipSuccess) {
+        c->last_hip = hipGetErrorString(e);
+        return SKE_ENOMEM;
+    }
+    HIPCHK(c, launch_keytab_lookup(c->kt_key, c->kt_slot, c->kt_cap ? c->kt_cap - 1 : 0, cols->kh,
+                                   cols->status, cols->id_len, n, slot, *flag, *mlen, c->cus, c->st));
+    return SKE_OK;
+}
+
+int ske_keytab_lookup(ske_ctx *c, const ske_ingest_cols_t *cols, uint64_t n, uint32_t *slot_dev,
+                      uint64_t *nmiss) {
+    if (!c || !cols || !slot_dev) return SKE_EINVAL;
+    if (nmiss) *nmiss = 0;
+    if (!n) return SKE_OK;
+    uint32_t *flag, *mlen;
+    int rc = keytab_lookup(c, cols, n, slot_dev, &flag, &mlen);
+    if (rc) return rc;
+    if (nmiss) {
+        // decoded - found = misses (flag is 1 for found keys)
+        hipError_t e = hipSuccess;
+        uint32_t *incl = (uint32_t *)scratch_get(c->scratch, 20, n * 4, &e);
+        if (!incl) {
+            c->last_hip = hipGetErrorString(e);
+            return SKE_ENOMEM;
+        }
+        HIPCHK(c, scan_inclusive_u32(c->scratch, flag, incl, n, c->st));
+        uint32_t found = 0;
+        HIPCHK(c, hipMemcpyAsync(&found, incl + (n - 1), 4, hipMemcpyDeviceToHost, c->st));
+        std::vector<uint8_t> st(n);
+        HIPCHK(c, hipMemcpyAsync(st.data(), cols->status, n, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(c, hipStreamSynchronize(c->st));
+        uint64_t decoded = 0;
+        for (uint64_t i = 0; i < n; i++) decoded += st[i] == 0;
+        *nmiss = decoded - found;
+    } else {
+        HIPCHK(c, hipStreamSynchronize(c->st));
+    }
+    return SKE_OK;
+}
+
+static int keytab_grow(ske_ctx *c, uint64_t want) {
+    uint64_t cap = 1024;
+    while (cap < want * 2) cap <<= 1;
+    if (cap <= c->kt_cap) return SKE_OK;
+    uint64_t *nk = nullptr;
+    uint32_t *ns = nullptr;
+    hipError_t e = hipMalloc(&nk, cap * 16);
+    if (e == hipSuccess) e = hipMalloc(&ns, cap * 4);
+    if (e == hipSuccess) e = hipMemsetAsync(nk, 0, cap * 16, c->st);
+    if (e != hipSuccess) {
+        if (nk) (void)hipFree(nk);
+        if (ns) (void)hipFree(ns);
+        c->last_hip = std::string("key table: ") + hipGetErrorString(e);
+        return SKE_ENOMEM;
+    }
+    if (c->kt_cap)  // rehash the old entries (empty ones are skipped)
+        HIPCHK(c, launch_keytab_insert(nk, ns, cap - 1, c->kt_key, c->kt_slot, c->kt_cap, c->cus, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    if (c->kt_key) (void)hipFree(c->kt_key);
+    if (c->kt_slot) (void)hipFree(c->kt_slot);
+    c->kt_key = nk;
+    c->kt_slot = ns;
+    c->kt_cap = cap;
+    return SKE_OK;
+}
+
+int ske_keytab_insert(ske_ctx *c, const uint64_t *kh_host, const uint32_t *slots_host, uint64_t n) {
+    if (!c || (n && (!kh_host || !slots_host))) return SKE_EINVAL;
+    if (!n) return SKE_OK;
+    for (uint64_t i = 0; i < n; i++)
+        if ((kh_host[2 * i] & 1) == 0) return SKE_EINVAL;  // kh0 is odd by construction
+    int rc = keytab_grow(c, c->kt_count + n);
+    if (rc) return rc;
+    int r2 = SKE_OK;
+    uint64_t *dk = (uint64_t *)stage_buf(c, 6, n * 16, &r2);
+    uint32_t *ds = (uint32_t *)stage_buf(c, 7, n * 4, &r2);
+    if (r2) return r2;
+    HIPCHK(c, hipMemcpyAsync(dk, kh_host, n * 16, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, hipMemcpyAsync(ds, slots_host, n * 4, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, launch_keytab_insert(c->kt_key, c->kt_slot, c->kt_cap - 1, dk, ds, n, c->cus, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    c->kt_count += n;
+    return SKE_OK;
+}
+
+int ske_keytab_clear(ske_ctx *c) {
+    if (!c) return SKE_EINVAL;
+    if (c->kt_cap) {
+        HIPCHK(c, hipMemsetAsync(c->kt_key, 0, c->kt_cap * 16, c->st));
+        HIPCHK(c, hipStreamSynchronize(c->st));
+    }
+    c->kt_count = 0;
+    return SKE_OK;
+}
+
+int ske_ingest_swipes(ske_ctx *c, uint32_t fid, const uint8_t *msgs, const ske_ingest_cols_t *cols,
+                      uint64_t n, uint8_t *valid_dev, uint64_t *ntaken) {
+    if (!c || !cols || !valid_dev || (n && !msgs)) return SKE_EINVAL;
+    Filter *F = get_filter(c, fid);
+    if (!F) return SKE_EINVAL;
+    if (ntaken) *ntaken = 0;
+    if (!n) return SKE_OK;
+    if (n >= (uint64_t(1) << 31)) return SKE_EINVAL;
+    hipError_t e = hipSuccess;
+    uint32_t *slot = (uint32_t *)scratch_get(c->scratch, 21, n * 4, &e);
+    uint32_t *flag_incl = (uint32_t *)scratch_get(c->scratch, 22, n * 4, &e);
+    uint32_t *len_incl = (uint32_t *)scratch_get(c->scratch, 23, n * 4, &e);
+    if (e != hipSuccess) {
+        c->last_hip = hipGetErrorString(e);
+        return SKE_ENOMEM;
+    }
+    uint32_t *flag, *mlen;
+    int rc = keytab_lookup(c, cols, n, slot, &flag, &mlen);
+    if (rc) return rc;
+    HIPCHK(c, scan_inclusive_u32(c->scratch, flag, flag_incl, n, c->st));
+    HIPCHK(c, scan_inclusive_u32(c->scratch, mlen, len_incl, n, c->st));
+    uint32_t tot[2] = {0, 0};
+    HIPCHK(c, hipMemcpyAsync(&tot[0], flag_incl + (n - 1), 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipMemcpyAsync(&tot[1], len_incl + (n - 1), 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    const uint32_t taken = tot[0], nbytes = tot[1];
+    uint8_t *ids = (uint8_t *)scratch_get(c->scratch, 24, size_t(nbytes) + 16, &e);
+    uint32_t *ids_offs = (uint32_t *)scratch_get(c->scratch, 25, (size_t(taken) + 1) * 4, &e);
+    uint32_t *kslot = (uint32_t *)scratch_get(c->scratch, 26, size_t(taken) * 4 + 4, &e);
+    uint8_t *kvalid = (uint8_t *)scratch_get(c->scratch, 27, size_t(taken) + 4, &e);
+    if (e != hipSuccess) {
+        c->last_hip = hipGetErrorString(e);
+        return SKE_ENOMEM;
+    }
+    const IngestCols k = ingest_cols(cols);
+    HIPCHK(c, launch_ingest_pack(msgs, k, slot, flag_incl, len_incl, n, ids, ids_offs, kslot, c->cus,
+                                 c->st));
+    HIPCHK(c, hipMemsetAsync(c->err, 0, 4, c->st));
+    HIPCHK(c, hipMemsetAsync(kvalid, 0, size_t(taken) + 4, c->st));
+    if (taken && F->exists) {
+        rc = launch_k1(c, cached_chain(*F), ids, ids_offs, 0, kslot, taken, kvalid);
+        if (rc) return rc;
+    }
+    HIPCHK(c, launch_ingest_unpack(k, slot, flag_incl, kvalid, n, valid_dev, c->cus, c->st));
+    if (ntaken) *ntaken = taken;
+    return check_err_flag(c, SKE_ERANGE);
 }
 
 // ------------------------------------------------------------------ graphs

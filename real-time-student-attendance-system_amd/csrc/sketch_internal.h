@@ -66,6 +66,29 @@ hipError_t launch_swipes_lds(const K1Args &A, bool hll, int tile, int cus, hipSt
 hipError_t k1_lds_setup();
 hipError_t set_k1_stamp_buffer(void *p);  // -DSKE_STAMPS diagnostic build only
 
+// sketch_ingest.hip -- JSON event decode and key-slot resolution (device columns)
+struct IngestCols {
+    uint8_t *status;  // 0 decoded on the device, 1 for the host
+    uint32_t *id_start, *id_len, *lec_start, *lec_len, *ts_start, *ts_len;
+    int32_t *day;     // UTC day number (README key form)
+    uint64_t *kh;     // 2 per message: key hash
+};
+hipError_t launch_ingest_parse(const uint8_t *msgs, const uint32_t *moffs, uint64_t n, int day_form,
+                               const IngestCols &out, int cus, hipStream_t st);
+hipError_t launch_keytab_insert(uint64_t *tk, uint32_t *tslot, uint64_t mask, const uint64_t *kh,
+                                const uint32_t *slots, uint64_t n, int cus, hipStream_t st);
+hipError_t launch_keytab_lookup(const uint64_t *tk, const uint32_t *tslot, uint64_t mask,
+                                const uint64_t *kh, const uint8_t *status, const uint32_t *id_len,
+                                uint64_t n, uint32_t *slot, uint32_t *flag, uint32_t *mlen, int cus,
+                                hipStream_t st);
+hipError_t launch_ingest_pack(const uint8_t *msgs, const IngestCols &c, const uint32_t *slot,
+                              const uint32_t *flag_incl, const uint32_t *len_incl, uint64_t n,
+                              uint8_t *ids, uint32_t *ids_offs, uint32_t *kslot, int cus,
+                              hipStream_t st);
+hipError_t launch_ingest_unpack(const IngestCols &c, const uint32_t *slot, const uint32_t *flag_incl,
+                                const uint8_t *kvalid, uint64_t n, uint8_t *valid, int cus,
+                                hipStream_t st);
+
 // sketch_xr.hip -- XCD-partitioned K1 for chains larger than the LDS image
 bool xr_supported(const ChainDev &ch);
 uint64_t xr_scratch_bytes(uint64_t n, int nlinks);

@@ -20,8 +20,8 @@
 namespace ske {
 
 struct Scratch {
-    void *p[24] = {};
-    size_t cap[24] = {};
+    void *p[32] = {};
+    size_t cap[32] = {};
 };
 
 void *scratch_get(Scratch *s, int slot, size_t bytes, hipError_t *err) {
@@ -42,7 +42,7 @@ void *scratch_get(Scratch *s, int slot, size_t bytes, hipError_t *err) {
 }
 
 void scratch_free_all(Scratch *s) {
-    for (int i = 0; i < 24; i++)
+    for (int i = 0; i < 32; i++)
         if (s->p[i]) (void)hipFree(s->p[i]);
 }
 

@@ -1,0 +1,93 @@
+"""Ingest throughput: raw JSON payloads in host memory ->
+BF.EXISTS answers + PFADDs, through ``SketchClient.ingest`` (device JSON
+decode, device key table, fused K1), against the reference's per-event
+Python loop (attendance_processor.py:100-137: json.loads, fromisoformat,
+BF.EXISTS, PFADD) over the CPU oracle on a sample of the same messages.
+
+Messages follow the reference generator's schema (data_generator.py:112-118):
+{"student_id": <5-digit int>, "timestamp": "<ISO>", "lecture_id":
+"LECTURE_<YYYYMMDD>", "is_valid": ..., "event_type": ...}, C2-sized: 100k
+students (10 % invalid swipes), 50 lecture days.  The timed region includes
+the host-side packing and the H2D copy of the payloads (PCIe), so the rate is
+end to end.  usage: python tools/bench_ingest.py [--messages N] [--reps R]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+
+def make_messages(rng, n, members, invalid):
+    days = rng.integers(0, 50, n)
+    bad = rng.random(n) < 0.10
+    ids = np.where(bad, rng.choice(invalid, n), rng.choice(members, n))
+    hh, mm = rng.integers(8, 18, n), rng.integers(0, 60, n)
+    out = []
+    for i in range(n):
+        d = 1 + int(days[i]) % 28
+        mo = 3 + int(days[i]) // 28
+        ts = f"2025-{mo:02d}-{d:02d}T{int(hh[i]):02d}:{int(mm[i]):02d}:00"
+        out.append(('{"student_id": %d, "timestamp": "%s", "lecture_id": "LECTURE_2025%02d%02d", '
+                    '"is_valid": %s, "event_type": "entry"}' % (ids[i], ts, mo, d,
+                                                                  "false" if bad[i] else "true")).encode())
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--messages", type=int, default=1_000_000)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--cpu-messages", type=int, default=50_000)
+    args = ap.parse_args()
+    pkg = ge.load_package()
+    orc = ge.load_oracle()
+    rng = np.random.default_rng(20251003)
+    members = rng.choice(np.arange(10000, 100000), 20_000, replace=False)
+    invalid = np.setdiff1d(np.arange(100000, 200000), members)[:50]
+    msgs = make_messages(rng, args.messages, members, invalid)
+    client = pkg.SketchClient(decode_responses=True)
+    client.execute_command("BF.RESERVE", "bf:students", 0.01, 100000)
+    client.bf_madd_packed("bf:students", *pkg.pack_ints(members))
+    client.ingest("bf:students", msgs[:1000])  # warm: key table, buffers
+    times = []
+    for _ in range(args.reps):
+        t0 = time.perf_counter()
+        valid, status = client.ingest("bf:students", msgs)
+        times.append(time.perf_counter() - t0)
+    best = min(times)
+    # the reference's per-event loop over the oracle, on a sample
+    chain = orc.Chain(100000, 0.01)
+    for m in members:
+        chain.add(str(int(m)).encode())
+    hlls = {}
+    from datetime import datetime
+    sample = msgs[:args.cpu_messages]
+    t0 = time.perf_counter()
+    for m in sample:
+        data = json.loads(m.decode())
+        sid = str(data["student_id"]).encode()
+        ts = datetime.fromisoformat(data["timestamp"])
+        if chain.exists(sid):
+            hlls.setdefault(f"hll:unique:{data['lecture_id']}:{ts.date().isoformat()}",
+                            orc.HLL()).add(sid)
+    cpu_s = time.perf_counter() - t0
+    print(json.dumps({
+        "metric": "ingested swipes/s (JSON payloads in host memory -> answers + PFADD), end to end",
+        "messages": args.messages, "payload_bytes": int(sum(len(m) for m in msgs)),
+        "value": args.messages / best, "best_s": best, "reps_s": times,
+        "device_decoded_frac": float((status == 0).mean()), "valid_frac": float(valid.mean()),
+        "cpu_reference_loop": {"value": len(sample) / cpu_s, "unit": "swipes/s", "cores": 1,
+                               "sample": f"{len(sample)} messages, json.loads + fromisoformat + "
+                                         "oracle BF.EXISTS / PFADD per event"},
+    }), flush=True)
+
+
+if __name__ == "__main__":
+    main()
