@@ -592,21 +592,43 @@ class SketchClient:
         ``(valid, status)``: per message the BF.EXISTS answer and 0 decoded on
         the device, 1 decoded on the host, -1 not decodable (the reference's
         negative_acknowledge, :134-136)."""
+        n = len(messages)
+        try:
+            joined = b"".join(messages)
+            raw = messages
+        except TypeError:  # str payloads: as .decode() would see them
+            raw = [m if isinstance(m, (bytes, bytearray, memoryview)) else str(m).encode()
+                   for m in messages]
+            joined = b"".join(raw)
+        lens = np.fromiter(map(len, raw), np.uint32, count=n)
+        moffs = np.zeros(n + 1, np.uint32)
+        np.cumsum(lens, out=moffs[1:])
+        return self.ingest_packed(bf_key, np.frombuffer(joined, np.uint8), moffs, hll_key_prefix,
+                                  key_form)
+
+    def ingest_packed(self, bf_key, blob: np.ndarray, moffs: np.ndarray,
+                      hll_key_prefix: str = "hll:unique:", key_form: str = "readme"):
+        """``ingest`` over payloads already laid end to end: message i is
+        ``blob[moffs[i]:moffs[i+1]]`` (the layout a network consumer fills)."""
         import json
         from datetime import datetime, timezone
         from ._lib import IngestCols
-        n = len(messages)
+        blob = np.ascontiguousarray(blob, np.uint8)
+        moffs = np.ascontiguousarray(moffs, np.uint32)
+        n = len(moffs) - 1
         valid = np.zeros(n, bool)
         status = np.zeros(n, np.int8)
-        if n == 0:
+        if n <= 0:
             return valid, status
         day_form = 1 if key_form == "readme" else 0
         prefix = str(hll_key_prefix)
-        raw = [m if isinstance(m, (bytes, bytearray, memoryview)) else str(m).encode() for m in messages]
-        lens = np.fromiter((len(m) for m in raw), np.uint32, count=n)
-        moffs = np.zeros(n + 1, np.uint32)
-        np.cumsum(lens, out=moffs[1:])
-        blob = np.frombuffer(b"".join(raw), np.uint8)
+        mv = memoryview(blob)
+
+        class _Raw:  # message i as bytes (host-path decode only)
+            def __getitem__(self, i):
+                return mv[moffs[i]:moffs[i + 1]].tobytes()
+
+        raw = _Raw()
         B = self._ingest_buffers(n, blob.size)
         if blob.size:
             self.ctx.call("ske_memcpy", C.c_void_p(B["msgs"].ptr), _ptr(blob), blob.size, 0)
