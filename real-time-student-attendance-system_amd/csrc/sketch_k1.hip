@@ -58,22 +58,6 @@ hipError_t set_k1_stamp_buffer(void *p) {
 
 __device__ __forceinline__ uint64_t mul_m(uint64_t x) { return x * kMurmurM; }
 
-__device__ __forceinline__ uint64_t bytes_of(uint64_t w0, uint64_t w1, uint32_t s8, uint32_t len) {
-    // bytes s8 .. s8+len-1 of the 16-byte little-endian word pair w1:w0
-    const uint32_t sh = s8 * 8;
-    const bool hi = sh >= 32;
-    const uint32_t a = hi ? uint32_t(w0 >> 32) : uint32_t(w0);
-    const uint32_t b = hi ? uint32_t(w1) : uint32_t(w0 >> 32);
-    const uint32_t c = hi ? uint32_t(w1 >> 32) : uint32_t(w1);
-    uint32_t lo = __builtin_amdgcn_alignbit(b, a, sh & 31);
-    uint32_t up = __builtin_amdgcn_alignbit(c, b, sh & 31);
-    // keep len bytes (len <= 8)
-    const uint32_t lbits = len * 8;
-    lo &= lbits >= 32 ? 0xffffffffu : ((1u << lbits) - 1u);
-    up &= lbits >= 64 ? 0xffffffffu : (lbits <= 32 ? 0u : ((1u << (lbits - 32)) - 1u));
-    return (uint64_t(up) << 32) | lo;
-}
-
 // Copy this wave's P pieces of the LDS image: piece p of the flat piece list
 // (links newest first, each padded to whole 1 KiB pieces) lands at img + p*1024.
 // Pieces past the end repeat the last one (same bytes, same place), so every
@@ -81,7 +65,21 @@ __device__ __forceinline__ uint64_t bytes_of(uint64_t w0, uint64_t w1, uint32_t 
 // tile's own loads with vmcnt(P) while the image is still in flight.  Bytes past
 // a link's 16-byte-padded end read as zero (buffer range check).
 template <int P>
-__device__ __forceinline__ void k1_stage(const K1Args &A, lds_u8 *img, uint32_t wave, uint32_t lane) {
+__device__ __forceinline__ void k1_stage(const K1Args &A, lds_u8 *img, uint32_t wave, uint32_t lane,
+                                         const __amdgpu_buffer_rsrc_t &r0) {
+    if (A.nlinks == 1) {
+        // one link (every RESERVEd filter that has not grown): r0, set up at
+        // kernel entry, covers every piece -- no per-piece descriptor loads
+#pragma unroll
+        for (int j = 0; j < P; j++) {
+            uint32_t p = wave + kK1Waves * uint32_t(j);
+            p = p < A.npieces ? p : A.npieces - 1;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                r0, (__attribute__((address_space(3))) void *)(img + p * 1024), 16,
+                int(p * 1024 + lane * 16), 0, 0, 0);
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < P; j++) {
         uint32_t p = wave + kK1Waves * uint32_t(j);
@@ -360,10 +358,13 @@ __global__ void __launch_bounds__(kK1Block) k_swipes_lds(const K1Args A) {
     // the tile's loads first, then the image copy behind them: the hash waits
     // for its own loads only (vmcnt(P)) while the P pieces land.  (Copy first,
     // loads behind: measured 3 % slower at 524k swipes.)
+    const K1Link &L0 = A.link[A.nlinks - 1];  // the newest link: LDS offset 0
+    const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(L0.bf), 0, int(L0.nbytes16), 0x00020000);
     k1_issue_a<kHll, U>(A, R, c0, c1, in);
     k1_issue_b<U>(R, in);
     __builtin_amdgcn_sched_barrier(0);
-    k1_stage<P>(A, img, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x & 63);
+    k1_stage<P>(A, img, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x & 63, r0);
     __builtin_amdgcn_sched_barrier(0);
     K1_STAMP(1);
     k1_hash<kHll, U>(A, in, hot);
