@@ -108,10 +108,21 @@ class ShardedSketch:
     def _max(self):
         return self.dist.ReduceOp.MAX
 
+    def _all_reduce(self, t, op):
+        """RCCL reduces device tensors in place; gloo (CPU tests, or ranks
+        rehearsed on one GPU) gets a host copy of a device tensor."""
+        if self.use_reduce_scatter or t.device.type == "cpu":
+            self.dist.all_reduce(t, op=op, group=self.group)
+            return t
+        h = t.cpu()
+        self.dist.all_reduce(h, op=op, group=self.group)
+        t.copy_(h)
+        return t
+
     def pfcount_union(self, keys: Sequence) -> int:
         mine = [k for k in keys if self.owns(k)]
         t = self.ops.merge_groups([mine])
-        self.dist.all_reduce(t, op=self._max(), group=self.group)
+        self._all_reduce(t, self._max())
         return int(self.ops.count_raw(t)[0])
 
     def pfcount_each(self, keys: Sequence) -> np.ndarray:
@@ -138,7 +149,7 @@ class ShardedSketch:
             mine = torch.empty((per, HLL_REGISTERS), dtype=t.dtype, device=t.device)
             self.dist.reduce_scatter_tensor(mine, t, op=self._max(), group=self.group)
         else:
-            self.dist.all_reduce(t, op=self._max(), group=self.group)
+            self._all_reduce(t, self._max())
             mine = t[self.rank * per:(self.rank + 1) * per].contiguous()
         local = torch.from_numpy(self.ops.count_raw(mine).astype(np.int64))
         if self.use_reduce_scatter:
