@@ -563,3 +563,39 @@ def test_pfmerge_many_sources_two_level(client):
     client.ctx.call("ske_hll_pfcount_each", None, n, out.ctypes.data_as(C.c_void_p), 0)
     slots = [client.keys.slot[f"day{i}".encode()] for i in range(0, 3000, 250)]
     assert [int(out[s]) for s in slots] == client.pfcount_each([f"day{i}" for i in range(0, 3000, 250)]).tolist()
+
+
+def test_property_swipes_vs_oracle(pkg, orc):
+    """Hypothesis: fused swipes on random byte ids (0..64 B), random key skews
+    and batch sizes from 0 to a few thousand == the oracle's sequential
+    BF.EXISTS + PFADD, answers and registers."""
+    from hypothesis import HealthCheck, given, settings, strategies as st
+    client = pkg.SketchClient(decode_responses=True)
+    members = [bytes([i % 256, i // 256, 7]) * (1 + i % 5) for i in range(3000)]
+    client.execute_command("BF.RESERVE", "bf", 0.01, 5000)
+    client.execute_command("BF.MADD", "bf", *members)
+    chain = orc.Chain(5000, 0.01)
+    for m in members:
+        chain.add(m)
+    counter = [0]
+
+    @settings(max_examples=25, deadline=None, suppress_health_check=list(HealthCheck))
+    @given(st.lists(st.one_of(st.binary(min_size=0, max_size=64), st.sampled_from(members)),
+                    min_size=0, max_size=3000),
+           st.integers(1, 40), st.floats(0.0, 3.0))
+    def run(items, nkeys, skew):
+        counter[0] += 1
+        rng = np.random.default_rng(counter[0])
+        w = 1.0 / np.arange(1, nkeys + 1) ** skew
+        kid = rng.choice(nkeys, size=len(items), p=w / w.sum())
+        keys = [f"h{counter[0]}:{int(k)}" for k in kid]
+        valid = client.swipes("bf", keys, items)
+        regs = {}
+        for x, k in zip(items, keys):
+            if chain.exists(x):
+                regs.setdefault(k, orc.HLL()).add(x)
+        assert valid.tolist() == [bool(chain.exists(x)) for x in items]
+        for k, h in regs.items():
+            assert np.array_equal(client.hll_registers(k), h.regs)
+
+    run()
