@@ -66,10 +66,20 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_threads():
+    """Host threads for the all-cores CPU baseline: OMP_NUM_THREADS when set
+    (the GPU box sets it to its CPU share, 16), else this process's affinity."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    n = int(env) if env.isdigit() and int(env) > 0 else len(os.sched_getaffinity(0))
+    return max(1, min(n, 64))
+
+
 def cpu_baseline(engine, pkg, w, p, b0, seconds):
-    """Oracle (C restatement of Redis/RedisBloom, 1 thread) running the
-    processor loop attendance_processor.py:100-137 (BF.EXISTS then PFADD) on
-    the same batch, repeated for ~`seconds`."""
+    """Oracle (C restatement of Redis/RedisBloom) running the processor loop
+    attendance_processor.py:100-137 (BF.EXISTS then PFADD) on the same batch,
+    repeated for ~`seconds`: half the time on all host threads
+    (orc_process_swipes_mt, the reported value), half on 1 thread (SURVEY.md
+    §8d item 2)."""
     import numpy as np
     import __graft_entry__ as ge
     orc = ge.load_oracle()
@@ -81,17 +91,26 @@ def cpu_baseline(engine, pkg, w, p, b0, seconds):
     buf, offs, slot = b0.to_host()
     slot = slot.astype(np.uint32)
     regs = np.zeros((int(slot.max()) + 1, 16384), np.uint8)
-    n, passes = len(offs) - 1, 0
-    t0 = time.perf_counter()
-    while True:
-        orc.process_swipes(chain, regs, slot, buf, offs)
-        passes += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": n * passes / dt, "unit": "swipes/s", "cores": 1, "kind": "port",
-            "sample": f"{passes} passes over the first {n}-swipe batch (C oracle, "
-                      f"orc_process_swipes, 1 thread, {dt:.1f}s)"}
+    n = len(offs) - 1
+
+    def run(threads, budget):
+        passes = 0
+        t0 = time.perf_counter()
+        while True:
+            orc.process_swipes(chain, regs, slot, buf, offs, threads=threads)
+            passes += 1
+            if time.perf_counter() - t0 >= budget:
+                break
+        return passes, time.perf_counter() - t0
+
+    nt = cpu_threads()
+    p1, dt1 = run(1, seconds / 2)
+    pm, dtm = run(nt, seconds / 2)
+    return {"value": n * pm / dtm, "unit": "swipes/s", "cores": nt, "kind": "port",
+            "sample": f"{pm} passes over the first {n}-swipe batch (C oracle, "
+                      f"orc_process_swipes_mt, {nt} threads, {dtm:.1f}s)",
+            "single_thread": {"value": n * p1 / dt1, "cores": 1,
+                              "sample": f"{p1} passes, orc_process_swipes, {dt1:.1f}s"}}
 
 
 def main():

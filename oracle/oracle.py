@@ -84,6 +84,9 @@ def lib():
     L.orc_process_swipes.restype = C.c_uint64
     L.orc_process_swipes.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_uint64, C.c_void_p, u64p]
+    L.orc_process_swipes_mt.restype = C.c_uint64
+    L.orc_process_swipes_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_void_p, C.c_uint64, C.c_void_p, u64p, C.c_int]
     L.orc_hll_madd.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                C.c_void_p]
     _lib = L
@@ -210,17 +213,23 @@ class Chain:
 
 
 def process_swipes(chain: Chain | None, regs: np.ndarray, slot: np.ndarray, buf: np.ndarray,
-                   offs: np.ndarray) -> tuple[np.ndarray, int, int]:
+                   offs: np.ndarray, threads: int = 1) -> tuple[np.ndarray, int, int]:
     """Per-event loop of attendance_processor.py:100-137 (no transport).
 
-    regs: (nkeys, 16384) u8, updated in place.  Returns (valid u8[n], nvalid, probes)."""
+    regs: (nkeys, 16384) u8, updated in place.  Returns (valid u8[n], nvalid, probes).
+    threads > 1 runs orc_process_swipes_mt (same results, host-thread timing)."""
     n = len(offs) - 1
     out = np.zeros(n, np.uint8)
     probes = C.c_uint64(0)
     assert regs.dtype == np.uint8 and regs.flags.c_contiguous
-    nvalid = lib().orc_process_swipes(chain.p if chain else None, _ptr(regs),
-                                      _ptr(np.ascontiguousarray(slot, np.uint32)), _ptr(buf),
-                                      _ptr(offs), n, _ptr(out), C.byref(probes))
+    slot = np.ascontiguousarray(slot, np.uint32)
+    if threads > 1:
+        nvalid = lib().orc_process_swipes_mt(chain.p if chain else None, _ptr(regs), _ptr(slot),
+                                             _ptr(buf), _ptr(offs), n, _ptr(out),
+                                             C.byref(probes), int(threads))
+    else:
+        nvalid = lib().orc_process_swipes(chain.p if chain else None, _ptr(regs), _ptr(slot),
+                                          _ptr(buf), _ptr(offs), n, _ptr(out), C.byref(probes))
     return out, nvalid, probes.value
 
 

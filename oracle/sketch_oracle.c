@@ -8,9 +8,11 @@
  * that the PFCOUNT estimator performs exactly the IEEE double operations of
  * Redis's hllCount().
  */
+#define _POSIX_C_SOURCE 200809L /* pthread_barrier_t under -std=c11 */
 #include "sketch_oracle.h"
 
 #include <math.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -462,6 +464,71 @@ uint64_t orc_process_swipes(const orc_chain *c, uint8_t *regs, const uint32_t *s
             nvalid++;
         }
     }
+    return nvalid;
+}
+
+/* The same loop on T host threads (SURVEY.md §8d "all host cores"): the
+ * BF.EXISTS answers of a contiguous share of the swipes per thread, then the
+ * valid-gated PFADDs with each key owned by one thread (slot % T), so the
+ * register writes never race and the result is the sequential one (register
+ * max commutes).  Timing counterpart only; the checker is orc_process_swipes. */
+typedef struct {
+    const orc_chain *c;
+    uint8_t *regs;
+    const uint32_t *slot;
+    const uint8_t *bytes;
+    const uint32_t *offs;
+    uint8_t *valid;
+    uint64_t n, nvalid, probes;
+    pthread_barrier_t *bar;
+    int t, nt;
+} orc_mt_arg;
+
+static void *orc_mt_worker(void *p) {
+    orc_mt_arg *a = (orc_mt_arg *)p;
+    uint64_t lo = a->n * (uint64_t)a->t / (uint64_t)a->nt;
+    uint64_t hi = a->n * (uint64_t)(a->t + 1) / (uint64_t)a->nt;
+    uint64_t probes = 0, nvalid = 0;
+    for (uint64_t i = lo; i < hi; i++) {
+        const uint8_t *id = a->bytes + a->offs[i];
+        a->valid[i] = a->c ? (uint8_t)orc_chain_check(a->c, id, a->offs[i + 1] - a->offs[i], &probes) : 0;
+    }
+    pthread_barrier_wait(a->bar);
+    for (uint64_t i = 0; i < a->n; i++) {
+        if (!a->valid[i] || a->slot[i] % (uint32_t)a->nt != (uint32_t)a->t) continue;
+        orc_hll_add(a->regs + (size_t)a->slot[i] * ORC_HLL_REGISTERS, a->bytes + a->offs[i],
+                    a->offs[i + 1] - a->offs[i]);
+        nvalid++;
+    }
+    a->probes = probes;
+    a->nvalid = nvalid;
+    return NULL;
+}
+
+uint64_t orc_process_swipes_mt(const orc_chain *c, uint8_t *regs, const uint32_t *slot,
+                               const uint8_t *bytes, const uint32_t *offs, uint64_t n,
+                               uint8_t *out_valid, uint64_t *probes, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    orc_mt_arg args[256];
+    pthread_barrier_t bar;
+    pthread_barrier_init(&bar, NULL, (unsigned)nthreads);
+    uint8_t *valid = out_valid ? out_valid : (uint8_t *)malloc(n ? n : 1);
+    for (int t = 0; t < nthreads; t++) {
+        args[t] = (orc_mt_arg){c, regs, slot, bytes, offs, valid, n, 0, 0, &bar, t, nthreads};
+        if (t) pthread_create(&th[t], NULL, orc_mt_worker, &args[t]);
+    }
+    orc_mt_worker(&args[0]);
+    uint64_t nvalid = args[0].nvalid;
+    if (probes) *probes += args[0].probes;
+    for (int t = 1; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        nvalid += args[t].nvalid;
+        if (probes) *probes += args[t].probes;
+    }
+    pthread_barrier_destroy(&bar);
+    if (!out_valid) free(valid);
     return nvalid;
 }
 

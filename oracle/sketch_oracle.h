@@ -130,6 +130,11 @@ uint64_t orc_chain_mexists(const orc_chain *c, const uint8_t *bytes, const uint3
 uint64_t orc_process_swipes(const orc_chain *c, uint8_t *regs, const uint32_t *slot,
                             const uint8_t *bytes, const uint32_t *offs, uint64_t n,
                             uint8_t *out_valid, uint64_t *probes);
+/* The same on nthreads host threads (BF.EXISTS by swipe share, PFADD by key
+ * owner); identical results.  CPU-baseline timing only. */
+uint64_t orc_process_swipes_mt(const orc_chain *c, uint8_t *regs, const uint32_t *slot,
+                               const uint8_t *bytes, const uint32_t *offs, uint64_t n,
+                               uint8_t *out_valid, uint64_t *probes, int nthreads);
 /* PFADD of many elements with per-element "this element changed a register"
  * flags (sequential Redis order). */
 void orc_hll_madd(uint8_t *regs, const uint32_t *slot, const uint8_t *bytes,

@@ -1,0 +1,99 @@
+"""Parity at the benchmark's own sizes (BASELINE.json configs), bit-exact.
+
+The C oracle finishes a whole bench step in seconds, so the configurations
+bench.py measures are checked exactly, not only through properties:
+
+- C2: the bench's workload (100k members, 50 keys, 1M-swipe steps), four
+  steps recorded into a HIP graph and replayed as bench.py does;
+- C4: the adversarial stream (50 % invalid, half of them near-collisions of
+  members: one decimal digit changed), one 1M-swipe step;
+- C3: one GPU's shard of the 8-GPU C3 run (10M-member filter of 19.8 MB,
+  12.5k Zipf lecture-day keys), one 16M-swipe step through the
+  XCD-partitioned K1.
+
+Answers, every register array and the probe / valid counts must equal the
+oracle's (attendance_processor.py:100-137 restated, oracle/sketch_oracle.c).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle(orc, engine, w, p, batches, nkeys):
+    chain = orc.Chain(w.bf_capacity, w.bf_error)
+    mb = engine.members_batch(p, 0, w.n_members)
+    buf, offs, _ = mb.to_host()
+    mb.free()
+    chain.madd_packed(buf, offs)
+    regs = np.zeros((nkeys, 16384), np.uint8)
+    answers, probes, nvalid = [], 0, 0
+    for b in batches:
+        buf, offs, slot = b.to_host()
+        v, nv, pr = orc.process_swipes(chain, regs, slot.astype(np.uint32), buf, offs)
+        answers.append(v)
+        probes += pr
+        nvalid += nv
+    return chain, regs, answers, probes, nvalid
+
+
+def _setup(engine, w):
+    engine.reserve(0, w.bf_error, w.bf_capacity)
+    p = engine.gen_params(w)
+    engine.preload(0, p, w.n_members)
+    engine.hll_reserve(w.n_keys)
+    return p
+
+
+def test_c2_bench_steps_graph_replay(engine, orc):
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import DeviceBuffer
+    w = synthetic.WORKLOADS["c2"]
+    p = _setup(engine, w)
+    n = w.step_swipes
+    batches = [engine.swipe_batch(p, j * n, n) for j in range(4)]
+    outs = [DeviceBuffer(engine.ctx, n) for _ in batches]
+    g = engine.capture(lambda: [engine.swipes_async(0, b, o) for b, o in zip(batches, outs)])
+    g.launch()
+    engine.sync()
+    g.free()
+    _, regs, answers, probes, nvalid = _oracle(orc, engine, w, p, batches, w.n_keys)
+    for a, o in zip(answers, outs):
+        assert np.array_equal(o.to_host(np.uint8, n), a)
+    assert np.array_equal(engine.registers_all(w.n_keys), regs)
+    stats = [engine.swipes_stats(0, b) for b in batches]
+    assert (sum(s[0] for s in stats), sum(s[1] for s in stats)) == (probes, nvalid)
+    assert 0.85 < nvalid / (4 * n) < 0.95
+
+
+def test_c4_adversarial_step(engine, orc):
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import DeviceBuffer
+    w = synthetic.WORKLOADS["c4"]
+    p = _setup(engine, w)
+    b = engine.swipe_batch(p, 0, w.step_swipes)
+    out = DeviceBuffer(engine.ctx, b.n)
+    engine.swipes(0, b, out)
+    _, regs, answers, probes, nvalid = _oracle(orc, engine, w, p, [b], w.n_keys)
+    assert np.array_equal(out.to_host(np.uint8, b.n), answers[0])
+    assert np.array_equal(engine.registers_all(w.n_keys), regs)
+    assert engine.swipes_stats(0, b) == (probes, nvalid)
+    # half the swipes are non-members; about 1 % of those pass the filter
+    assert 0.49 < nvalid / b.n < 0.52
+
+
+def test_c3_gpu_shard_full_step(engine, orc):
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import DeviceBuffer
+    w = synthetic.shard(synthetic.WORKLOADS["c3"], 8)
+    assert w.n_keys == 12_500 and w.step_swipes == 16_000_000
+    p = _setup(engine, w)
+    assert engine.variant(0) == 2  # XCD-partitioned K1 for the 19.8 MB filter
+    b = engine.swipe_batch(p, 0, w.step_swipes)
+    out = DeviceBuffer(engine.ctx, b.n)
+    engine.swipes(0, b, out)
+    chain, regs, answers, probes, nvalid = _oracle(orc, engine, w, p, [b], w.n_keys)
+    assert np.array_equal(engine.bloom_bits(0, 0, chain.link_info(0)["bytes"]), chain.link_bits(0))
+    assert np.array_equal(out.to_host(np.uint8, b.n), answers[0])
+    assert np.array_equal(engine.registers_all(w.n_keys), regs)
+    assert engine.swipes_stats(0, b) == (probes, nvalid)

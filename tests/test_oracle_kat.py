@@ -108,3 +108,23 @@ def test_hll_string_decode(orc):
     s = b"HYLL" + bytes([0, 0, 0, 0]) + bytes(8) + h.dense()
     assert np.array_equal(orc.hll_decode_string(s), h.regs)
     assert orc.hll_decode_string(b"HYLL" + bytes([1, 0, 0, 0]) + bytes(8) + bytes([0x00])) is None
+
+
+def test_process_swipes_threads_identical(orc):
+    """The multi-threaded CPU baseline (orc_process_swipes_mt, bench.py's
+    cpu_baseline) gives the sequential loop's answers, counts and registers."""
+    rng = np.random.default_rng(3)
+    members = rng.choice(np.arange(10**5, 10**6), 3000, replace=False)
+    chain = orc.Chain(5000, 0.01)
+    chain.madd_packed(*orc.pack([str(int(x)).encode() for x in members]))
+    ids = np.where(rng.random(20000) < 0.9, rng.choice(members, 20000),
+                   rng.integers(10**6, 2 * 10**6, 20000))
+    buf, offs = orc.pack([str(int(x)).encode() for x in ids])
+    slot = rng.integers(0, 37, 20000).astype(np.uint32)
+    want = np.zeros((37, 16384), np.uint8)
+    v1, n1, p1 = orc.process_swipes(chain, want, slot, buf, offs)
+    for threads in (2, 5, 16):
+        got = np.zeros_like(want)
+        v2, n2, p2 = orc.process_swipes(chain, got, slot, buf, offs, threads=threads)
+        assert np.array_equal(v1, v2) and (n1, p1) == (n2, p2)
+        assert np.array_equal(want, got)
