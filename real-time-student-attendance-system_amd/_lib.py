@@ -10,7 +10,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "csrc", "libsketch.so")
+# SKE_LIB names another build of the same ABI (A/B timing of kernel variants;
+# tools/ab_build.sh); the default is the in-tree build.
+LIB_PATH = os.environ.get("SKE_LIB") or os.path.join(_HERE, "csrc", "libsketch.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "sketch.h")
 
 SKE_OK = 0
@@ -146,6 +148,14 @@ def load() -> C.CDLL:
         raise ImportError(
             f"libsketch.so is not built at {LIB_PATH}; run `python -c 'import __graft_entry__ as g; "
             "g.build()'` (the sketch engine has no CPU fallback)")
+    # One HIP runtime per process: libsketch and PyTorch-ROCm both need
+    # libamdhip64.so.7 (same soname), and whichever loads first serves both.
+    # PyTorch's runtime must be the one (its HIP stack fails to find the device
+    # on top of /opt/rocm's), so torch is loaded before libsketch.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

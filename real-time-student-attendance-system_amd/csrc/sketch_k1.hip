@@ -95,19 +95,6 @@ __device__ __forceinline__ void k1_stage(const K1Args &A, lds_u8 *img, uint32_t 
     }
 }
 
-__device__ __forceinline__ bool k1_reg_max(uint8_t *reg, uint32_t rank) {
-    const uint32_t b = uint32_t(reinterpret_cast<uintptr_t>(reg) & 3);
-    uint32_t *w = reinterpret_cast<uint32_t *>(reg - b);
-    const uint32_t sh = b * 8;
-    uint32_t old = *w;
-    while (((old >> sh) & 0xffu) < rank) {
-        const uint32_t prev = atomicCAS(w, old, (old & ~(0xffu << sh)) | (rank << sh));
-        if (prev == old) return true;
-        old = prev;
-    }
-    return false;
-}
-
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t k1_rsrc(const void *p, uint32_t nbytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, int(nbytes), 0x00020000);
 }
@@ -159,11 +146,18 @@ struct K1In {  // a tile's loads in flight
 
 template <int U>
 struct K1Hot {  // a hashed tile
-    uint32_t idx[U], sl[U], rank[U], cur[U];
+    uint32_t idx[U], sl[U], rank[U], cur[U], sh[U];
     bool act[U];
     uint64_t ha[U], hb[U];
-    uint8_t *reg[U];
+    uint32_t *w[U];  // the aligned word holding the swipe's register
     ProbeWalk32 wk[U];
+};
+
+template <int U>
+struct K1Pend {  // a committed tile's register CASes, settled one tile later
+    uint32_t *w[U];
+    uint32_t exp[U], prev[U], rank[U], sh[U];
+    bool on[U];
 };
 
 struct K1Rsrc {
@@ -271,11 +265,15 @@ __device__ __forceinline__ void k1_hash(const K1Args &A, const K1In<U> &in, K1Ho
             uint32_t ridx;
             hll_patlen(hh[u], ridx, h.rank[u]);
             const bool ok = in.act[u] && in.sl[u] < A.nslots;
-            h.reg[u] = ok ? A.regs + (uint64_t(in.sl[u]) << kHllP) + ridx : const_cast<uint8_t *>(A.zero16);
+            uint8_t *reg = ok ? A.regs + (uint64_t(in.sl[u]) << kHllP) + (ridx & ~3u)
+                              : const_cast<uint8_t *>(A.zero16);
+            h.w[u] = reinterpret_cast<uint32_t *>(reg);
+            h.sh[u] = (ridx & 3) * 8;
         }
-        // the pre-check load flies over the probes
+        // the pre-check load of the register's word flies over the probes; it
+        // is also the expected value of the CAS that raises the register
 #pragma unroll
-        for (int u = 0; u < U; u++) h.cur[u] = *h.reg[u];
+        for (int u = 0; u < U; u++) h.cur[u] = *h.w[u];
     }
     const K1Link &L = A.link[A.nlinks - 1];
     const Divisor D{L.d, L.m, L.t, L.sh, 0};
@@ -312,17 +310,30 @@ __device__ __forceinline__ void k1_probe(const K1Args &A, const lds_u8 *img, K1H
     }
 }
 
-// PFADD of the valid swipes, answers
+// PFADD of the valid swipes, answers.  A register below the swipe's rank is
+// raised by one CAS whose expected value is the pre-check word: it is issued
+// here and its result is looked at one tile later (k1_settle), after the next
+// tile's hash and probes, so the atomic's round trip to memory is hidden.
+// The pre-check may be stale, never too high (registers only grow): a stale
+// word makes the CAS fail, and k1_settle finishes the byte max in a loop.
 template <bool kHll, int U>
-__device__ __forceinline__ void k1_commit(const K1Args &A, const K1Hot<U> &h, const uint32_t *valid) {
+__device__ __forceinline__ void k1_commit(const K1Args &A, const K1Hot<U> &h, const uint32_t *valid,
+                                          K1Pend<U> &pd) {
     if constexpr (kHll) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            if (!valid[u]) continue;
-            if (h.sl[u] >= A.nslots)
-                atomicOr(A.err, 1u);
-            else if (h.cur[u] < h.rank[u])  // the pre-check may be stale, never too high
-                k1_reg_max(h.reg[u], h.rank[u]);
+            const bool slot_ok = h.sl[u] < A.nslots;
+            if (valid[u] && !slot_ok) atomicOr(A.err, 1u);
+            const bool need = valid[u] && slot_ok && ((h.cur[u] >> h.sh[u]) & 0xffu) < h.rank[u];
+            pd.on[u] = need;
+            pd.w[u] = h.w[u];
+            pd.exp[u] = h.cur[u];
+            pd.prev[u] = h.cur[u];
+            pd.rank[u] = h.rank[u];
+            pd.sh[u] = h.sh[u];
+            if (need)
+                pd.prev[u] = atomicCAS(h.w[u], h.cur[u],
+                                       (h.cur[u] & ~(0xffu << h.sh[u])) | (h.rank[u] << h.sh[u]));
         }
     }
     if (A.out) {
@@ -331,6 +342,25 @@ __device__ __forceinline__ void k1_commit(const K1Args &A, const K1Hot<U> &h, co
         for (int u = 0; u < U; u++)  // lanes past the chunk store out of range (dropped)
             __builtin_amdgcn_raw_buffer_store_b8(uint8_t(valid[u]), r_out, h.act[u] ? h.idx[u] : 0xffffffffu,
                                                  0, 0);
+    }
+}
+
+template <bool kHll, int U>
+__device__ __forceinline__ void k1_settle(K1Pend<U> &pd) {
+    if constexpr (kHll) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (!pd.on[u] || pd.prev[u] == pd.exp[u]) continue;
+            const uint32_t sh = pd.sh[u], rank = pd.rank[u];
+            uint32_t old = pd.prev[u];
+            while (((old >> sh) & 0xffu) < rank) {
+                const uint32_t p = atomicCAS(pd.w[u], old, (old & ~(0xffu << sh)) | (rank << sh));
+                if (p == old) break;
+                old = p;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) pd.on[u] = false;
     }
 }
 
@@ -355,23 +385,27 @@ __global__ void __launch_bounds__(kK1Block) k_swipes_lds(const K1Args A) {
     K1In<U> in;
     K1Hot<U> hot;
     K1_STAMP(0);
-    // the tile's loads first, then the image copy behind them: the hash waits
-    // for its own loads only (vmcnt(P)) while the P pieces land.  (Copy first,
-    // loads behind: measured 3 % slower at 524k swipes.)
+    // the tile's offset / slot loads first, then the image copy behind them,
+    // then the id-word loads (which need the offsets): the id loads and the
+    // hash wait for their own loads only (vmcnt(P)) while the P pieces land.
+    // (Copy first, loads behind: measured 3 % slower at 524k swipes.)
     const K1Link &L0 = A.link[A.nlinks - 1];  // the newest link: LDS offset 0
     const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(L0.bf), 0, int(L0.nbytes16), 0x00020000);
     k1_issue_a<kHll, U>(A, R, c0, c1, in);
-    k1_issue_b<U>(R, in);
     __builtin_amdgcn_sched_barrier(0);
     k1_stage<P>(A, img, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x & 63, r0);
     __builtin_amdgcn_sched_barrier(0);
+    k1_issue_b<U>(R, in);  // waits for the offsets only (vmcnt(P): the copy is younger)
     K1_STAMP(1);
     k1_hash<kHll, U>(A, in, hot);
     K1_STAMP(2);
     __syncthreads();  // the image has landed
     K1_STAMP(3);
     [[maybe_unused]] int it = 0;  // stamp index only
+    K1Pend<U> pend;
+#pragma unroll
+    for (int u = 0; u < U; u++) pend.on[u] = false;
     for (uint32_t base = c0;; it++) {
         const uint32_t next = base + kK1Block * U;
         const bool more = next < c1;  // block-uniform
@@ -380,13 +414,15 @@ __global__ void __launch_bounds__(kK1Block) k_swipes_lds(const K1Args A) {
         k1_probe<U>(A, img, hot, valid);
         K1_STAMP(4 + 3 * it);
         k1_issue_b<U>(R, in);
-        k1_commit<kHll, U>(A, hot, valid);
+        k1_settle<kHll, U>(pend);  // the previous tile's CASes (landed during this tile)
+        k1_commit<kHll, U>(A, hot, valid, pend);
         K1_STAMP(5 + 3 * it);
         if (!more) break;
         k1_hash<kHll, U>(A, in, hot);
         K1_STAMP(6 + 3 * it);
         base = next;
     }
+    k1_settle<kHll, U>(pend);
     K1_STAMP(15);
 }
 
