@@ -416,58 +416,89 @@ __global__ void __launch_bounds__(256)
 }
 
 // K2 for one key per group (PFCOUNT of every lecture-day key, the C5
-// rankings): one wave per key, four keys per block in flight.  Each lane bins
-// its 256 registers into a lane-private column of packed counters in LDS
-// (word w of lane l holds bins 2w and 2w+1 as two 16-bit counts, at
-// (w*64 + l)*4: every lane a different bank, no contention even when all
-// registers share a value, which the block-per-group kernel's shared bins
-// serialise on); 32 lanes then sum the columns and lane 0 runs hllCount().
-// A wave's LDS operations complete in order; wave_sync() keeps the compiler
-// from reordering across the cross-lane hand-offs and drains lgkmcnt.
+// rankings): one wave per key, four waves per block.  Each lane bins its 256
+// registers into a lane-private column of 64 counters in LDS (bin r of lane l
+// at wave base + r*256 + l*4: every lane a different bank, no contention even
+// when all registers share a value, which the block-per-group kernel's shared
+// bins serialise on), so a register costs one bit-field extract, one OR and
+// one ds_add.  The columns are never cleared: they keep running totals over
+// the wave's keys, lane r keeps the previous sum of bin r over the 64 columns,
+// and a key's bin r is the difference.  The sums read the columns in a
+// lane-rotated order (bank-conflict free), and the next key's registers are
+// loaded while this key is binned.  hllCount()'s 50-step dependent chain runs
+// for kK2Batch keys side by side, one lane each, once their histograms are
+// in (run per key on lane 0 it cost 0.8 ms of the 6 ms C5 pass).  A wave's LDS
+// operations complete in order; wave_sync() keeps the compiler from
+// reordering across the cross-lane hand-offs and drains lgkmcnt.
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ void __launch_bounds__(256)
+constexpr int kK2Waves = 4;
+constexpr int kK2Batch = 8;  // keys whose estimates a wave runs side by side
+__global__ void __launch_bounds__(64 * kK2Waves)
     k_pfcount_wave(const uint8_t *__restrict__ regs, const uint32_t *__restrict__ slots,
                    uint32_t nkeys, const double *__restrict__ tau_tab,
                    const double *__restrict__ sig_tab, uint64_t *__restrict__ out) {
-    __shared__ uint32_t cols[4][32 * 64];
-    __shared__ uint32_t hist[4][64];
+    __shared__ uint32_t cols[kK2Waves * 64 * 64];  // [wave][bin][lane]
+    __shared__ uint32_t hist[kK2Waves][kK2Batch][64];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t *col = cols[wave];
-    for (uint32_t g = blockIdx.x * 4 + wave; g < nkeys; g += gridDim.x * 4) {
-        const uint32_t key = slots ? slots[g] : g;
-        const uint4 *src = reinterpret_cast<const uint4 *>(regs + size_t(key) * kHllRegs);
-        uint4 v[16];
+    // byte address of this lane's bin 0; bits 8..13 stay free for the bin
+    const uint32_t base = wave * 16384 + lane * 4;
+    char *lds = reinterpret_cast<char *>(cols);
+#pragma unroll
+    for (int r = 0; r < 64; r++) *(uint32_t *)(lds + base + r * 256) = 0;
+    uint32_t prev = 0;  // lane r: sum of bin r over the columns after the last key
+    const uint32_t stride = gridDim.x * kK2Waves;
+    uint32_t g = blockIdx.x * kK2Waves + wave;
+    uint4 v[16];
+    if (g < nkeys) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(regs + size_t(slots ? slots[g] : g) * kHllRegs);
 #pragma unroll
         for (int q = 0; q < 16; q++) v[q] = src[q * 64 + lane];  // coalesced 1 KiB per step
+    }
+    wave_sync();
+    uint32_t e = 0;  // histograms waiting for their estimate
+    for (; g < nkeys; g += stride) {
+        const uint32_t gn = g + stride;
+        uint4 nv[16];
+        if (gn < nkeys) {  // the next key's registers fly while this one is binned
+            const uint4 *src =
+                reinterpret_cast<const uint4 *>(regs + size_t(slots ? slots[gn] : gn) * kHllRegs);
 #pragma unroll
-        for (int w = 0; w < 32; w++) col[w * 64 + lane] = 0;
+            for (int q = 0; q < 16; q++) nv[q] = src[q * 64 + lane];
+        }
 #pragma unroll
         for (int q = 0; q < 16; q++) {
             const uint32_t wd[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
-            for (int e = 0; e < 4; e++)
+            for (int e4 = 0; e4 < 4; e4++)
 #pragma unroll
                 for (int b = 0; b < 32; b += 8) {
-                    const uint32_t r = (wd[e] >> b) & 63;
-                    atomicAdd(&col[(r >> 1) * 64 + lane], 1u << ((r & 1) * 16));
+                    const uint32_t r = __builtin_amdgcn_ubfe(wd[e4], b, 6);
+                    __hip_atomic_fetch_add((uint32_t *)(lds + ((r << 8) | base)), 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
         }
         wave_sync();
-        if (lane < 32) {
-            uint32_t sum = 0;
+        const char *bin = lds + wave * 16384 + lane * 256;  // lane r sums bin r
+        uint32_t sum = 0;
 #pragma unroll 8
-            for (int l = 0; l < 64; l++) sum += col[lane * 64 + l];
-            hist[wave][2 * lane] = sum & 0xffffu;
-            hist[wave][2 * lane + 1] = sum >> 16;
+        for (int l = 0; l < 64; l++) sum += *(const uint32_t *)(bin + (((l + lane) & 63) << 2));
+        hist[wave][e][lane] = sum - prev;
+        prev = sum;
+        // hllCount() of the batch: lane j < kK2Batch estimates the key
+        // binned j keys after the batch's first (g - (e - j) * stride)
+        if (++e == kK2Batch || gn >= nkeys) {
+            wave_sync();
+            if (lane < e) out[g - (e - 1 - lane) * stride] = hll_estimate_dev(hist[wave][lane], tau_tab, sig_tab);
+            e = 0;
         }
         wave_sync();
-        if (lane == 0) out[g] = hll_estimate_dev(hist[wave], tau_tab, sig_tab);
-        wave_sync();
+#pragma unroll
+        for (int q = 0; q < 16; q++) v[q] = nv[q];
     }
 }
 
@@ -703,8 +734,8 @@ hipError_t launch_pfcount(const uint8_t *regs, const uint32_t *slots, const uint
                           int cus, hipStream_t st) {
     if (ngroups == 0) return hipSuccess;
     if (!goffs) {  // one key per group
-        const unsigned want = (ngroups + 3) / 4, cap = unsigned(cus) * 8;
-        hipLaunchKernelGGL(k_pfcount_wave, dim3(want < cap ? want : cap), dim3(256), 0, st, regs,
+        const unsigned want = (ngroups + kK2Waves - 1) / kK2Waves, cap = unsigned(cus) * 2;
+        hipLaunchKernelGGL(k_pfcount_wave, dim3(want < cap ? want : cap), dim3(64 * kK2Waves), 0, st, regs,
                            slots, ngroups, tau, sig, out);
         return hipGetLastError();
     }

@@ -599,3 +599,32 @@ def test_property_swipes_vs_oracle(pkg, orc):
             assert np.array_equal(client.hll_registers(k), h.regs)
 
     run()
+
+
+def test_pfcount_each_many_keys_vs_oracle(client, orc):
+    """PFCOUNT of every key over more keys than the wave-per-key kernel has
+    waves (each wave bins several keys into running-total columns), in slab
+    order (null slot list) and in a shuffled key order: every count ==
+    Redis's hllCount on the same registers."""
+    rng = np.random.default_rng(21)
+    n = 5000
+    fill = rng.integers(0, 6, n)
+    arrays = np.zeros((n, 16384), np.uint8)
+    for i in range(n):
+        dens = [0.0, 0.01, 0.1, 0.5, 0.9, 1.0][fill[i]]
+        vals = rng.geometric(0.5, 16384).clip(1, 51)
+        arrays[i] = np.where(rng.random(16384) < dens, vals, 0)
+    arrays[7] = 51
+    arrays[8] = 0
+    names = [f"k{i}" for i in range(n)]
+    for k, a in zip(names, arrays):
+        client.hll_load_registers(k, a)
+    want = np.array([orc.hll_count_regs(a) for a in arrays], np.uint64)
+    order = rng.permutation(n)
+    got = client.pfcount_each([names[i] for i in order])
+    assert np.array_equal(got, want[order])
+    slots = np.array([client.keys.slot[k.encode()] for k in names])
+    cap = client.ctx.lib.ske_hll_capacity(client.ctx.ptr)
+    out = np.zeros(cap, np.uint64)
+    client.ctx.call("ske_hll_pfcount_each", None, cap, out.ctypes.data_as(C.c_void_p), 0)
+    assert np.array_equal(out[slots], want)
