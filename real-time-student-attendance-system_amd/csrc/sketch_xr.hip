@@ -154,7 +154,10 @@ __global__ void __launch_bounds__(256)
 // waits for every probe before taking the next step).
 constexpr int kXrBatchK = 16;
 
-template <int U>
+// KB: probes issued per swipe (the smallest instantiated count >= every
+// link's k; loads past k are issued out of range, and every lane of an issued
+// load costs address-unit time whether it is in the slice or not)
+template <int U, int KB>
 __global__ void __launch_bounds__(256)
     k_xr_region_b(const ChainDev ch, uint64_t n, uint64_t chunk, XrState st,
                   unsigned long long *__restrict__ fail) {
@@ -183,13 +186,13 @@ __global__ void __launch_bounds__(256)
                 inc0[u] = st.bm[uint64_t(l) * n + ic];
                 wrap[u] = st.wrap[uint64_t(l) * n + ic];
             }
-            uint32_t byte[U][kXrBatchK], pos[U][kXrBatchK];
+            uint32_t byte[U][KB], pos[U][KB];
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const uint32_t m = inc0[u] - t;
                 inc1[u] = umin32(m, m + d);
 #pragma unroll
-                for (int j = 0; j < kXrBatchK; j++) {
+                for (int j = 0; j < KB; j++) {
                     // a probe outside the slice (or past k) reads out of range: 0,
                     // and is not tested below
                     const bool mine = uint32_t(j) < k && (x[u] - lo) < len;
@@ -204,7 +207,7 @@ __global__ void __launch_bounds__(256)
             for (int u = 0; u < U; u++) {
                 ok[u] = act[u];
 #pragma unroll
-                for (int j = 0; j < kXrBatchK; j++) {
+                for (int j = 0; j < KB; j++) {
                     const bool mine = uint32_t(j) < k && (pos[u][j] - lo) < len;
                     ok[u] &= mine ? __builtin_amdgcn_ubfe(byte[u][j], pos[u][j] & 7, 1) : 1u;
                 }
@@ -317,11 +320,20 @@ hipError_t launch_swipes_xr(const ChainDev &ch, const uint8_t *bytes, const uint
     chunk = (chunk + tile - 1) / tile * tile;
     chunks = (n + chunk - 1) / chunk;
     const dim3 g(unsigned(chunks * kRegions));
-    bool batch = region_u > 0;  // region_u < 0: the per-step loop (A/B diagnostics)
-    for (int l = 0; l < ch.nlinks; l++) batch &= ch.link[l].k <= uint32_t(kXrBatchK);
+    uint32_t kmax = 0;
+    for (int l = 0; l < ch.nlinks; l++) kmax = ch.link[l].k > kmax ? ch.link[l].k : kmax;
+    const bool batch = region_u > 0 && kmax <= uint32_t(kXrBatchK);  // < 0: the per-step loop
     if (batch) {
-        if (U >= 2) hipLaunchKernelGGL(k_xr_region_b<2>, g, dim3(256), 0, st, ch, n, chunk, s, fail);
-        else hipLaunchKernelGGL(k_xr_region_b<1>, g, dim3(256), 0, st, ch, n, chunk, s, fail);
+#define SKE_XR_B(KB)                                                                               \
+    if (U >= 2) hipLaunchKernelGGL((k_xr_region_b<2, KB>), g, dim3(256), 0, st, ch, n, chunk, s, fail); \
+    else hipLaunchKernelGGL((k_xr_region_b<1, KB>), g, dim3(256), 0, st, ch, n, chunk, s, fail);
+        if (kmax <= 7) { SKE_XR_B(7) }
+        else if (kmax <= 8) { SKE_XR_B(8) }
+        else if (kmax <= 10) { SKE_XR_B(10) }
+        else if (kmax <= 11) { SKE_XR_B(11) }
+        else if (kmax <= 13) { SKE_XR_B(13) }
+        else { SKE_XR_B(16) }
+#undef SKE_XR_B
     } else if (U == 8) hipLaunchKernelGGL(k_xr_region<8>, g, dim3(256), 0, st, ch, n, chunk, s, fail);
     else if (U == 4) hipLaunchKernelGGL(k_xr_region<4>, g, dim3(256), 0, st, ch, n, chunk, s, fail);
     else if (U == 2) hipLaunchKernelGGL(k_xr_region<2>, g, dim3(256), 0, st, ch, n, chunk, s, fail);
