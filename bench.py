@@ -6,11 +6,14 @@ swipes, 7-digit ids from a 100k-student population, 10 % invalid, 50
 lecture-day HLL keys, Bloom RESERVE 0.01 / 100k preloaded).  Inputs are
 generated on the GPU and resident in HBM before timing; each step consumes a
 distinct batch of the stream.  The K timed steps are recorded once into a HIP
-graph and replayed (one K1 launch per step, back to back on one stream), so
-the kernel's average duration is the per-step device time that rocprofv3
-reports.  (--streams 2 alternates the steps over two streams, so one batch's
-launch tail overlaps the next batch's head: about 6 % more swipes/s at C2, but
-overlapping launches have no single duration.)  N>1: one process per GPU
+graph of four independent branches (step j on branch j mod 4) and replayed,
+so one launch's tail overlaps the next launches' heads (+15 % swipes/s at C2
+over one chain; --streams 1 gives the single chain).  Overlapping launches
+have no single duration and HIP events cannot time nodes inside a graph, so
+the roofline's kernel duration comes from an untimed replay of the same K
+launches as one back-to-back chain, whose per-launch time equals rocprofv3's
+per-dispatch average (under the profiler the branches do not overlap).
+N>1: one process per GPU
 (torchrun), each rank runs its own stream over its own key shard with the
 Bloom replicated (no data-path collective; weak scaling).
 
@@ -47,17 +50,18 @@ def parse():
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: K1 parts removed (bits)")
     ap.add_argument("--xr-u", type=int, default=0, help="XCD-partitioned K1: slice-pass tile")
     ap.add_argument("--xr-fu", type=int, default=0, help="XCD-partitioned K1: finish-pass tile")
-    ap.add_argument("--streams", type=int, default=1,
-                    help="HIP streams the steps alternate over (launch tails overlap)")
+    ap.add_argument("--streams", type=int, default=4,
+                    help="HIP streams the steps alternate over, so launch tails overlap "
+                         "(with --graph 1: one graph of that many independent branches)")
     ap.add_argument("--k1-legacy", action="store_true",
                     help="diagnostic: the generic LDS K1 instead of the short-id kernel")
     ap.add_argument("--k1-grid", type=int, default=0,
                     help="blocks of the short-id LDS K1 (0: one per CU); with --streams S > 1 "
                          "consecutive steps run side by side on disjoint CUs")
     ap.add_argument("--graph", type=int, default=1,
-                    help="with --streams 1: 1 = the K timed steps are recorded once into a "
-                         "HIP graph (one K1 launch per step, each over its own resident batch) "
-                         "and replayed; 0 = launched one by one from the host")
+                    help="1 = the K timed steps are recorded once into a HIP graph (one K1 "
+                         "launch per step, each over its own resident batch, step j on branch "
+                         "j mod --streams) and replayed; 0 = launched one by one from the host")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N>1 (nccl = RCCL over xGMI; gloo only to rehearse "
                          "several ranks on a one-GPU box)")
@@ -191,6 +195,43 @@ def main():
     if args.graph and len(streams) == 1:
         # the timed steps, recorded (not run) into one uploaded graph
         graph = engine.capture(lambda: [step(args.warmup + j) for j in range(args.steps)])
+    elif args.graph and len(streams) > 1:
+        # fork/join capture: step j on branch j mod S, so one graph holds S
+        # independent chains of launches whose tails overlap on replay
+        # The average launch duration of K1 comes from an untimed replay of the
+        # same K launches as a one-stream graph (HIP events cannot time event
+        # nodes inside a graph): the kernel's own duration, without the overlap.
+        def forked():
+            fork = torch.cuda.Event()
+            joins = [torch.cuda.Event() for _ in streams[1:]]
+
+            def record():
+                fork.record(stream)
+                for s_ in streams[1:]:
+                    s_.wait_event(fork)
+                for j in range(args.steps):
+                    step(args.warmup + j)
+                for s_, ev in zip(streams[1:], joins):
+                    ev.record(s_)
+                    stream.wait_event(ev)
+                engine.set_stream(stream.cuda_stream)
+            engine.set_stream(stream.cuda_stream)
+            return engine.capture(record)
+
+        def serial():
+            one = engine.swipes_fixed_async if fixed else engine.swipes_async
+            for j in range(args.steps):
+                one(0, batches[(args.warmup + j) % nb])
+        engine.set_stream(stream.cuda_stream)
+        cal = engine.capture(serial)
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record(stream)
+        cal.launch()
+        c1.record(stream)
+        torch.cuda.synchronize()
+        cal_ms = c0.elapsed_time(c1) / args.steps
+        cal.free()
+        graph = forked()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -200,7 +241,7 @@ def main():
     # stream it runs on, so the kernel's average duration is measured even
     # though consecutive launches overlap
     per = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)] if len(streams) > 1 else []
+           for _ in range(args.steps)] if len(streams) > 1 and graph is None else []
     t0 = time.perf_counter()
     e0.record(stream)
     if graph is not None:
@@ -228,6 +269,8 @@ def main():
     # bound); several streams -- the mean of the per-launch event pairs
     step_ms = e0.elapsed_time(e1) / args.steps
     kern_ms = sum(a.elapsed_time(b) for a, b in per) / len(per) if per else step_ms
+    if graph is not None and len(streams) > 1:
+        kern_ms = cal_ms
     if world > 1:
         t = torch.tensor([elapsed, kern_ms, step_ms], dtype=torch.float64,
                          device="cuda" if args.dist_backend == "nccl" else "cpu")
