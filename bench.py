@@ -6,13 +6,15 @@ swipes, 7-digit ids from a 100k-student population, 10 % invalid, 50
 lecture-day HLL keys, Bloom RESERVE 0.01 / 100k preloaded).  Inputs are
 generated on the GPU and resident in HBM before timing; each step consumes a
 distinct batch of the stream.  The K timed steps are recorded once into a HIP
-graph of four independent branches (step j on branch j mod 4) and replayed,
-so one launch's tail overlaps the next launches' heads (+15 % swipes/s at C2
-over one chain; --streams 1 gives the single chain).  Overlapping launches
-have no single duration and HIP events cannot time nodes inside a graph, so
-the roofline's kernel duration comes from an untimed replay of the same K
-launches as one back-to-back chain, whose per-launch time equals rocprofv3's
-per-dispatch average (under the profiler the branches do not overlap).
+graph of eight independent branches (step j on branch j mod 8) and replayed;
+K1 runs on one block per two CUs, so two consecutive steps run side by side,
+each on half the chip, and one launch's fixed cost overlaps the other's
+steady state (C2: 10.6 us per step against 13.2 us for one chain of
+full-chip launches; --streams 1 gives that chain).  Overlapping launches have
+no single duration and HIP events cannot time nodes inside a graph, so the
+roofline's kernel duration comes from an untimed replay of the same K
+launches as one chain, whose per-launch time equals rocprofv3's per-dispatch
+average.
 N>1: one process per GPU
 (torchrun), each rank runs its own stream over its own key shard with the
 Bloom replicated (no data-path collective; weak scaling).
@@ -50,14 +52,15 @@ def parse():
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: K1 parts removed (bits)")
     ap.add_argument("--xr-u", type=int, default=0, help="XCD-partitioned K1: slice-pass tile")
     ap.add_argument("--xr-fu", type=int, default=0, help="XCD-partitioned K1: finish-pass tile")
-    ap.add_argument("--streams", type=int, default=4,
+    ap.add_argument("--streams", type=int, default=8,
                     help="HIP streams the steps alternate over, so launch tails overlap "
                          "(with --graph 1: one graph of that many independent branches)")
     ap.add_argument("--k1-legacy", action="store_true",
                     help="diagnostic: the generic LDS K1 instead of the short-id kernel")
-    ap.add_argument("--k1-grid", type=int, default=0,
-                    help="blocks of the short-id LDS K1 (0: one per CU); with --streams S > 1 "
-                         "consecutive steps run side by side on disjoint CUs")
+    ap.add_argument("--k1-grid", type=int, default=-1,
+                    help="blocks of the short-id LDS K1 (0: one per CU; -1: one per CU with "
+                         "--streams 1, else one per two CUs, so two consecutive steps run side "
+                         "by side, each on half the CUs)")
     ap.add_argument("--graph", type=int, default=1,
                     help="1 = the K timed steps are recorded once into a HIP graph (one K1 "
                          "launch per step, each over its own resident batch, step j on branch "
@@ -155,6 +158,9 @@ def main():
         engine.set_option("variant", args.variant)
     if args.ablate:
         engine.set_option("ablate", args.ablate)
+    if args.k1_grid < 0:
+        cus = torch.cuda.get_device_properties(local).multi_processor_count
+        args.k1_grid = cus // 2 if args.streams > 1 else 0
     if args.k1_grid:
         engine.set_option("k1_grid", args.k1_grid)
     if args.k1_legacy:
@@ -318,6 +324,7 @@ def main():
                    "id_bytes": width, "parallelism": f"dp{world} (key-sharded, Bloom replicated)",
                    "k1_variant": {0: "global-bloom", 1: "lds-bloom", 2: "xcd-regions"}[variant],
                    "tile": args.tile or 2, "layout": args.layout, "streams": args.streams,
+                   "k1_grid": args.k1_grid or "one block per CU",
                    "launch": "hip-graph" if graph is not None else "host"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -99,20 +99,22 @@ def test_c3_gpu_shard_full_step(engine, orc):
     assert engine.swipes_stats(0, b) == (probes, nvalid)
 
 
-def test_c2_bench_steps_forked_graph(engine, orc):
-    """bench.py's default timing: the steps recorded into one graph as four
-    independent branches (step j on branch j mod 4), so consecutive launches
-    overlap on replay and update the same registers concurrently."""
+@pytest.mark.parametrize("branches,grid", [(4, 0), (8, 128)])
+def test_c2_bench_steps_forked_graph(engine, orc, branches, grid):
+    """bench.py's timing: the steps recorded into one graph as independent
+    branches (step j on branch j mod B), so consecutive launches overlap on
+    replay and update the same registers concurrently; with grid 128 two
+    launches run side by side on half the CUs each (the bench default)."""
     import torch
     from rtsas_amd import synthetic
     from rtsas_amd.engine import DeviceBuffer
     w = synthetic.WORKLOADS["c2"]
     p = _setup(engine, w)
     n = w.step_swipes
-    batches = [engine.swipe_batch(p, j * n, n) for j in range(8)]
+    batches = [engine.swipe_batch(p, j * n, n) for j in range(2 * branches)]
     outs = [DeviceBuffer(engine.ctx, n) for _ in batches]
     main = torch.cuda.Stream()
-    side = [torch.cuda.Stream() for _ in range(3)]
+    side = [torch.cuda.Stream() for _ in range(branches - 1)]
     streams = [main] + side
     fork = torch.cuda.Event()
     joins = [torch.cuda.Event() for _ in side]
@@ -122,7 +124,7 @@ def test_c2_bench_steps_forked_graph(engine, orc):
         for s_ in side:
             s_.wait_event(fork)
         for j, (b, o) in enumerate(zip(batches, outs)):
-            engine.set_stream(streams[j % 4].cuda_stream)
+            engine.set_stream(streams[j % branches].cuda_stream)
             engine.swipes_async(0, b, o)
         for s_, ev in zip(side, joins):
             ev.record(s_)
@@ -130,11 +132,15 @@ def test_c2_bench_steps_forked_graph(engine, orc):
         engine.set_stream(main.cuda_stream)
 
     engine.set_stream(main.cuda_stream)
-    g = engine.capture(record)
-    g.launch()
-    torch.cuda.synchronize()
-    g.free()
-    engine.set_stream(None)
+    engine.set_option("k1_grid", grid)
+    try:
+        g = engine.capture(record)
+        g.launch()
+        torch.cuda.synchronize()
+        g.free()
+    finally:
+        engine.set_option("k1_grid", 0)
+        engine.set_stream(None)
     _, regs, answers, probes, nvalid = _oracle(orc, engine, w, p, batches, w.n_keys)
     for a, o in zip(answers, outs):
         assert np.array_equal(o.to_host(np.uint8, n), a)
