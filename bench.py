@@ -24,6 +24,7 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import functools
 import json
 import os
 import sys
@@ -202,34 +203,14 @@ def main():
         # the timed steps, recorded (not run) into one uploaded graph
         graph = engine.capture(lambda: [step(args.warmup + j) for j in range(args.steps)])
     elif args.graph and len(streams) > 1:
-        # fork/join capture: step j on branch j mod S, so one graph holds S
-        # independent chains of launches whose tails overlap on replay
-        # The average launch duration of K1 comes from an untimed replay of the
-        # same K launches as a one-stream graph (HIP events cannot time event
-        # nodes inside a graph): the kernel's own duration, without the overlap.
-        def forked():
-            fork = torch.cuda.Event()
-            joins = [torch.cuda.Event() for _ in streams[1:]]
-
-            def record():
-                fork.record(stream)
-                for s_ in streams[1:]:
-                    s_.wait_event(fork)
-                for j in range(args.steps):
-                    step(args.warmup + j)
-                for s_, ev in zip(streams[1:], joins):
-                    ev.record(s_)
-                    stream.wait_event(ev)
-                engine.set_stream(stream.cuda_stream)
-            engine.set_stream(stream.cuda_stream)
-            return engine.capture(record)
-
-        def serial():
-            one = engine.swipes_fixed_async if fixed else engine.swipes_async
-            for j in range(args.steps):
-                one(0, batches[(args.warmup + j) % nb])
+        one = engine.swipes_fixed_async if fixed else engine.swipes_async
+        timed = [functools.partial(one, 0, batches[(args.warmup + j) % nb])
+                 for j in range(args.steps)]
+        # K1's average launch duration: HIP events cannot time event nodes
+        # inside a graph, so the same K launches are first replayed (untimed)
+        # as one chain on the kernel's stream, bracketed by an event pair
         engine.set_stream(stream.cuda_stream)
-        cal = engine.capture(serial)
+        cal = engine.capture(lambda: [fn() for fn in timed])
         c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         c0.record(stream)
         cal.launch()
@@ -237,7 +218,8 @@ def main():
         torch.cuda.synchronize()
         cal_ms = c0.elapsed_time(c1) / args.steps
         cal.free()
-        graph = forked()
+        # the timed graph: step j on branch j mod S (fork/join capture)
+        graph = engine.capture_branched(timed, stream, streams[1:])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

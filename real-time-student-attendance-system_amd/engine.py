@@ -197,6 +197,33 @@ class SketchEngine:
             self.ctx.call("ske_capture_end", C.byref(g))
         return Graph(self.ctx, g.value)
 
+    def capture_branched(self, steps, main, side) -> "Graph":
+        """Record `steps` (callables, each enqueuing one *_async call) into one
+        graph of 1 + len(side) independent branches: step j on branch
+        j mod (1 + len(side)), forked from and joined back into `main` (torch
+        streams).  On replay, launches of different branches overlap; with the
+        "k1_grid" option at half the CUs two K1 launches share the chip.  The
+        context stream is `main` afterwards."""
+        import torch
+        streams = [main] + list(side)
+        fork = torch.cuda.Event()
+        joins = [torch.cuda.Event() for _ in side]
+
+        def record():
+            fork.record(main)
+            for s_ in side:
+                s_.wait_event(fork)
+            for j, fn in enumerate(steps):
+                self.set_stream(streams[j % len(streams)].cuda_stream)
+                fn()
+            for s_, ev in zip(side, joins):
+                ev.record(s_)
+                main.wait_event(ev)
+            self.set_stream(main.cuda_stream)
+
+        self.set_stream(main.cuda_stream)
+        return self.capture(record)
+
     # ---- HLL reads
     def registers(self, slot: int) -> np.ndarray:
         out = np.zeros(16384, np.uint8)

@@ -105,6 +105,7 @@ def test_c2_bench_steps_forked_graph(engine, orc, branches, grid):
     branches (step j on branch j mod B), so consecutive launches overlap on
     replay and update the same registers concurrently; with grid 128 two
     launches run side by side on half the CUs each (the bench default)."""
+    import functools
     import torch
     from rtsas_amd import synthetic
     from rtsas_amd.engine import DeviceBuffer
@@ -115,26 +116,10 @@ def test_c2_bench_steps_forked_graph(engine, orc, branches, grid):
     outs = [DeviceBuffer(engine.ctx, n) for _ in batches]
     main = torch.cuda.Stream()
     side = [torch.cuda.Stream() for _ in range(branches - 1)]
-    streams = [main] + side
-    fork = torch.cuda.Event()
-    joins = [torch.cuda.Event() for _ in side]
-
-    def record():
-        fork.record(main)
-        for s_ in side:
-            s_.wait_event(fork)
-        for j, (b, o) in enumerate(zip(batches, outs)):
-            engine.set_stream(streams[j % branches].cuda_stream)
-            engine.swipes_async(0, b, o)
-        for s_, ev in zip(side, joins):
-            ev.record(s_)
-            main.wait_event(ev)
-        engine.set_stream(main.cuda_stream)
-
-    engine.set_stream(main.cuda_stream)
+    steps = [functools.partial(engine.swipes_async, 0, b, o) for b, o in zip(batches, outs)]
     engine.set_option("k1_grid", grid)
     try:
-        g = engine.capture(record)
+        g = engine.capture_branched(steps, main, side)
         g.launch()
         torch.cuda.synchronize()
         g.free()
