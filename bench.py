@@ -6,10 +6,10 @@ swipes, 7-digit ids from a 100k-student population, 10 % invalid, 50
 lecture-day HLL keys, Bloom RESERVE 0.01 / 100k preloaded).  Inputs are
 generated on the GPU and resident in HBM before timing; each step consumes a
 distinct batch of the stream.  The K timed steps are recorded once into a HIP
-graph of eight independent branches (step j on branch j mod 8) and replayed;
+graph of sixteen independent branches (step j on branch j mod 16) and replayed;
 K1 runs on one block per two CUs, so two consecutive steps run side by side,
 each on half the chip, and one launch's fixed cost overlaps the other's
-steady state (C2: 10.6 us per step against 13.2 us for one chain of
+steady state (C2: 9.9 us per step against 13.2 us for one chain of
 full-chip launches; --streams 1 gives that chain).  Overlapping launches have
 no single duration and HIP events cannot time nodes inside a graph, so the
 roofline's kernel duration comes from an untimed replay of the same K
@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: K1 parts removed (bits)")
     ap.add_argument("--xr-u", type=int, default=0, help="XCD-partitioned K1: slice-pass tile")
     ap.add_argument("--xr-fu", type=int, default=0, help="XCD-partitioned K1: finish-pass tile")
-    ap.add_argument("--streams", type=int, default=8,
+    ap.add_argument("--streams", type=int, default=16,
                     help="HIP streams the steps alternate over, so launch tails overlap "
                          "(with --graph 1: one graph of that many independent branches)")
     ap.add_argument("--k1-legacy", action="store_true",
