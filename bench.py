@@ -218,8 +218,13 @@ def main():
         torch.cuda.synchronize()
         cal_ms = c0.elapsed_time(c1) / args.steps
         cal.free()
-        # the timed graph: step j on branch j mod S (fork/join capture)
-        graph = engine.capture_branched(timed, stream, streams[1:])
+        # the timed graph: one native call, step j on branch j mod S
+        # (ske_swipes_many_async forks its side streams from the context stream)
+        engine.swipes_many_async(0, [], branches=len(streams))  # side streams, before capture
+        torch.cuda.synchronize()
+        graph = engine.capture(lambda: engine.swipes_many_async(
+            0, [batches[(args.warmup + j) % nb] for j in range(args.steps)],
+            branches=len(streams), fixed=fixed))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -194,6 +194,30 @@ int ske_swipes_fixed(ske_ctx *ctx, uint32_t fid, const uint32_t *slot, const uin
                      uint32_t width, uint64_t n, uint8_t *out_valid, int mem);
 int ske_swipes_fixed_async(ske_ctx *ctx, uint32_t fid, const uint32_t *slot,
                            const uint8_t *bytes, uint32_t width, uint64_t n, uint8_t *out_valid);
+/* Several device-resident batches in one call (enqueue only, graph-capturable):
+ * batch j runs on branch j mod `branches` (0: SKE_MANY_DEFAULT_BRANCHES), each
+ * branch a side stream forked from and joined back into the context stream.
+ * With more than one branch the short-id K1 runs on one block per two CUs
+ * (unless the "k1_grid" option is set), so two batches share the chip.  A
+ * batch with width > 0 is fixed-width (offs unused), else bytes + offsets.
+ * Same answers and registers as calling ske_swipes_async per batch in order
+ * (the register update is a commutative max).  nbatch == 0 only creates the
+ * branches' side streams (do that once before recording the call into a
+ * graph).  No reference counterpart: the
+ * reference's processor handles one Pulsar message per loop iteration
+ * (attendance_processor.py:100-137); this is its batched-throughput form. */
+#define SKE_MANY_MAX_BRANCHES 32
+#define SKE_MANY_DEFAULT_BRANCHES 16
+typedef struct ske_swipe_batch {
+    const uint32_t *slot;
+    const uint8_t *bytes;
+    const uint32_t *offs;
+    uint32_t width;
+    uint64_t n;
+    uint8_t *out_valid;
+} ske_swipe_batch;
+int ske_swipes_many_async(ske_ctx *ctx, uint32_t fid, const ske_swipe_batch *batches,
+                          uint32_t nbatch, uint32_t branches);
 /* probe statistics of the same swipes (untimed): Bloom bit tests performed
  * and valid count, to price the algorithmic bytes of the roofline. */
 int ske_swipes_stats(ske_ctx *ctx, uint32_t fid, const uint8_t *bytes, const uint32_t *offs,

@@ -84,6 +84,11 @@ struct ske_ctx {
     // a launch on another stream first waits for the previous one
     hipEvent_t xr_done = nullptr;
     hipStream_t xr_stream = nullptr;
+    // ske_swipes_many_async: side streams of the fork/join branches (lazy)
+    hipStream_t many_st[SKE_MANY_MAX_BRANCHES - 1] = {};
+    hipEvent_t many_join[SKE_MANY_MAX_BRANCHES - 1] = {};
+    hipEvent_t many_fork = nullptr;
+    int many_n = 0;
     // ingest key table (open addressing on the 128-bit key hash)
     uint64_t *kt_key = nullptr;  // 2 per entry, kh0 == 0: empty
     uint32_t *kt_slot = nullptr;
@@ -447,6 +452,11 @@ int ske_close(ske_ctx *c) {
     if (c->err) (void)hipFree(c->err);
     if (c->zero16) (void)hipFree(c->zero16);
     if (c->xr_done) (void)hipEventDestroy(c->xr_done);
+    for (int i = 0; i < c->many_n; i++) {
+        (void)hipStreamDestroy(c->many_st[i]);
+        (void)hipEventDestroy(c->many_join[i]);
+    }
+    if (c->many_fork) (void)hipEventDestroy(c->many_fork);
     if (c->kt_key) (void)hipFree(c->kt_key);
     if (c->kt_slot) (void)hipFree(c->kt_slot);
     if (c->stats) (void)hipFree(c->stats);
@@ -909,6 +919,67 @@ int ske_swipes_async(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8
     if (!F) return SKE_EINVAL;
     static const ChainDev empty{};
     return launch_k1(c, F->exists ? cached_chain(*F) : empty, bytes, offs, 0, slot, n, out_valid);
+}
+
+// Several resident batches in one call: batch j on branch j mod B, each branch
+// a side stream forked from and joined back into the context stream (so the
+// call also records into a graph).  With B > 1 the short-id K1 runs on one
+// block per two CUs unless "k1_grid" is set, so two launches share the chip
+// and one launch's fixed cost overlaps the other's steady state.
+static int swipes_many_body(ske_ctx *c, const ChainDev &ch, const ske_swipe_batch *b,
+                            uint32_t nb, uint32_t br, hipStream_t home) {
+    HIPCHK(c, hipEventRecord(c->many_fork, home));
+    for (uint32_t i = 0; i + 1 < br; i++) HIPCHK(c, hipStreamWaitEvent(c->many_st[i], c->many_fork, 0));
+    for (uint32_t j = 0; j < nb; j++) {
+        uint32_t k = j % br;
+        c->st = k ? c->many_st[k - 1] : home;
+        int rc = launch_k1(c, ch, b[j].bytes, b[j].width ? nullptr : b[j].offs, b[j].width, b[j].slot, b[j].n,
+                           b[j].out_valid);
+        if (rc) return rc;
+    }
+    c->st = home;
+    for (uint32_t i = 0; i + 1 < br; i++) {
+        HIPCHK(c, hipEventRecord(c->many_join[i], c->many_st[i]));
+        HIPCHK(c, hipStreamWaitEvent(home, c->many_join[i], 0));
+    }
+    return SKE_OK;
+}
+
+int ske_swipes_many_async(ske_ctx *c, uint32_t fid, const ske_swipe_batch *b, uint32_t nb,
+                          uint32_t branches) {
+    if (!c || (nb && !b) || branches > SKE_MANY_MAX_BRANCHES) return SKE_EINVAL;
+    Filter *F = get_filter(c, fid);
+    if (!F) return SKE_EINVAL;
+    for (uint32_t j = 0; j < nb; j++)
+        if (!b[j].slot || (b[j].width == 0 && !b[j].offs) || b[j].width > 4096) return SKE_EINVAL;
+    uint32_t br = branches ? branches : SKE_MANY_DEFAULT_BRANCHES;
+    if (nb && br > nb) br = nb;
+    if (br > 1) {  // with nb == 0: only prepares the side streams (e.g. before capture)
+        if (!c->many_fork) HIPCHK(c, hipEventCreateWithFlags(&c->many_fork, hipEventDisableTiming));
+        while (c->many_n < int(br) - 1) {
+            HIPCHK(c, hipStreamCreateWithFlags(&c->many_st[c->many_n], hipStreamNonBlocking));
+            HIPCHK(c, hipEventCreateWithFlags(&c->many_join[c->many_n], hipEventDisableTiming));
+            c->many_n++;
+        }
+    }
+    if (nb == 0) return SKE_OK;
+    static const ChainDev empty{};
+    const ChainDev &ch = F->exists ? cached_chain(*F) : empty;
+    if (br == 1) {
+        for (uint32_t j = 0; j < nb; j++) {
+            int rc = launch_k1(c, ch, b[j].bytes, b[j].width ? nullptr : b[j].offs, b[j].width, b[j].slot, b[j].n,
+                               b[j].out_valid);
+            if (rc) return rc;
+        }
+        return SKE_OK;
+    }
+    hipStream_t home = c->st;
+    int grid0 = c->k1_grid;
+    if (!grid0) c->k1_grid = c->cus / 2 > 0 ? c->cus / 2 : 1;
+    int rc = swipes_many_body(c, ch, b, nb, br, home);
+    c->st = home;
+    c->k1_grid = grid0;
+    return rc;
 }
 
 int ske_swipes_fixed_async(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *bytes,

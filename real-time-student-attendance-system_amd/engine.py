@@ -44,6 +44,12 @@ class DeviceBuffer:
                           a.nbytes, 0)
 
 
+class SweBatch(C.Structure):
+    """ske_swipe_batch (include/sketch.h)."""
+    _fields_ = [("slot", C.c_void_p), ("bytes", C.c_void_p), ("offs", C.c_void_p),
+                ("width", C.c_uint32), ("n", C.c_uint64), ("out_valid", C.c_void_p)]
+
+
 class DeviceBatch:
     """Packed swipes resident on the device."""
 
@@ -166,6 +172,24 @@ class SketchEngine:
     def swipes_fixed_async(self, fid: int, b: DeviceBatch, out: DeviceBuffer | None = None):
         self.ctx.call("ske_swipes_fixed_async", fid, C.c_void_p(b.slot.ptr),
                       C.c_void_p(b.bytes.ptr), b.width, b.n, C.c_void_p(out.ptr) if out else None)
+
+    def swipes_many_async(self, fid: int, batches, outs=None, branches: int = 0,
+                          fixed: bool = False):
+        """Enqueue K1 over several resident batches in one native call
+        (ske_swipes_many_async): batch j on branch j mod `branches` (0: 16),
+        forked from and joined back into the context stream; with several
+        branches two launches share the chip, half the CUs each.  `fixed`:
+        read the ids as fixed-width (as swipes_fixed_async)."""
+        outs = outs if outs is not None else [None] * len(batches)
+        arr = (SweBatch * len(batches))()
+        for a, b, o in zip(arr, batches, outs):
+            a.slot, a.bytes = b.slot.ptr, b.bytes.ptr
+            a.offs = None if fixed else b.offs.ptr
+            a.width = b.width if fixed else 0
+            a.n = b.n
+            a.out_valid = o.ptr if o is not None else None
+        self.ctx.call("ske_swipes_many_async", fid, C.cast(arr, C.c_void_p), len(batches),
+                      branches)
 
     def swipes_stats(self, fid: int, b: DeviceBatch) -> tuple[int, int]:
         probes, nvalid = C.c_uint64(), C.c_uint64()

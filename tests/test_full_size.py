@@ -99,12 +99,14 @@ def test_c3_gpu_shard_full_step(engine, orc):
     assert engine.swipes_stats(0, b) == (probes, nvalid)
 
 
-@pytest.mark.parametrize("branches,grid", [(4, 0), (8, 128)])
-def test_c2_bench_steps_forked_graph(engine, orc, branches, grid):
-    """bench.py's timing: the steps recorded into one graph as independent
-    branches (step j on branch j mod B), so consecutive launches overlap on
-    replay and update the same registers concurrently; with grid 128 two
-    launches run side by side on half the CUs each (the bench default)."""
+@pytest.mark.parametrize("mode,branches", [("capture_branched", 4), ("native", 4),
+                                           ("native-graph", 16), ("native-graph-fixed", 16)])
+def test_c2_bench_steps_forked_graph(engine, orc, mode, branches):
+    """bench.py's timing: the steps recorded as independent branches (step j
+    on branch j mod B), so consecutive launches overlap and update the same
+    registers concurrently.  capture_branched: torch streams, full-chip grid;
+    native: ske_swipes_many_async (two launches side by side on half the
+    CUs), enqueued directly or recorded into a graph (the bench default)."""
     import functools
     import torch
     from rtsas_amd import synthetic
@@ -114,17 +116,30 @@ def test_c2_bench_steps_forked_graph(engine, orc, branches, grid):
     n = w.step_swipes
     batches = [engine.swipe_batch(p, j * n, n) for j in range(2 * branches)]
     outs = [DeviceBuffer(engine.ctx, n) for _ in batches]
+    fixed = mode.endswith("fixed")
     main = torch.cuda.Stream()
-    side = [torch.cuda.Stream() for _ in range(branches - 1)]
-    steps = [functools.partial(engine.swipes_async, 0, b, o) for b, o in zip(batches, outs)]
-    engine.set_option("k1_grid", grid)
+    engine.set_stream(main.cuda_stream)
     try:
-        g = engine.capture_branched(steps, main, side)
-        g.launch()
+        if mode == "capture_branched":
+            side = [torch.cuda.Stream() for _ in range(branches - 1)]
+            steps = [functools.partial(engine.swipes_async, 0, b, o)
+                     for b, o in zip(batches, outs)]
+            g = engine.capture_branched(steps, main, side)
+        elif mode == "native":
+            g = None
+            engine.swipes_many_async(0, batches, outs, branches=branches)
+        else:
+            engine.swipes_many_async(0, [], branches=branches)
+            engine.swipes_many_async(0, batches[:1], outs[:1], branches=1, fixed=fixed)
+            torch.cuda.synchronize()
+            g = engine.capture(lambda: engine.swipes_many_async(
+                0, batches[1:], outs[1:], branches=branches, fixed=fixed))
+        if g is not None:
+            g.launch()
         torch.cuda.synchronize()
-        g.free()
+        if g is not None:
+            g.free()
     finally:
-        engine.set_option("k1_grid", 0)
         engine.set_stream(None)
     _, regs, answers, probes, nvalid = _oracle(orc, engine, w, p, batches, w.n_keys)
     for a, o in zip(answers, outs):
