@@ -76,3 +76,29 @@ def test_null_context_is_rejected(pkg):
     assert lib.ske_close(None) == -1
     assert lib.ske_sync(None) == -1
     assert lib.ske_swipes(None, 0, None, None, None, 0, None, 0) == -1
+
+
+def test_swipe_batch_struct_layout(tmp_path):
+    """ctypes' SweBatch mirrors ske_swipe_batch (include/sketch.h) field by field."""
+    from rtsas_amd.engine import SweBatch
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "sketch.h"\n'
+                   "int main(void) { printf(\"%zu %zu %zu %zu %zu %zu %zu\\n\", "
+                   "sizeof(ske_swipe_batch), offsetof(ske_swipe_batch, slot), "
+                   "offsetof(ske_swipe_batch, bytes), offsetof(ske_swipe_batch, offs), "
+                   "offsetof(ske_swipe_batch, width), offsetof(ske_swipe_batch, n), "
+                   "offsetof(ske_swipe_batch, out_valid)); return 0; }\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)],
+                   check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    want = [C.sizeof(SweBatch)] + [getattr(SweBatch, f).offset
+                                   for f in ("slot", "bytes", "offs", "width", "n", "out_valid")]
+    assert got == want
+
+
+def test_swipes_many_rejects_bad_arguments(pkg):
+    lib = pkg.load_library()
+    # a null context is rejected before any device work
+    assert lib.ske_swipes_many_async(None, 0, None, 0, 0) < 0
