@@ -84,6 +84,7 @@ struct ske_ctx {
     // a launch on another stream first waits for the previous one
     hipEvent_t xr_done = nullptr;
     hipStream_t xr_stream = nullptr;
+    unsigned long long xr_cap = 0;  // capture id xr_done was recorded in (0: none)
     // ske_swipes_many_async: side streams of the fork/join branches (lazy)
     hipStream_t many_st[SKE_MANY_MAX_BRANCHES - 1] = {};
     hipEvent_t many_join[SKE_MANY_MAX_BRANCHES - 1] = {};
@@ -360,11 +361,20 @@ int launch_k1(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32
             return SKE_ENOMEM;
         }
         if (!c->xr_done) HIPCHK(c, hipEventCreateWithFlags(&c->xr_done, hipEventDisableTiming));
-        if (c->xr_stream && c->xr_stream != c->st) HIPCHK(c, hipStreamWaitEvent(c->st, c->xr_done, 0));
+        // the wait only links launches of the same capture (or of none): an event
+        // recorded outside a capture cannot be waited on inside it, nor the reverse
+        // (the caller synchronises before recording a graph, as engine.capture does)
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        unsigned long long cid = 0;
+        HIPCHK(c, hipStreamGetCaptureInfo(c->st, &cs, &cid));
+        if (cs != hipStreamCaptureStatusActive) cid = 0;
+        if (c->xr_stream && c->xr_stream != c->st && c->xr_cap == cid)
+            HIPCHK(c, hipStreamWaitEvent(c->st, c->xr_done, 0));
         HIPCHK(c, launch_swipes_xr(ch, bytes, offs, fixed_w, slot, n, c->regs, c->nslots, out,
                                    scr, c->err, c->cus, c->xr_region_u, c->xr_finish_u, c->st));
         HIPCHK(c, hipEventRecord(c->xr_done, c->st));
         c->xr_stream = c->st;
+        c->xr_cap = cid;
         return SKE_OK;
     }
     if (c->ablate) {

@@ -145,3 +145,37 @@ def test_c2_bench_steps_forked_graph(engine, orc, mode, branches):
     for a, o in zip(answers, outs):
         assert np.array_equal(o.to_host(np.uint8, n), a)
     assert np.array_equal(engine.registers_all(w.n_keys), regs)
+
+
+def test_c3_xr_many_batches_graph(engine, orc):
+    """The XCD-partitioned K1 through ske_swipes_many_async recorded into a
+    graph: its launches share the context scratch, so each waits for the
+    previous one across branches; answers and registers == the oracle."""
+    import torch
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import DeviceBuffer
+    w = synthetic.shard(synthetic.WORKLOADS["c3"], 8)
+    p = _setup(engine, w)
+    assert engine.variant(0) == 2
+    n = 1 << 21
+    batches = [engine.swipe_batch(p, j * n, n) for j in range(4)]
+    outs = [DeviceBuffer(engine.ctx, n) for _ in batches]
+    main = torch.cuda.Stream()
+    engine.set_stream(main.cuda_stream)
+    try:
+        engine.swipes_many_async(0, [], branches=4)
+        # the first call after BF.RESERVE uploads the chain descriptors (a
+        # synchronous copy), so it runs before the capture
+        engine.swipes_many_async(0, batches[:1], outs[:1], branches=1)
+        torch.cuda.synchronize()
+        g = engine.capture(lambda: engine.swipes_many_async(0, batches[1:], outs[1:],
+                                                            branches=3))
+        g.launch()
+        torch.cuda.synchronize()
+        g.free()
+    finally:
+        engine.set_stream(None)
+    _, regs, answers, probes, nvalid = _oracle(orc, engine, w, p, batches, w.n_keys)
+    for a, o in zip(answers, outs):
+        assert np.array_equal(o.to_host(np.uint8, n), a)
+    assert np.array_equal(engine.registers_all(w.n_keys), regs)
