@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: K1 parts removed (bits)")
     ap.add_argument("--xr-u", type=int, default=0, help="XCD-partitioned K1: slice-pass tile")
     ap.add_argument("--xr-fu", type=int, default=0, help="XCD-partitioned K1: finish-pass tile")
+    ap.add_argument("--part-sub", type=int, default=0,
+                    help="partitioned K1: swipes per sub-batch of its three passes (0 = default)")
     ap.add_argument("--streams", type=int, default=16,
                     help="HIP streams the steps alternate over, so launch tails overlap "
                          "(with --graph 1: one graph of that many independent branches)")
@@ -170,6 +172,8 @@ def main():
         engine.set_option("xr_region_u", args.xr_u)
     if args.xr_fu:
         engine.set_option("xr_finish_u", args.xr_fu)
+    if args.part_sub:
+        engine.set_option("part_sub", args.part_sub)
 
     # Bloom preload (replicated on every rank), HLL key shard of this rank
     engine.reserve(0, w.bf_error, w.bf_capacity)
@@ -289,7 +293,8 @@ def main():
     alg_bytes = n * s_io + 64 * probes + 128 * nvalid
     variant = engine.variant(0)
     kernel_name = {0: "k_swipes", 1: "k_swipes" if args.k1_legacy else "k_swipes_lds",
-                   2: "k_xr_hash+k_xr_region+k_xr_finish"}[variant]
+                   2: "k_xr_hash+k_xr_region+k_xr_finish",
+                   3: "k_part_a+k_part_b+k_part_c"}[variant]
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     line = {
         "metric": METRIC,
@@ -309,7 +314,8 @@ def main():
                    "hll_keys_per_gpu": w.n_keys, "invalid_frac": w.invalid_frac,
                    "bloom": {"error": w.bf_error, "capacity": w.bf_capacity},
                    "id_bytes": width, "parallelism": f"dp{world} (key-sharded, Bloom replicated)",
-                   "k1_variant": {0: "global-bloom", 1: "lds-bloom", 2: "xcd-regions"}[variant],
+                   "k1_variant": {0: "global-bloom", 1: "lds-bloom", 2: "xcd-regions",
+                                  3: "partitioned"}[variant],
                    "tile": args.tile or 2, "layout": args.layout, "streams": args.streams,
                    "k1_grid": args.k1_grid or "one block per CU",
                    "launch": "hip-graph" if graph is not None else "host"},

@@ -49,6 +49,7 @@ extern "C" {
 #define SKE_EBADEXP -10      /* "ERR expansion should be greater or equal to 1" */
 #define SKE_EBADHLL -11      /* corrupted HLL string on import */
 #define SKE_ETOOLONG -12     /* item longer than the supported maximum */
+#define SKE_EBUSY -13        /* device buffers (scratch, HLL slab) pinned by a recorded graph */
 
 #define SKE_MEM_HOST 0
 #define SKE_MEM_DEVICE 1
@@ -102,7 +103,11 @@ int ske_close(ske_ctx *ctx);
 const char *ske_strerror(int code);
 const char *ske_last_hip_error(ske_ctx *ctx);
 int ske_set_stream(ske_ctx *ctx, void *hip_stream); /* NULL = the context's own stream */
+/* Wait for the context stream.  Also reports (and clears) the sticky device
+ * error word that enqueue-only calls leave set: SKE_ERANGE when a valid swipe
+ * named an HLL slot outside the slab since the last check. */
 int ske_sync(ske_ctx *ctx);
+int ske_check_errors(ske_ctx *ctx);  /* the same check: sync + report + clear */
 int ske_device_alloc(ske_ctx *ctx, uint64_t bytes, void **out); /* device scratch for callers */
 int ske_device_free(ske_ctx *ctx, void *p);
 int ske_memcpy(ske_ctx *ctx, void *dst, const void *src, uint64_t bytes, int kind); /* 0 H2D 1 D2H 2 D2D */

@@ -27,6 +27,8 @@ SKE_EBADRATE = -8
 SKE_EBADCAP = -9
 SKE_EBADEXP = -10
 SKE_EBADHLL = -11
+SKE_ETOOLONG = -12
+SKE_EBUSY = -13
 SKE_MEM_HOST = 0
 SKE_MEM_DEVICE = 1
 SKE_MAX_FILTERS = 4096
@@ -79,6 +81,7 @@ SIGNATURES = {
     "ske_last_hip_error": (C.c_char_p, [_CTX]),
     "ske_set_stream": (C.c_int, [_CTX, _vp]),
     "ske_sync": (C.c_int, [_CTX]),
+    "ske_check_errors": (C.c_int, [_CTX]),
     "ske_device_alloc": (C.c_int, [_CTX, C.c_uint64, C.POINTER(C.c_void_p)]),
     "ske_device_free": (C.c_int, [_CTX, _vp]),
     "ske_memcpy": (C.c_int, [_CTX, _vp, _vp, C.c_uint64, C.c_int]),
@@ -173,7 +176,7 @@ def strerror(code: int) -> str:
 def check(code: int, ctx=None) -> int:
     if code < 0:
         msg = strerror(code)
-        if code == SKE_EHIP and ctx:
+        if code in (SKE_EHIP, SKE_EBUSY) and ctx:
             msg += " (" + load().ske_last_hip_error(ctx).decode() + ")"
         raise SketchLibError(code, msg)
     return code

@@ -75,6 +75,7 @@ struct ske_ctx {
     uint32_t ablate = 0;  // diagnostic only (kAblate* bits)
     int xr_region_u = 2;  // XCD-partitioned K1: swipes per lane in the slice passes
     int xr_finish_u = 1;  //   and in the finish pass
+    uint32_t part_sub = 0;  // partitioned K1: swipes per sub-batch (0: default)
     bool lds_ok = false;
     bool k1_ok = false;       // short-id LDS K1 (sketch_k1.hip) usable
     int k1_legacy = 0;        // 1: always the generic LDS kernel (A/B diagnostics)
@@ -85,6 +86,10 @@ struct ske_ctx {
     hipEvent_t xr_done = nullptr;
     hipStream_t xr_stream = nullptr;
     unsigned long long xr_cap = 0;  // capture id xr_done was recorded in (0: none)
+    // executable graphs alive (recorded, not yet freed): they hold pointers to
+    // the scratch and the register slab, so neither may be reallocated
+    int live_graphs = 0;
+    bool capturing = false;
     // ske_swipes_many_async: side streams of the fork/join branches (lazy)
     hipStream_t many_st[SKE_MANY_MAX_BRANCHES - 1] = {};
     hipEvent_t many_join[SKE_MANY_MAX_BRANCHES - 1] = {};
@@ -254,21 +259,63 @@ LinkDev link_dev(const Link &L) {
 
 bool use_lds(const ske_ctx *c, const ChainDev &ch) {
     if (!c->lds_ok || ch.nlinks == 0) return false;
-    if (c->variant == 0 || c->variant == 2) return false;
+    if (c->variant == 0 || c->variant == 2 || c->variant == 3) return false;
     return ch.lds_bytes <= lds_bloom_max();
 }
 
-// K1 variant for a chain: 1 LDS image (fits 152 KiB), 2 XCD-partitioned
-// (larger than ~2 L2s, every link <= 2^31 bits), else 0 global.
+// K1 variant for a chain: 1 LDS image (fits 152 KiB); for larger chains
+// (>= 8 MB, or when asked for) 3 partitioned (probes routed to LDS-resident
+// slices; sketch_part.hip) or 2 XCD-partitioned (L2-resident slices;
+// sketch_xr.hip) when the chain's shape does not fit the partitioned
+// kernel; else 0 global.
 constexpr uint64_t kXrMinBytes = 8ull << 20;
 int k1_variant(const ske_ctx *c, const ChainDev &ch) {
     if (ch.nlinks == 0) return 0;
     if (use_lds(c, ch)) return 1;
+    if (c->variant == 0) return 0;
     uint64_t total = 0;
     for (int l = 0; l < ch.nlinks; l++) total += ch.link[l].div.d >> 3;
-    if (!xr_supported(ch) || c->variant == 0) return 0;
-    if (c->variant == 2 || total >= kXrMinBytes) return 2;
+    const bool big = total >= kXrMinBytes || c->variant == 2 || c->variant == 3;
+    if (!big) return 0;
+    if (c->variant != 2 && part_supported(ch)) return 3;
+    if (xr_supported(ch)) return 2;
     return 0;
+}
+
+// The XCD-partitioned and partitioned K1 keep per-launch state in the
+// context scratch: a launch on another stream first waits for the previous
+// one.  The wait only links launches of the same capture (or of none): an
+// event recorded outside a capture cannot be waited on inside it, nor the
+// reverse (the caller synchronises before recording a graph, as
+// engine.capture does; ske_graph_launch records the event after a replay).
+int scratch_user_begin(ske_ctx *c, unsigned long long *cid_out) {
+    if (!c->xr_done) HIPCHK(c, hipEventCreateWithFlags(&c->xr_done, hipEventDisableTiming));
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    unsigned long long cid = 0;
+    HIPCHK(c, hipStreamGetCaptureInfo(c->st, &cs, &cid));
+    if (cs != hipStreamCaptureStatusActive) cid = 0;
+    if (c->xr_stream && c->xr_stream != c->st && c->xr_cap == cid)
+        HIPCHK(c, hipStreamWaitEvent(c->st, c->xr_done, 0));
+    *cid_out = cid;
+    return SKE_OK;
+}
+
+int scratch_user_end(ske_ctx *c, unsigned long long cid) {
+    HIPCHK(c, hipEventRecord(c->xr_done, c->st));
+    c->xr_stream = c->st;
+    c->xr_cap = cid;
+    return SKE_OK;
+}
+
+// scratch that cannot grow (a graph is being recorded, or alive) -> SKE_EBUSY
+int scratch_error(ske_ctx *c, hipError_t e) {
+    if (e == hipErrorStreamCaptureUnsupported) {
+        c->last_hip = "scratch too small while a graph is recorded or alive: run the same call "
+                      "(same or larger batch) once before recording, or free the graphs";
+        return SKE_EBUSY;
+    }
+    c->last_hip = hipGetErrorString(e);
+    return SKE_ENOMEM;
 }
 
 Filter *get_filter(ske_ctx *c, uint32_t fid) {
@@ -316,10 +363,18 @@ int ensure_tables(ske_ctx *c) {
     return SKE_OK;
 }
 
+// The device error word is sticky: kernels only ever set it (a valid swipe
+// naming a slot outside the slab).  Enqueue-only calls leave it set; the next
+// synchronous call that checks it -- a synchronous K1 / PFADD, ske_sync,
+// ske_check_errors -- reports it and clears it.
 int check_err_flag(ske_ctx *c, int code_if_set) {
     unsigned int h = 0;
     HIPCHK(c, hipMemcpyAsync(&h, c->err, 4, hipMemcpyDeviceToHost, c->st));
     HIPCHK(c, hipStreamSynchronize(c->st));
+    if (h) {
+        HIPCHK(c, hipMemsetAsync(c->err, 0, 4, c->st));
+        HIPCHK(c, hipStreamSynchronize(c->st));
+    }
     return h ? code_if_set : SKE_OK;
 }
 
@@ -353,29 +408,27 @@ int launch_k1(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32
         HIPCHK(c, launch_swipes_lds(A, true, c->pb, c->k1_grid ? c->k1_grid : c->cus, c->st));
         return SKE_OK;
     }
-    if (k1_variant(c, ch) == 2 && !c->ablate) {
+    const int var = c->ablate ? 0 : k1_variant(c, ch);
+    if (var == 3) {
+        hipError_t e = part_reserve(ch, n, c->part_sub, c->scratch);
+        if (e != hipSuccess) return scratch_error(c, e);
+        unsigned long long cid = 0;
+        int rc = scratch_user_begin(c, &cid);
+        if (rc) return rc;
+        HIPCHK(c, launch_swipes_part(ch, bytes, offs, fixed_w, slot, n, c->regs, c->nslots, out,
+                                     c->scratch, c->err, c->cus, c->part_sub, c->st));
+        return scratch_user_end(c, cid);
+    }
+    if (var == 2) {
         hipError_t e = hipSuccess;
         void *scr = scratch_get(c->scratch, 16, xr_scratch_bytes(n, ch.nlinks), &e);
-        if (e != hipSuccess) {
-            c->last_hip = hipGetErrorString(e);
-            return SKE_ENOMEM;
-        }
-        if (!c->xr_done) HIPCHK(c, hipEventCreateWithFlags(&c->xr_done, hipEventDisableTiming));
-        // the wait only links launches of the same capture (or of none): an event
-        // recorded outside a capture cannot be waited on inside it, nor the reverse
-        // (the caller synchronises before recording a graph, as engine.capture does)
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (e != hipSuccess) return scratch_error(c, e);
         unsigned long long cid = 0;
-        HIPCHK(c, hipStreamGetCaptureInfo(c->st, &cs, &cid));
-        if (cs != hipStreamCaptureStatusActive) cid = 0;
-        if (c->xr_stream && c->xr_stream != c->st && c->xr_cap == cid)
-            HIPCHK(c, hipStreamWaitEvent(c->st, c->xr_done, 0));
+        int rc = scratch_user_begin(c, &cid);
+        if (rc) return rc;
         HIPCHK(c, launch_swipes_xr(ch, bytes, offs, fixed_w, slot, n, c->regs, c->nslots, out,
                                    scr, c->err, c->cus, c->xr_region_u, c->xr_finish_u, c->st));
-        HIPCHK(c, hipEventRecord(c->xr_done, c->st));
-        c->xr_stream = c->st;
-        c->xr_cap = cid;
-        return SKE_OK;
+        return scratch_user_end(c, cid);
     }
     if (c->ablate) {
         ChainDev cha = ch;
@@ -409,6 +462,7 @@ const char *ske_strerror(int code) {
     case SKE_EBADEXP: return "ERR expansion should be greater or equal to 1";
     case SKE_EBADHLL: return "INVALIDOBJ Corrupted HLL object detected";
     case SKE_ETOOLONG: return "ERR item too long";
+    case SKE_EBUSY: return "ERR device buffers in use by a recorded graph";
     default: return "ERR unknown";
     }
 }
@@ -435,7 +489,8 @@ int ske_open(int device, ske_ctx **out) {
     c->st = c->own;
     c->filters.resize(SKE_MAX_FILTERS);
     c->scratch = scratch_new();
-    if (hipMalloc(&c->err, 64) != hipSuccess || hipMalloc(&c->stats, 64) != hipSuccess) {
+    if (hipMalloc(&c->err, 64) != hipSuccess || hipMalloc(&c->stats, 64) != hipSuccess ||
+        hipMemset(c->err, 0, 64) != hipSuccess) {
         ske_close(c);
         return SKE_ENOMEM;
     }
@@ -485,7 +540,12 @@ int ske_set_stream(ske_ctx *c, void *stream) {
 int ske_sync(ske_ctx *c) {
     if (!c) return SKE_EINVAL;
     HIPCHK(c, hipStreamSynchronize(c->st));
-    return SKE_OK;
+    return check_err_flag(c, SKE_ERANGE);
+}
+
+int ske_check_errors(ske_ctx *c) {
+    if (!c) return SKE_EINVAL;
+    return check_err_flag(c, SKE_ERANGE);
 }
 
 int ske_device_alloc(ske_ctx *c, uint64_t bytes, void **out) {
@@ -529,6 +589,11 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
         (name[3] == 'r' ? c->xr_region_u : c->xr_finish_u) = int(value);
         return SKE_OK;
     }
+    if (!strcmp(name, "part_sub")) {  // partitioned K1 sub-batch (swipes; 0 = default)
+        if (value < 0 || value > (int64_t(1) << 24)) return SKE_EINVAL;
+        c->part_sub = uint32_t(value);
+        return SKE_OK;
+    }
     if (!strcmp(name, "ablate")) {
         if (value < 0 || value > 7) return SKE_EINVAL;
         c->ablate = uint32_t(value);
@@ -545,7 +610,7 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
         return SKE_OK;
     }
     if (!strcmp(name, "variant")) {
-        if (value < -1 || value > 2) return SKE_EINVAL;
+        if (value < -1 || value > 3) return SKE_EINVAL;
         c->variant = int(value);
         return SKE_OK;
     }
@@ -835,6 +900,10 @@ int ske_bf_madd(ske_ctx *c, uint32_t fid, const uint8_t *bytes, const uint32_t *
 int ske_hll_reserve(ske_ctx *c, uint32_t nslots) {
     if (!c) return SKE_EINVAL;
     if (nslots <= c->nslots) return SKE_OK;
+    if (c->live_graphs > 0 || c->capturing) {
+        c->last_hip = "the HLL slab cannot move while a recorded graph points to it";
+        return SKE_EBUSY;
+    }
     uint64_t want = std::max<uint64_t>(nslots, uint64_t(c->nslots) * 3 / 2);
     want = std::max<uint64_t>(want, 16);
     uint8_t *nr = nullptr;
@@ -878,7 +947,6 @@ int ske_hll_pfadd(ske_ctx *c, const uint32_t *slot, const uint8_t *bytes, const 
     const uint32_t *dslot;
     rc = stage_u32(c, slot, n, mem, 2, &dslot);
     if (rc) return rc;
-    HIPCHK(c, hipMemsetAsync(c->err, 0, 4, c->st));
     if (changed) {
         uint8_t *dch = changed;
         if (mem != SKE_MEM_DEVICE) {
@@ -913,7 +981,6 @@ int ske_swipes(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *by
         dout = (uint8_t *)stage_buf(c, 3, n, &rc);
         if (rc) return rc;
     }
-    HIPCHK(c, hipMemsetAsync(c->err, 0, 4, c->st));
     static const ChainDev empty{};
     rc = launch_k1(c, F->exists ? cached_chain(*F) : empty, s.bytes, s.offs, 0, dslot, n, dout);
     if (rc) return rc;
@@ -939,20 +1006,35 @@ int ske_swipes_async(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8
 static int swipes_many_body(ske_ctx *c, const ChainDev &ch, const ske_swipe_batch *b,
                             uint32_t nb, uint32_t br, hipStream_t home) {
     HIPCHK(c, hipEventRecord(c->many_fork, home));
-    for (uint32_t i = 0; i + 1 < br; i++) HIPCHK(c, hipStreamWaitEvent(c->many_st[i], c->many_fork, 0));
-    for (uint32_t j = 0; j < nb; j++) {
+    uint32_t forked = 0;
+    int rc = SKE_OK;
+    for (; forked + 1 < br; forked++) {
+        hipError_t e = hipStreamWaitEvent(c->many_st[forked], c->many_fork, 0);
+        if (e != hipSuccess) {
+            c->last_hip = std::string("hipStreamWaitEvent(fork): ") + hipGetErrorString(e);
+            rc = SKE_EHIP;
+            break;
+        }
+    }
+    for (uint32_t j = 0; j < nb && rc == SKE_OK; j++) {
         uint32_t k = j % br;
         c->st = k ? c->many_st[k - 1] : home;
-        int rc = launch_k1(c, ch, b[j].bytes, b[j].width ? nullptr : b[j].offs, b[j].width, b[j].slot, b[j].n,
-                           b[j].out_valid);
-        if (rc) return rc;
+        rc = launch_k1(c, ch, b[j].bytes, b[j].width ? nullptr : b[j].offs, b[j].width, b[j].slot, b[j].n,
+                       b[j].out_valid);
     }
     c->st = home;
-    for (uint32_t i = 0; i + 1 < br; i++) {
-        HIPCHK(c, hipEventRecord(c->many_join[i], c->many_st[i]));
-        HIPCHK(c, hipStreamWaitEvent(home, c->many_join[i], 0));
+    // join every forked branch on every path (an unjoined side stream would
+    // invalidate a capture, and outside one leave work the home stream does
+    // not wait for); the first error is returned
+    for (uint32_t i = 0; i < forked; i++) {
+        hipError_t e = hipEventRecord(c->many_join[i], c->many_st[i]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(home, c->many_join[i], 0);
+        if (e != hipSuccess && rc == SKE_OK) {
+            c->last_hip = std::string("join: ") + hipGetErrorString(e);
+            rc = SKE_EHIP;
+        }
     }
-    return SKE_OK;
+    return rc;
 }
 
 int ske_swipes_many_async(ske_ctx *c, uint32_t fid, const ske_swipe_batch *b, uint32_t nb,
@@ -975,6 +1057,19 @@ int ske_swipes_many_async(ske_ctx *c, uint32_t fid, const ske_swipe_batch *b, ui
     if (nb == 0) return SKE_OK;
     static const ChainDev empty{};
     const ChainDev &ch = F->exists ? cached_chain(*F) : empty;
+    // the scratch of the largest batch before the first launch: batches of
+    // different sizes never reallocate it between recorded launches
+    uint64_t nmax = 0;
+    for (uint32_t j = 0; j < nb; j++) nmax = b[j].n > nmax ? b[j].n : nmax;
+    const int var = c->ablate ? 0 : k1_variant(c, ch);
+    if (var == 3 && nmax) {
+        hipError_t e = part_reserve(ch, nmax, c->part_sub, c->scratch);
+        if (e != hipSuccess) return scratch_error(c, e);
+    } else if (var == 2 && nmax) {
+        hipError_t e = hipSuccess;
+        (void)scratch_get(c->scratch, 16, xr_scratch_bytes(nmax, ch.nlinks), &e);
+        if (e != hipSuccess) return scratch_error(c, e);
+    }
     if (br == 1) {
         for (uint32_t j = 0; j < nb; j++) {
             int rc = launch_k1(c, ch, b[j].bytes, b[j].width ? nullptr : b[j].offs, b[j].width, b[j].slot, b[j].n,
@@ -1024,7 +1119,6 @@ int ske_swipes_fixed(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8
             if (rc) return rc;
         }
     }
-    HIPCHK(c, hipMemsetAsync(c->err, 0, 4, c->st));
     rc = ske_swipes_fixed_async(c, fid, dslot, db, width, n, dout);
     if (rc) return rc;
     if (out_valid && mem != SKE_MEM_DEVICE)
@@ -1415,7 +1509,6 @@ int ske_ingest_swipes(ske_ctx *c, uint32_t fid, const uint8_t *msgs, const ske_i
     const IngestCols k = ingest_cols(cols);
     HIPCHK(c, launch_ingest_pack(msgs, k, slot, flag_incl, len_incl, n, ids, ids_offs, kslot, c->cus,
                                  c->st));
-    HIPCHK(c, hipMemsetAsync(c->err, 0, 4, c->st));
     HIPCHK(c, hipMemsetAsync(kvalid, 0, size_t(taken) + 4, c->st));
     if (taken && F->exists) {
         rc = launch_k1(c, cached_chain(*F), ids, ids_offs, 0, kslot, taken, kvalid);
@@ -1430,6 +1523,8 @@ int ske_ingest_swipes(ske_ctx *c, uint32_t fid, const uint8_t *msgs, const ske_i
 int ske_capture_begin(ske_ctx *c) {
     if (!c) return SKE_EINVAL;
     HIPCHK(c, hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
+    c->capturing = true;
+    scratch_set_recording(c->scratch, true);
     return SKE_OK;
 }
 
@@ -1437,34 +1532,55 @@ int ske_capture_end(ske_ctx *c, void **graph_out) {
     if (!c || !graph_out) return SKE_EINVAL;
     *graph_out = nullptr;
     hipGraph_t g = nullptr;
-    HIPCHK(c, hipStreamEndCapture(c->st, &g));
+    c->capturing = false;
+    scratch_set_recording(c->scratch, false);
+    hipError_t e = hipStreamEndCapture(c->st, &g);
     hipGraphExec_t ge = nullptr;
-    hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(g);
-    if (e != hipSuccess) {
-        c->last_hip = std::string("hipGraphInstantiate: ") + hipGetErrorString(e);
-        return SKE_EHIP;
+    const char *what = "hipStreamEndCapture";
+    if (e == hipSuccess) {
+        what = "hipGraphInstantiate";
+        e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
     }
-    e = hipGraphUpload(ge, c->st);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+    if (e == hipSuccess) {
+        what = "hipGraphUpload";
+        e = hipGraphUpload(ge, c->st);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+        if (e != hipSuccess) (void)hipGraphExecDestroy(ge);
+    }
     if (e != hipSuccess) {
-        (void)hipGraphExecDestroy(ge);
-        c->last_hip = std::string("hipGraphUpload: ") + hipGetErrorString(e);
+        // no graph holds what this capture pinned
+        if (c->live_graphs == 0) scratch_unpin(c->scratch);
+        c->last_hip = std::string(what) + ": " + hipGetErrorString(e);
         return SKE_EHIP;
     }
     *graph_out = ge;
+    c->live_graphs++;  // the slots it pinned stay pinned until every graph is freed
     return SKE_OK;
 }
 
 int ske_graph_launch(ske_ctx *c, void *graph) {
     if (!c || !graph) return SKE_EINVAL;
     HIPCHK(c, hipGraphLaunch(hipGraphExec_t(graph), c->st));
+    // a replay may hold scratch users (the partitioned / XCD-partitioned K1):
+    // a later direct launch on another stream waits for it.  Two replays of
+    // graphs holding scratch users on different streams are not ordered by
+    // this; replay such graphs on one stream.
+    if (c->xr_done) {
+        HIPCHK(c, hipEventRecord(c->xr_done, c->st));
+        c->xr_stream = c->st;
+        c->xr_cap = 0;
+    }
     return SKE_OK;
 }
 
 int ske_graph_free(ske_ctx *c, void *graph) {
     if (!c) return SKE_EINVAL;
-    if (graph) HIPCHK(c, hipGraphExecDestroy(hipGraphExec_t(graph)));
+    if (graph) {
+        HIPCHK(c, hipGraphExecDestroy(hipGraphExec_t(graph)));
+        if (c->live_graphs > 0) c->live_graphs--;
+        if (c->live_graphs == 0 && !c->capturing) scratch_unpin(c->scratch);
+    }
     return SKE_OK;
 }
 

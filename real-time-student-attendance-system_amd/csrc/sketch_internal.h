@@ -97,9 +97,28 @@ hipError_t launch_swipes_xr(const ChainDev &ch, const uint8_t *bytes, const uint
                             uint32_t nslots, uint8_t *out, void *scratch, unsigned int *err,
                             int cus, int region_u, int finish_u, hipStream_t st);
 
+// sketch_part.hip -- partitioned K1 (probe records routed to LDS-resident
+// 64 KiB slices of each link) for chains larger than the LDS image
+constexpr int kPSliceLog = 19;
+constexpr uint32_t kPSliceBits = 1u << kPSliceLog;
+constexpr uint32_t kPMaxSlices = 2047;
+constexpr int kPMaxLinks = 8;
+struct Scratch;
+bool part_supported(const ChainDev &ch);
+// sizes the context scratch for batches of up to n swipes (no launch)
+// sub: swipes per sub-batch of the three passes (0: the default, 16M)
+hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub, Scratch *scr);
+hipError_t launch_swipes_part(const ChainDev &ch, const uint8_t *bytes, const uint32_t *offs,
+                              uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *regs,
+                              uint32_t nslots, uint8_t *out, Scratch *scr, unsigned int *err, int cus,
+                              uint32_t sub, hipStream_t st);
+
 // sketch_order.hip -- order-exact paths (replies that depend on item order)
 struct Scratch;  // growable device scratch, owned by the context
+constexpr int kScratchSlots = 40;
 void *scratch_get(Scratch *s, int slot, size_t bytes, hipError_t *err);
+void scratch_set_recording(Scratch *s, bool on);  // slots handed out now get pinned
+void scratch_unpin(Scratch *s);                    // every graph freed: slots may grow
 
 // PFADD with per-element "changed" flags in sequential order.
 hipError_t pfadd_exact(Scratch *s, const uint32_t *slot, const uint8_t *bytes,

@@ -20,12 +20,29 @@
 namespace ske {
 
 struct Scratch {
-    void *p[32] = {};
-    size_t cap[32] = {};
+    void *p[kScratchSlots] = {};
+    size_t cap[kScratchSlots] = {};
+    bool recording = false;              // a stream capture is recording
+    bool pinned[kScratchSlots] = {};     // handed out while recording
 };
 
+void scratch_set_recording(Scratch *s, bool on) { s->recording = on; }
+void scratch_unpin(Scratch *s) {
+    for (int i = 0; i < kScratchSlots; i++) s->pinned[i] = false;
+}
+
+// A slot grows by hipFree + hipMalloc.  A slot handed out while a graph was
+// being recorded is pinned until every graph is freed: its growth is refused
+// with hipErrorStreamCaptureUnsupported (the allocation would be prohibited
+// inside a capture, and the hipFree would release memory that recorded nodes
+// still point to).
 void *scratch_get(Scratch *s, int slot, size_t bytes, hipError_t *err) {
     if (bytes == 0) bytes = 16;
+    if (s->recording) s->pinned[slot] = true;
+    if (s->cap[slot] < bytes && s->pinned[slot]) {
+        *err = hipErrorStreamCaptureUnsupported;
+        return nullptr;
+    }
     if (s->cap[slot] < bytes) {
         if (s->p[slot]) (void)hipFree(s->p[slot]);
         s->p[slot] = nullptr;
@@ -42,7 +59,7 @@ void *scratch_get(Scratch *s, int slot, size_t bytes, hipError_t *err) {
 }
 
 void scratch_free_all(Scratch *s) {
-    for (int i = 0; i < 32; i++)
+    for (int i = 0; i < kScratchSlots; i++)
         if (s->p[i]) (void)hipFree(s->p[i]);
 }
 

@@ -207,7 +207,12 @@ class SketchEngine:
         self.ctx.call("ske_set_stream", C.c_void_p(stream_ptr) if stream_ptr else None)
 
     def sync(self):
+        """Wait for the context stream; raises SKE_ERANGE (SketchLibError)
+        when an enqueued K1 met a valid swipe whose slot is outside the slab."""
         self.ctx.call("ske_sync")
+
+    def check_errors(self):
+        self.ctx.call("ske_check_errors")
 
     # ---- HIP graphs: record enqueue-only calls once, replay many times
     def capture(self, fn) -> "Graph":
@@ -216,9 +221,15 @@ class SketchEngine:
         self.ctx.call("ske_capture_begin")
         try:
             fn()
-        finally:
+        except BaseException:
+            # end the capture (the stream must leave capture mode) and drop
+            # the partial graph; the recording call's error is the one raised
             g = C.c_void_p()
-            self.ctx.call("ske_capture_end", C.byref(g))
+            if self.ctx.lib.ske_capture_end(self.ctx.ptr, C.byref(g)) == 0 and g.value:
+                self.ctx.lib.ske_graph_free(self.ctx.ptr, g)
+            raise
+        g = C.c_void_p()
+        self.ctx.call("ske_capture_end", C.byref(g))
         return Graph(self.ctx, g.value)
 
     def capture_branched(self, steps, main, side) -> "Graph":

@@ -9,7 +9,8 @@ bench.py measures are checked exactly, not only through properties:
   members: one decimal digit changed), one 1M-swipe step;
 - C3: one GPU's shard of the 8-GPU C3 run (10M-member filter of 19.8 MB,
   12.5k Zipf lecture-day keys), one 16M-swipe step through the
-  XCD-partitioned K1.
+  partitioned K1 (and the XCD-partitioned one);
+- C3 at one GPU of the driver's N=1 bench (100k keys), one 16M-swipe step.
 
 Answers, every register array and the probe / valid counts must equal the
 oracle's (attendance_processor.py:100-137 restated, oracle/sketch_oracle.c).
@@ -82,13 +83,15 @@ def test_c4_adversarial_step(engine, orc):
     assert 0.49 < nvalid / b.n < 0.52
 
 
-def test_c3_gpu_shard_full_step(engine, orc):
+@pytest.mark.parametrize("variant", [-1, 2])
+def test_c3_gpu_shard_full_step(engine, orc, variant):
     from rtsas_amd import synthetic
     from rtsas_amd.engine import DeviceBuffer
     w = synthetic.shard(synthetic.WORKLOADS["c3"], 8)
     assert w.n_keys == 12_500 and w.step_swipes == 16_000_000
     p = _setup(engine, w)
-    assert engine.variant(0) == 2  # XCD-partitioned K1 for the 19.8 MB filter
+    assert engine.variant(0) == 3  # partitioned K1 for the 19.8 MB filter
+    engine.set_option("variant", variant)
     b = engine.swipe_batch(p, 0, w.step_swipes)
     out = DeviceBuffer(engine.ctx, b.n)
     engine.swipes(0, b, out)
@@ -147,26 +150,40 @@ def test_c2_bench_steps_forked_graph(engine, orc, mode, branches):
     assert np.array_equal(engine.registers_all(w.n_keys), regs)
 
 
-def test_c3_xr_many_batches_graph(engine, orc):
-    """The XCD-partitioned K1 through ske_swipes_many_async recorded into a
-    graph: its launches share the context scratch, so each waits for the
-    previous one across branches; answers and registers == the oracle."""
+@pytest.mark.parametrize("variant", [-1, 2])
+def test_c3_many_batches_graph(engine, orc, variant):
+    """The partitioned (and XCD-partitioned) K1 through ske_swipes_many_async
+    recorded into a graph, batches of different sizes: its launches share the
+    context scratch (sized for the largest batch before the first launch), so
+    each waits for the previous one across branches; answers and registers ==
+    the oracle."""
     import torch
     from rtsas_amd import synthetic
     from rtsas_amd.engine import DeviceBuffer
     w = synthetic.shard(synthetic.WORKLOADS["c3"], 8)
     p = _setup(engine, w)
-    assert engine.variant(0) == 2
-    n = 1 << 21
-    batches = [engine.swipe_batch(p, j * n, n) for j in range(4)]
-    outs = [DeviceBuffer(engine.ctx, n) for _ in batches]
+    engine.set_option("variant", variant)
+    assert engine.variant(0) == (3 if variant == -1 else 2)
+    sizes = [1 << 21, 1 << 20, 3 << 20, 1 << 21]
+    starts = np.cumsum([0] + sizes)
+    batches = [engine.swipe_batch(p, int(s), n) for s, n in zip(starts, sizes)]
+    outs = [DeviceBuffer(engine.ctx, b.n) for b in batches]
     main = torch.cuda.Stream()
     engine.set_stream(main.cuda_stream)
     try:
         engine.swipes_many_async(0, [], branches=4)
-        # the first call after BF.RESERVE uploads the chain descriptors (a
-        # synchronous copy), so it runs before the capture
+        # the first call sizes the scratch for the largest batch of the graph:
+        # a capture cannot allocate (the recorded call would fail with EBUSY)
         engine.swipes_many_async(0, batches[:1], outs[:1], branches=1)
+        torch.cuda.synchronize()
+        from rtsas_amd._lib import SketchLibError, SKE_EBUSY
+        if variant == -1:
+            with pytest.raises(SketchLibError) as ei:
+                engine.capture(lambda: engine.swipes_many_async(0, batches[1:], outs[1:],
+                                                                branches=3))
+            assert ei.value.code == SKE_EBUSY
+            torch.cuda.synchronize()
+        engine.swipes_many_async(0, batches[2:3], outs[2:3], branches=1)  # the largest
         torch.cuda.synchronize()
         g = engine.capture(lambda: engine.swipes_many_async(0, batches[1:], outs[1:],
                                                             branches=3))
@@ -175,7 +192,27 @@ def test_c3_xr_many_batches_graph(engine, orc):
         g.free()
     finally:
         engine.set_stream(None)
+    # batch 2 ran twice (sizing call + graph): registers are a max, answers equal
     _, regs, answers, probes, nvalid = _oracle(orc, engine, w, p, batches, w.n_keys)
-    for a, o in zip(answers, outs):
-        assert np.array_equal(o.to_host(np.uint8, n), a)
+    for a, o, b in zip(answers, outs, batches):
+        assert np.array_equal(o.to_host(np.uint8, b.n), a)
     assert np.array_equal(engine.registers_all(w.n_keys), regs)
+
+
+def test_c3_bench_shard_one_gpu(engine, orc):
+    """C3 as the driver's N=1 bench runs it (synthetic.shard(c3, 1): 100k
+    Zipf lecture-day keys, a 1.6 GB slab), one 16M-swipe step through the
+    partitioned K1, bit-exact vs the oracle on every answer and register."""
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import DeviceBuffer
+    w = synthetic.shard(synthetic.WORKLOADS["c3"], 1)
+    assert w.n_keys == 100_000
+    p = _setup(engine, w)
+    assert engine.variant(0) == 3
+    b = engine.swipe_batch(p, 0, w.step_swipes)
+    out = DeviceBuffer(engine.ctx, b.n)
+    engine.swipes(0, b, out)
+    _, regs, answers, _, _ = _oracle(orc, engine, w, p, [b], w.n_keys)
+    assert np.array_equal(out.to_host(np.uint8, b.n), answers[0])
+    got = engine.registers_all(w.n_keys)
+    assert np.array_equal(got, regs)

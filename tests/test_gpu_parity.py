@@ -227,7 +227,7 @@ def _oracle_swipes(orc, chain, nkeys, buf, offs, slot):
     return valid, regs, probes
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("pb", [1, 4, 8])
 def test_swipes_c2_shape_vs_oracle(engine, orc, variant, pb):
     """Fused BF.EXISTS + PFADD on a C2-shaped stream (7-digit ids, 10 %
@@ -257,7 +257,7 @@ def test_swipes_c2_shape_vs_oracle(engine, orc, variant, pb):
     assert engine.variant(0) == variant
 
 
-@pytest.mark.parametrize("variant", [-1, 0, 2])
+@pytest.mark.parametrize("variant", [-1, 0, 2, 3])
 def test_swipes_facade_multilink_and_ragged(client, orc, variant):
     """swipes() over a 4-link default chain with ragged ids (0..40 B), keys
     created only when they receive a valid swipe; every K1 variant."""
@@ -375,7 +375,7 @@ def test_hll_get_set_interop(client, orc):
     assert client.pfcount("hll:b") == h.count()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_swipes_fixed_width_equals_offsets(engine, orc, variant):
     """ske_swipes_fixed (ids at bytes + i*width, no offsets) == ske_swipes on
     the same batch == the oracle, registers and flags."""
@@ -404,18 +404,22 @@ def test_swipes_fixed_width_equals_offsets(engine, orc, variant):
     assert np.array_equal(regs[w.n_keys:], oregs)
 
 
-def test_swipes_c3_filter_xcd_regions_vs_oracle(engine, orc):
-    """The XCD-partitioned K1 at C3's real filter size (RESERVE 0.001 / 1e7:
-    19.8 MB, 158M bits, k = 11, slices of ~2.5 MB) on a 1.5M-swipe slice of
-    the C3 stream (Zipf keys), bit-exact vs the oracle; and equal to the
-    global-Bloom variant on the next slice."""
+@pytest.mark.parametrize("variant", [-1, 2])
+def test_swipes_c3_filter_vs_oracle(engine, orc, variant):
+    """K1 at C3's real filter size (RESERVE 0.001 / 1e7: 19.8 MB, 158M bits,
+    k = 11) on a 1.5M-swipe slice of the C3 stream (Zipf keys), bit-exact vs
+    the oracle: the default partitioned K1 (302 LDS slices of 64 KiB) and the
+    XCD-partitioned one (L2 slices of ~2.5 MB); and equal to the global-Bloom
+    variant on the same batch."""
     from rtsas_amd import synthetic
     from rtsas_amd.engine import DeviceBuffer
     w = synthetic.WORKLOADS["c3"]
     engine.reserve(0, w.bf_error, w.bf_capacity)
     p = engine.gen_params(w)
     engine.preload(0, p, w.n_members)
-    assert engine.variant(0) == 2
+    assert engine.variant(0) == 3
+    engine.set_option("variant", variant)
+    assert engine.variant(0) == (3 if variant == -1 else variant)
     keys = 2000  # the stream's first keys only: keep the oracle's slab small
     w_small = synthetic.Workload(**{**w.__dict__, "n_keys": keys, "zipf_lectures": 20,
                                     "zipf_days": 100})
@@ -472,7 +476,7 @@ def test_graph_replay_equals_eager(engine):
         assert np.array_equal(o.to_host(np.uint8, b.n), a)
 
 
-@pytest.mark.parametrize("variant", [-1, 2])
+@pytest.mark.parametrize("variant", [-1, 2, 3])
 def test_two_streams_equal_one_stream(engine, variant):
     """Launches alternating over two HIP streams (overlapping K1 kernels; the
     XCD-partitioned variant serialises on its scratch) leave the same

@@ -1,0 +1,177 @@
+"""The partitioned K1 (sketch_part.hip) beyond the shared variant tests, the
+error channel of the enqueue-only calls, and graph / scratch safety.
+
+- multi-link chains through the partitioned kernel (links of different k,
+  slices numbered across links), ragged ids of 0..40 bytes;
+- ske_swipes_many_async with an out-of-range HLL slot, enqueued directly and
+  recorded into a graph: the sticky device error word surfaces as SKE_ERANGE
+  at ske_check_errors / ske_sync (the swipe's BF.EXISTS answer is still
+  written; its PFADD is dropped), and the next call starts clean;
+- a graph replay followed at once by a direct launch on a second stream:
+  both use the context scratch, the direct launch waits for the replay
+  (ADVICE r1), answers and registers == the oracle.
+
+Every check is bit-exact against the oracle (oracle/sketch_oracle.c, the
+restatement of RedisBloom SBChain_Check + Redis hllAdd that
+attendance_processor.py:109-113 / :127-129 reach).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand_items(rng, n, maxlen, minlen=0):
+    lens = rng.integers(minlen, maxlen + 1, n)
+    return [rng.integers(0, 256, int(l), dtype=np.uint8).tobytes() for l in lens]
+
+
+def _pack(items):
+    offs = np.zeros(len(items) + 1, np.uint32)
+    offs[1:] = np.cumsum([len(x) for x in items])
+    buf = np.frombuffer(b"".join(items) + b"\0" * 16, np.uint8).copy()
+    return buf, offs
+
+
+def test_partitioned_two_link_chain_ragged(engine, orc):
+    """RESERVE 0.01 / 20000 grown to two links (k = 8, 9: 17 probes per swipe,
+    tiles of 1024 swipes), ragged ids; the partitioned kernel forced."""
+    from rtsas_amd.engine import DeviceBatch, DeviceBuffer
+    rng = np.random.default_rng(21)
+    members = _rand_items(rng, 30000, 40, 1)
+    engine.reserve(0, 0.01, 20000)
+    mb, mo = _pack(members)
+    dm = DeviceBatch.from_host(engine.ctx, mb, mo, np.zeros(len(members), np.uint32))
+    import ctypes as C
+    engine.ctx.call("ske_bf_madd", 0, C.c_void_p(dm.bytes.ptr), C.c_void_p(dm.offs.ptr),
+                    len(members), None, 1)
+    chain = orc.Chain(20000, 0.01)
+    chain.madd_packed(mb, mo)
+    assert chain.nlinks == 2
+    engine.set_option("variant", 3)
+    assert engine.variant(0) == 3
+    items = [members[int(i)] for i in rng.integers(0, len(members), 60000)]
+    items += _rand_items(rng, 20000, 40)
+    items += [b"", b"x"]
+    keys = rng.integers(0, 37, len(items)).astype(np.uint32)
+    buf, offs = _pack(items)
+    engine.hll_reserve(37)
+    b = DeviceBatch.from_host(engine.ctx, buf, offs, keys)
+    out = DeviceBuffer(engine.ctx, b.n)
+    engine.swipes(0, b, out)
+    regs = np.zeros((37, 16384), np.uint8)
+    valid, _, _ = orc.process_swipes(chain, regs, keys, buf, offs)
+    assert np.array_equal(out.to_host(np.uint8, b.n), valid)
+    assert np.array_equal(engine.registers_all(37), regs)
+
+
+def _c3_small(engine, n_members=200_000):
+    from rtsas_amd import synthetic
+    w = synthetic.WORKLOADS["c3"]
+    w = synthetic.Workload(**{**w.__dict__, "n_members": n_members, "n_keys": 64,
+                              "zipf_lectures": 0, "zipf_days": 0})
+    engine.reserve(0, w.bf_error, w.bf_capacity)   # the 19.8 MB C3 geometry
+    p = engine.gen_params(w)
+    engine.preload(0, p, w.n_members)
+    engine.hll_reserve(w.n_keys)
+    assert engine.variant(0) == 3
+    return w, p
+
+
+@pytest.mark.parametrize("mode", ["direct", "graph"])
+def test_many_async_out_of_range_slot_surfaces(engine, orc, mode):
+    import torch
+    from rtsas_amd._lib import SketchLibError, SKE_ERANGE
+    from rtsas_amd.engine import DeviceBuffer
+    w, p = _c3_small(engine)
+    cap = engine.ctx.lib.ske_hll_capacity(engine.ctx.ptr)
+    bs = [engine.swipe_batch(p, j * 300_000, 300_000) for j in range(3)]
+    good = [b.slot.to_host(np.uint32, b.n) for b in bs]
+    bad = good[1].copy()
+    bad[12345] = cap + 7          # one swipe names a slot past the slab
+    bs[1].slot.from_host(bad)
+    outs = [DeviceBuffer(engine.ctx, b.n) for b in bs]
+    main = torch.cuda.Stream()
+    engine.set_stream(main.cuda_stream)
+    try:
+        engine.swipes_many_async(0, [], branches=2)
+        if mode == "direct":
+            engine.swipes_many_async(0, bs, outs, branches=2)
+        else:
+            engine.swipes_many_async(0, bs[:1], outs[:1], branches=1)  # sizes the scratch
+            torch.cuda.synchronize()
+            g = engine.capture(lambda: engine.swipes_many_async(0, bs, outs, branches=2))
+            g.launch()
+        with pytest.raises(SketchLibError) as ei:
+            engine.check_errors()
+        assert ei.value.code == SKE_ERANGE
+        engine.check_errors()     # cleared: the next check is clean
+        if mode == "graph":
+            g.free()
+    finally:
+        engine.set_stream(None)
+    # answers are still BF.EXISTS for every swipe; the bad swipe's PFADD is
+    # dropped (the oracle sends it to a spare row that is not compared)
+    chain = orc.Chain(w.bf_capacity, w.bf_error)
+    mb = engine.members_batch(p, 0, w.n_members).to_host()
+    chain.madd_packed(mb[0], mb[1])
+    regs = np.zeros((w.n_keys + 1, 16384), np.uint8)
+    for j, b in enumerate(bs):
+        buf, offs, _ = b.to_host()
+        sl = good[j].copy()
+        if j == 1:
+            sl[12345] = w.n_keys
+        v, _, _ = orc.process_swipes(chain, regs, sl, buf, offs)
+        assert np.array_equal(outs[j].to_host(np.uint8, b.n), v)
+    assert np.array_equal(engine.registers_all(w.n_keys), regs[:w.n_keys])
+
+
+def test_graph_replay_then_direct_launch_other_stream(engine, orc):
+    """A replayed graph holding the partitioned K1 and a direct K1 launch on
+    a second stream right behind it share the scratch: the direct launch
+    waits for the replay."""
+    import torch
+    from rtsas_amd.engine import DeviceBuffer
+    w, p = _c3_small(engine)
+    bs = [engine.swipe_batch(p, j * 500_000, 500_000) for j in range(3)]
+    outs = [DeviceBuffer(engine.ctx, b.n) for b in bs]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    engine.set_stream(s1.cuda_stream)
+    try:
+        engine.swipes_async(0, bs[0], outs[0])
+        torch.cuda.synchronize()
+        g = engine.capture(lambda: [engine.swipes_async(0, b, o) for b, o in zip(bs[:2], outs[:2])])
+        g.launch()
+        engine.set_stream(s2.cuda_stream)
+        engine.swipes_async(0, bs[2], outs[2])
+        torch.cuda.synchronize()
+        g.free()
+    finally:
+        engine.set_stream(None)
+    chain = orc.Chain(w.bf_capacity, w.bf_error)
+    mb = engine.members_batch(p, 0, w.n_members).to_host()
+    chain.madd_packed(mb[0], mb[1])
+    regs = np.zeros((w.n_keys, 16384), np.uint8)
+    for b, o in zip(bs, outs):
+        buf, offs, slot = b.to_host()
+        v, _, _ = orc.process_swipes(chain, regs, slot.astype(np.uint32), buf, offs)
+        assert np.array_equal(o.to_host(np.uint8, b.n), v)
+    assert np.array_equal(engine.registers_all(w.n_keys), regs)
+
+
+def test_hll_reserve_refused_while_graph_alive(engine):
+    from rtsas_amd._lib import SketchLibError, SKE_EBUSY
+    from rtsas_amd.engine import DeviceBuffer
+    w, p = _c3_small(engine, n_members=10_000)
+    b = engine.swipe_batch(p, 0, 100_000)
+    out = DeviceBuffer(engine.ctx, b.n)
+    engine.swipes(0, b, out)
+    g = engine.capture(lambda: engine.swipes_async(0, b, out))
+    cap = engine.ctx.lib.ske_hll_capacity(engine.ctx.ptr)
+    with pytest.raises(SketchLibError) as ei:
+        engine.hll_reserve(cap + 100)
+    assert ei.value.code == SKE_EBUSY
+    g.launch()
+    engine.sync()
+    g.free()
+    engine.hll_reserve(cap + 100)  # no graph holds the slab any more
