@@ -1,30 +1,38 @@
 """Benchmark of the fused validate-and-count hot path (K1: BF.EXISTS +
-valid-gated PFADD) -- BASELINE.json's metric on its configs[1] (C2).
+valid-gated PFADD) -- BASELINE.json's metric on its north-star configuration.
 
-One step = one K1 launch over one resident batch of synthetic swipes (C2: 1M
-swipes, 7-digit ids from a 100k-student population, 10 % invalid, 50
-lecture-day HLL keys, Bloom RESERVE 0.01 / 100k preloaded).  Inputs are
-generated on the GPU and resident in HBM before timing; each step consumes a
-distinct batch of the stream.  The K timed steps are recorded once into a HIP
-graph of sixteen independent branches (step j on branch j mod 16) and replayed;
-K1 runs on one block per two CUs, so two consecutive steps run side by side,
-each on half the chip, and one launch's fixed cost overlaps the other's
-steady state (C2: 9.9 us per step against 13.2 us for one chain of
-full-chip launches; --streams 1 gives that chain).  Overlapping launches have
-no single duration and HIP events cannot time nodes inside a graph, so the
-roofline's kernel duration comes from an untimed replay of the same K
-launches as one chain, whose per-launch time equals rocprofv3's per-dispatch
-average.
-N>1: one process per GPU
-(torchrun), each rank runs its own stream over its own key shard with the
-Bloom replicated (no data-path collective; weak scaling).
+Default workload: C3 (configs[2], the configuration BASELINE.md quotes the
+1/2/4/8-GPU curve on), this rank's shard of it: the replicated 10M-student
+Bloom filter (RESERVE 0.001 / 1e7: 19.8 MB, k = 11) preloaded by BF.MADD, a
+Zipf(1.1)-over-lectures x uniform-over-days stream of 8-digit ids with 10 %
+invalid swipes, and this rank's HLL keys (100k at N = 1, 12.5k per rank at
+N = 8; synthetic.shard).  One step = one K1 call over one resident batch of
+16M swipes (answers written, PFADD of the valid ones): the partitioned K1,
+three kernels (sketch_part.hip: hash + probe records, LDS-slice probes,
+answers + register max).  `--config c2` runs C2 (1M swipes, the LDS K1).
+
+Inputs are generated on the GPU and resident in HBM before timing; every
+step consumes a distinct batch of the stream.  Timing: W untimed warm-up
+steps, then K steps bracketed by barrier + synchronize; value = swipes of all
+ranks / the slowest rank's wall time.  With the library's pass timing on,
+every K1 kernel of the timed steps is bracketed by a HIP event pair on the
+stream it runs on (ske_pass_times): the roofline is priced on the kernel that
+takes the most time, from those live durations.
+
+N>1: one process per GPU (torch.distributed.run), RCCL ("nccl") process
+group; every rank runs its own stream over its own key shard with the Bloom
+replicated (no data-path collective; weak scaling).  After timing, every rank
+checks a verification batch against the CPU oracle and the cross-shard
+queries (all_reduce MAX union, reduce_scatter MAX rollup) against the same
+collectives over the oracle's registers; the line carries the outcome under
+"check".
 
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
-import functools
+import ctypes as C
 import json
 import os
 import sys
@@ -34,40 +42,40 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# tools/randbench.hip on MI355X (profiles/r02_randbench.json): one random
+# 4-byte read per lane over a 1.6 GB table -- 55 G sectors/s; the register
+# update of pass C is priced against it as well as against the HBM peak
+RANDOM_SECTOR_GPS = 55.3
 METRIC = "swipes/sec (fused BF.EXISTS+PFADD) at 1/2/4/8 GPUs; % of HBM peak"
+PASS_NAMES = ["k1", "k_part_a", "k_part_b", "k_part_c"]
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="c2")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c3")
     ap.add_argument("--batch", type=int, default=0, help="swipes per step (default: config)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--tile", type=int, default=0, help="K1 swipes per thread in flight (1,2,4,8)")
     ap.add_argument("--variant", type=int, default=-1,
-                    help="-1 auto, 0 global Bloom, 1 LDS Bloom, 2 XCD-partitioned Bloom")
+                    help="-1 auto, 0 global Bloom, 1 LDS Bloom, 2 XCD-partitioned, 3 partitioned")
     ap.add_argument("--max-batches", type=int, default=64)
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: K1 parts removed (bits)")
-    ap.add_argument("--xr-u", type=int, default=0, help="XCD-partitioned K1: slice-pass tile")
-    ap.add_argument("--xr-fu", type=int, default=0, help="XCD-partitioned K1: finish-pass tile")
     ap.add_argument("--part-sub", type=int, default=0,
                     help="partitioned K1: swipes per sub-batch of its three passes (0 = default)")
-    ap.add_argument("--streams", type=int, default=16,
-                    help="HIP streams the steps alternate over, so launch tails overlap "
-                         "(with --graph 1: one graph of that many independent branches)")
-    ap.add_argument("--k1-legacy", action="store_true",
-                    help="diagnostic: the generic LDS K1 instead of the short-id kernel")
-    ap.add_argument("--k1-grid", type=int, default=-1,
-                    help="blocks of the short-id LDS K1 (0: one per CU; -1: one per CU with "
-                         "--streams 1, else one per two CUs, so two consecutive steps run side "
-                         "by side, each on half the CUs)")
-    ap.add_argument("--graph", type=int, default=1,
-                    help="1 = the K timed steps are recorded once into a HIP graph (one K1 "
-                         "launch per step, each over its own resident batch, step j on branch "
-                         "j mod --streams) and replayed; 0 = launched one by one from the host")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="HIP streams / graph branches the steps alternate over (0: 16 for the "
+                         "LDS K1, 1 otherwise)")
+    ap.add_argument("--k1-grid", type=int, default=-1, help="blocks of the short-id LDS K1")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="1 = record the K timed steps into a HIP graph and replay it (default for "
+                         "the LDS K1); 0 = launch them from the host (default otherwise)")
+    ap.add_argument("--pass-timing", type=int, default=1,
+                    help="1 = HIP events around every K1 kernel of the timed steps (host launches)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N>1 (nccl = RCCL over xGMI; gloo only to rehearse "
                          "several ranks on a one-GPU box)")
@@ -84,55 +92,186 @@ def cpu_threads():
     return max(1, min(n, 64))
 
 
-def cpu_baseline(engine, pkg, w, p, b0, seconds):
-    """Oracle (C restatement of Redis/RedisBloom) running the processor loop
-    attendance_processor.py:100-137 (BF.EXISTS then PFADD) on the same batch,
-    repeated for ~`seconds`: half the time on all host threads
-    (orc_process_swipes_mt, the reported value), half on 1 thread (SURVEY.md
-    §8d item 2)."""
-    import numpy as np
-    import __graft_entry__ as ge
-    orc = ge.load_oracle()
-    mbatch = engine.members_batch(p, 0, w.n_members)
-    mb, mo, _ = mbatch.to_host()
-    mbatch.free()
+def chain_geometry(engine, fid=0):
+    """(bits, k) of every link of the chain (BF.DEBUG)."""
+    from rtsas_amd._lib import BfInfo, BfLink
+    info = BfInfo()
+    engine.ctx.call("ske_bf_info", fid, C.byref(info))
+    out = []
+    for i in range(info.nfilters):
+        li = BfLink()
+        engine.ctx.call("ske_bf_link_info", fid, i, C.byref(li))
+        out.append((int(li.bits), int(li.hashes)))
+    return out
+
+
+def oracle_chain(engine, orc, w, p):
+    """The Bloom chain as the oracle builds it from the same preload (RedisBloom
+    SBChain_Add restated, oracle/sketch_oracle.c) -- test infrastructure."""
+    mb = engine.members_batch(p, 0, w.n_members)
+    buf, offs, _ = mb.to_host()
+    mb.free()
     chain = orc.Chain(w.bf_capacity, w.bf_error)
-    chain.madd_packed(mb, mo)
+    chain.madd_packed(buf, offs)
+    return chain
+
+
+def cpu_baseline(orc, chain, w, b0, seconds):
+    """The processor loop attendance_processor.py:100-137 (BF.EXISTS, then
+    PFADD when valid) on the host, over a bounded sample of the first batch:
+      - the C oracle on all host threads (orc_process_swipes_mt; the value),
+        and on one thread (SURVEY.md §8d item 2);
+      - the reference's per-event Python loop (json.loads, fromisoformat,
+        BF.EXISTS, PFADD per message) over the oracle, one core (§8d item 1)."""
+    import numpy as np
+    from datetime import datetime
+    from rtsas_amd import synthetic
     buf, offs, slot = b0.to_host()
-    slot = slot.astype(np.uint32)
+    n = min(len(offs) - 1, 1 << 20)
+    offs = np.ascontiguousarray(offs[:n + 1])
+    slot = np.ascontiguousarray(slot[:n].astype(np.uint32))
     regs = np.zeros((int(slot.max()) + 1, 16384), np.uint8)
-    n = len(offs) - 1
 
     def run(threads, budget):
-        passes = 0
-        t0 = time.perf_counter()
+        passes, t0 = 0, time.perf_counter()
         while True:
             orc.process_swipes(chain, regs, slot, buf, offs, threads=threads)
             passes += 1
             if time.perf_counter() - t0 >= budget:
-                break
-        return passes, time.perf_counter() - t0
+                return passes, time.perf_counter() - t0
 
     nt = cpu_threads()
-    p1, dt1 = run(1, seconds / 2)
-    pm, dtm = run(nt, seconds / 2)
+    pm, dtm = run(nt, seconds * 0.45)
+    p1, dt1 = run(1, seconds * 0.3)
+    # per-event loop over JSON payloads of the generator's schema
+    # (data_generator.py:112-118) carrying the same swipes
+    m = 100_000
+    msgs = []
+    for i in range(m):
+        sid = bytes(buf[offs[i]:offs[i + 1]]).decode()
+        _, _, lecture, day = synthetic.key_name(w, int(slot[i])).split(":")
+        msgs.append('{"student_id": %s, "timestamp": "%sT09:00:00", "lecture_id": "%s", '
+                    '"is_valid": true, "event_type": "entry"}' % (sid, day, lecture))
+    hlls = {}
+    t0 = time.perf_counter()
+    for msg in msgs:
+        data = json.loads(msg)
+        sid = str(data["student_id"]).encode()
+        ts = datetime.fromisoformat(data["timestamp"])
+        if chain.exists(sid):
+            hlls.setdefault(f"hll:unique:{data['lecture_id']}:{ts.date().isoformat()}",
+                            orc.HLL()).add(sid)
+    dte = time.perf_counter() - t0
     return {"value": n * pm / dtm, "unit": "swipes/s", "cores": nt, "kind": "port",
-            "sample": f"{pm} passes over the first {n}-swipe batch (C oracle, "
-                      f"orc_process_swipes_mt, {nt} threads, {dtm:.1f}s)",
+            "sample": f"{pm} passes over the first {n} swipes of batch 0 (C oracle of RedisBloom + "
+                      f"Redis HLL, orc_process_swipes_mt on {nt} threads, {dtm:.1f}s)",
             "single_thread": {"value": n * p1 / dt1, "cores": 1,
-                              "sample": f"{p1} passes, orc_process_swipes, {dt1:.1f}s"}}
+                              "sample": f"{p1} passes, orc_process_swipes, {dt1:.1f}s"},
+            "per_event_python": {"value": m / dte, "cores": 1,
+                                 "sample": f"{m} JSON messages: json.loads + fromisoformat + "
+                                           "oracle BF.EXISTS / PFADD per event "
+                                           "(attendance_processor.py:100-137 without transport)"}}
+
+
+def verify(engine, orc, chain, w, rank, world, dist, dev):
+    """A verification batch through K1 into 64 spare slots of this rank,
+    compared with the oracle (answers + registers), then the cross-shard
+    queries: union PFCOUNT of the 64 keys of every rank (all_reduce MAX) and
+    the 64 per-key unions across ranks (reduce_scatter MAX), each against the
+    same collective over the oracle's registers."""
+    import numpy as np
+    import torch
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import DeviceBuffer
+    nk, base = 64, w.n_keys
+    wv = synthetic.Workload(**{**w.__dict__, "n_keys": nk, "zipf_lectures": 0, "zipf_days": 0})
+    pv = engine.gen_params(wv, seed=w.seed + 7919 * (rank + 1), slot_base=base)
+    n = 1 << 19
+    b = engine.swipe_batch(pv, 0, n)
+    out = DeviceBuffer(engine.ctx, n)
+    engine.swipes(0, b, out)
+    buf, offs, slot = b.to_host()
+    regs = np.zeros((nk, 16384), np.uint8)
+    want, _, _ = orc.process_swipes(chain, regs, (slot - base).astype(np.uint32), buf, offs)
+    ok_local = bool(np.array_equal(out.to_host(np.uint8, n), want)) and \
+        bool(np.array_equal(engine.registers_all(base + nk)[base:], regs))
+    b.free()
+    out.free()
+    slots = np.arange(base, base + nk, dtype=np.uint32)
+    # union of the 64 keys of every rank: device merge -> all_reduce MAX -> K2
+    t = torch.zeros((1, 16384), dtype=torch.uint8, device=dev)
+    go = np.array([0, nk], np.uint32)
+    torch.cuda.synchronize()
+    engine.ctx.call("ske_hll_merge_groups_dev", slots.ctypes.data_as(C.c_void_p),
+                    go.ctypes.data_as(C.c_void_p), 1, C.c_void_p(t.data_ptr()))
+    o = torch.from_numpy(regs.max(axis=0, keepdims=True)).to(dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(o, op=dist.ReduceOp.MAX)
+    torch.cuda.synchronize()
+    union = np.zeros(1, np.uint64)
+    engine.ctx.call("ske_hll_count_raw_dev", C.c_void_p(t.data_ptr()), 1,
+                    union.ctypes.data_as(C.c_void_p))
+    ok_union = bool(torch.equal(t, o)) and int(union[0]) == orc.hll_count_regs(o.cpu().numpy()[0])
+    # per-key unions across ranks: reduce_scatter MAX, each rank owns 64/world keys
+    per = -(-nk // world)
+    tk = torch.zeros((per * world, 16384), dtype=torch.uint8, device=dev)
+    gk = np.arange(nk + 1, dtype=np.uint32)
+    engine.ctx.call("ske_hll_merge_groups_dev", slots.ctypes.data_as(C.c_void_p),
+                    gk.ctypes.data_as(C.c_void_p), nk, C.c_void_p(tk.data_ptr()))
+    tk_o = torch.zeros_like(tk)
+    tk_o[:nk] = torch.from_numpy(regs).to(dev)
+    mine = torch.empty((per, 16384), dtype=torch.uint8, device=dev)
+    mine_o = torch.empty_like(mine)
+    if world > 1:
+        dist.reduce_scatter_tensor(mine, tk, op=dist.ReduceOp.MAX)
+        dist.reduce_scatter_tensor(mine_o, tk_o, op=dist.ReduceOp.MAX)
+    else:
+        mine.copy_(tk)
+        mine_o.copy_(tk_o)
+    torch.cuda.synchronize()
+    ok_rollup = bool(torch.equal(mine, mine_o))
+    ok = torch.tensor([int(ok_local and ok_union and ok_rollup)], device=dev)
+    if world > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    return {"ok": bool(ok.item()), "swipes_per_rank": n, "keys_per_rank": nk,
+            "local_answers_and_registers": ok_local, "union_all_reduce_max": ok_union,
+            "rollup_reduce_scatter_max": ok_rollup, "union_pfcount": int(union[0]),
+            "backend": dist.get_backend() if world > 1 else "none"}
+
+
+def pass_bytes(n, nvalid, probes, width, fixed, geometry):
+    """Algorithmic bytes per launch of each K1 kernel: streams
+    at their size, every random access at one 64-B HBM sector."""
+    s_off = 0 if fixed else 4
+    ksum = sum(k for _, k in geometry)
+    nslices = sum(-(-bits // (1 << 19)) for bits, _ in geometry)
+    filter_bytes = sum(bits // 8 for bits, _ in geometry)
+    rec = 4 * ksum * n
+    ntiles = -(-n // 1024)
+    return {
+        # one kernel: ids + offsets + slot + answer streamed, one sector per
+        # RedisBloom probe, one sector read + one written per valid swipe
+        "k1": n * (width + s_off + 4 + 1) + 64 * probes + 128 * nvalid,
+        # ids + offsets in; probe records, run table, HLL word, fail byte out
+        "k_part_a": n * (width + s_off) + rec + 4 * (nslices + 1) * ntiles + 4 * n + n * len(geometry),
+        # probe records + their run boundaries in, the filter staged once
+        "k_part_b": rec + 8 * nslices * ntiles + filter_bytes,
+        # fail byte, HLL word, slot in, answer out; one sector per valid swipe's register
+        "k_part_c": n * (len(geometry) + 4 + 4 + 1) + 64 * nvalid,
+    }
 
 
 def main():
     args = parse()
-    import numpy as np
+    import numpy as np  # noqa: F401
     import torch
     import torch.distributed as dist
 
     import __graft_entry__ as ge
-    pkg = ge.load_package()
+    ge.load_package()
     from rtsas_amd import synthetic
-    from rtsas_amd.engine import SketchEngine
+    from rtsas_amd.engine import DeviceBuffer, SketchEngine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -140,10 +279,11 @@ def main():
     # ranks on a one-GPU box (--dist-backend gloo), never on a full node
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if args.dist_backend == "nccl":  # RCCL
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.dist_backend)
 
@@ -151,94 +291,71 @@ def main():
     w = synthetic.shard(w_all, world)
     n = args.batch or w.step_swipes
     engine = SketchEngine(local)
-    # a dedicated (non-null) stream shared by libsketch and the timing events
-    stream = torch.cuda.Stream()
+    stream = torch.cuda.Stream()  # a dedicated stream shared by libsketch and torch
     torch.cuda.set_stream(stream)
     engine.set_stream(stream.cuda_stream)
-    if args.tile:
-        engine.set_option("tile", args.tile)
+    for name, val in (("tile", args.tile), ("ablate", args.ablate), ("part_sub", args.part_sub)):
+        if val:
+            engine.set_option(name, val)
     if args.variant >= 0:
         engine.set_option("variant", args.variant)
-    if args.ablate:
-        engine.set_option("ablate", args.ablate)
-    if args.k1_grid < 0:
-        cus = torch.cuda.get_device_properties(local).multi_processor_count
-        args.k1_grid = cus // 2 if args.streams > 1 else 0
-    if args.k1_grid:
-        engine.set_option("k1_grid", args.k1_grid)
-    if args.k1_legacy:
-        engine.set_option("k1_legacy", 1)
-    if args.xr_u:
-        engine.set_option("xr_region_u", args.xr_u)
-    if args.xr_fu:
-        engine.set_option("xr_finish_u", args.xr_fu)
-    if args.part_sub:
-        engine.set_option("part_sub", args.part_sub)
 
-    # Bloom preload (replicated on every rank), HLL key shard of this rank
+    # Bloom preload (replicated on every rank), this rank's HLL key shard, and
+    # 64 spare slots for the verification batch
     engine.reserve(0, w.bf_error, w.bf_capacity)
     p = engine.gen_params(w)
     t0 = time.perf_counter()
     engine.preload(0, p, w.n_members)
     preload_s = time.perf_counter() - t0
-    engine.hll_reserve(w.n_keys)
+    engine.hll_reserve(w.n_keys + 64)
+    variant = engine.variant(0)
+    lds_k1 = variant == 1
+    streams_n = args.streams or (16 if lds_k1 else 1)
+    use_graph = args.graph if args.graph >= 0 else (1 if lds_k1 else 0)
+    if args.k1_grid < 0:
+        cus = torch.cuda.get_device_properties(local).multi_processor_count
+        args.k1_grid = cus // 2 if (lds_k1 and streams_n > 1) else 0
+    if args.k1_grid:
+        engine.set_option("k1_grid", args.k1_grid)
 
     nb = max(1, min(args.max_batches, args.steps + args.warmup))
     batches = [engine.swipe_batch(p, (rank * nb + j) * n, n) for j in range(nb)]
+    out = DeviceBuffer(engine.ctx, n)  # BF.EXISTS answers (the reference stores is_valid)
     probes, nvalid = engine.swipes_stats(0, batches[0])
-    width = len(str(w.id_hi - 1))
-
+    width = synthetic.id_width(w)
     fixed = args.layout == "fixed"
-    streams = [stream] + [torch.cuda.Stream() for _ in range(max(0, args.streams - 1))]
+    streams = [stream] + [torch.cuda.Stream() for _ in range(max(0, streams_n - 1))]
 
     def step(j):
         if len(streams) > 1:
             engine.set_stream(streams[j % len(streams)].cuda_stream)
         if fixed:
-            engine.swipes_fixed_async(0, batches[j % nb])
+            engine.swipes_fixed_async(0, batches[j % nb], out)
         else:
-            engine.swipes_async(0, batches[j % nb])
+            engine.swipes_async(0, batches[j % nb], out)
 
     for j in range(args.warmup):
         step(j)
+    engine.set_stream(stream.cuda_stream)
     torch.cuda.synchronize()
+    engine.check_errors()
     graph = None
-    if args.graph and len(streams) == 1:
-        # the timed steps, recorded (not run) into one uploaded graph
+    if use_graph and len(streams) == 1:
         graph = engine.capture(lambda: [step(args.warmup + j) for j in range(args.steps)])
-    elif args.graph and len(streams) > 1:
-        one = engine.swipes_fixed_async if fixed else engine.swipes_async
-        timed = [functools.partial(one, 0, batches[(args.warmup + j) % nb])
-                 for j in range(args.steps)]
-        # K1's average launch duration: HIP events cannot time event nodes
-        # inside a graph, so the same K launches are first replayed (untimed)
-        # as one chain on the kernel's stream, bracketed by an event pair
-        engine.set_stream(stream.cuda_stream)
-        cal = engine.capture(lambda: [fn() for fn in timed])
-        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        c0.record(stream)
-        cal.launch()
-        c1.record(stream)
-        torch.cuda.synchronize()
-        cal_ms = c0.elapsed_time(c1) / args.steps
-        cal.free()
-        # the timed graph: one native call, step j on branch j mod S
-        # (ske_swipes_many_async forks its side streams from the context stream)
+    elif use_graph:
         engine.swipes_many_async(0, [], branches=len(streams))  # side streams, before capture
         torch.cuda.synchronize()
         graph = engine.capture(lambda: engine.swipes_many_async(
             0, [batches[(args.warmup + j) % nb] for j in range(args.steps)],
-            branches=len(streams), fixed=fixed))
+            [out] * args.steps, branches=len(streams), fixed=fixed))
+    timing = bool(args.pass_timing) and graph is None
+    engine.set_option("pass_timing", 1 if timing else 0)
+    engine.pass_times(reset=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
-    # several streams: every launch is bracketed by its own event pair on the
-    # stream it runs on, so the kernel's average duration is measured even
-    # though consecutive launches overlap
-    per = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)] if len(streams) > 1 and graph is None else []
     t0 = time.perf_counter()
     e0.record(stream)
     if graph is not None:
@@ -247,11 +364,8 @@ def main():
         for s_ in streams[1:]:
             s_.wait_stream(stream)
         for j in range(args.steps):
-            if per:
-                per[j][0].record(streams[(args.warmup + j) % len(streams)])
             step(args.warmup + j)
-            if per:
-                per[j][1].record(streams[(args.warmup + j) % len(streams)])
+        engine.set_stream(stream.cuda_stream)
         for s_ in streams[1:]:
             stream.wait_stream(s_)
     e1.record(stream)
@@ -260,42 +374,53 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    torch.cuda.synchronize()
-    # average launch duration of K1: one stream -- HIP events around the K
-    # back-to-back launches (includes the inter-kernel gaps, so an upper
-    # bound); several streams -- the mean of the per-launch event pairs
+    engine.set_option("pass_timing", 0)
+    engine.check_errors()  # an out-of-range slot in any timed step raises here
     step_ms = e0.elapsed_time(e1) / args.steps
-    kern_ms = sum(a.elapsed_time(b) for a, b in per) / len(per) if per else step_ms
-    if graph is not None and len(streams) > 1:
-        kern_ms = cal_ms
+    pt = engine.pass_times(reset=True)
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms, step_ms], dtype=torch.float64,
-                         device="cuda" if args.dist_backend == "nccl" else "cpu")
+        t = torch.tensor([elapsed, step_ms] + [ms for ms, _ in pt], dtype=torch.float64,
+                         device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms, step_ms = float(t[0]), float(t[1]), float(t[2])
+        elapsed, step_ms = float(t[0]), float(t[1])
+        pt = [(float(t[2 + i]), c) for i, (_, c) in enumerate(pt)]
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * n * args.steps / elapsed
-    # algorithmic bytes per launch: S_io per swipe (id bytes +
-    # u32 offset + u32 slot + u8 answer), one 64-B sector per RedisBloom probe
-    # (sequential count, measured), one 64-B sector read + write per PFADD
-    s_io = width + (0 if fixed else 4) + 4 + 1
-    # HBM-side bytes per K1 dispatch from the committed rocprofv3 PMC passes of
-    # this same command (FETCH_SIZE + WRITE_SIZE, separate passes; see
-    # profiles/README.md), or null when no summary exists for this workload
+    alg = pass_bytes(n, nvalid, probes, width, fixed, chain_geometry(engine))
+    passes = {}
+    for i, (ms, cnt) in enumerate(pt):
+        if cnt:
+            mean = ms / cnt
+            name = PASS_NAMES[i]
+            passes[name] = {"ms": mean, "launches": cnt, "alg_bytes": alg[name],
+                            "GBps": alg[name] / (mean * 1e-3) / 1e9}
+    if passes:
+        dom = max(passes, key=lambda k: passes[k]["ms"])
+        kern_ms, dom_bytes = passes[dom]["ms"], passes[dom]["alg_bytes"]
+    else:  # graph replay: the launch time is the replay's events / steps
+        dom, kern_ms, dom_bytes = "k1", step_ms, alg["k1"]
+    achieved = dom_bytes / (kern_ms * 1e-3) / 1e9
+    # HBM-side bytes per launch of that kernel from the committed rocprofv3 PMC
+    # passes of this workload (FETCH_SIZE + WRITE_SIZE, separate passes), or null
     traffic, traffic_src = None, None
-    pmc_path = os.path.join(ROOT, "profiles", f"k1_pmc_{args.config}.json")
+    pmc_path = os.path.join(ROOT, "profiles", f"r02_pmc_{args.config}_{dom}.json")
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
-            pmc = json.load(f)
-        traffic = pmc.get("hbm_bytes_per_dispatch")
+            traffic = json.load(f).get("hbm_bytes_per_dispatch")
         traffic_src = os.path.relpath(pmc_path, ROOT)
-    alg_bytes = n * s_io + 64 * probes + 128 * nvalid
-    variant = engine.variant(0)
-    kernel_name = {0: "k_swipes", 1: "k_swipes" if args.k1_legacy else "k_swipes_lds",
-                   2: "k_xr_hash+k_xr_region+k_xr_finish",
-                   3: "k_part_a+k_part_b+k_part_c"}[variant]
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                "kernel": dom, "kernel_ms": kern_ms, "alg_bytes_per_launch": dom_bytes,
+                "device_ms_per_step": step_ms, "probes_per_swipe": probes / n,
+                "valid_frac": nvalid / n, "passes": passes}
+    if dom == "k_part_c":
+        sectors = nvalid / (kern_ms * 1e-3) / 1e9
+        roofline["random_sector_bound"] = {
+            "what": "one 64-B HBM sector per valid swipe's register, against the measured random "
+                    "4-B read rate over a 1.6 GB table (tools/randbench.hip)",
+            "achieved_Gsectors_per_s": sectors, "peak_Gsectors_per_s": RANDOM_SECTOR_GPS,
+            "frac": sectors / RANDOM_SECTOR_GPS}
     line = {
         "metric": METRIC,
         "value": value,
@@ -310,34 +435,34 @@ def main():
         "dtype": "u64",
         "data": "synthetic (device counter-based generator, seed %d)" % w.seed,
         "config": {"workload": w.name, "swipes_per_step": n, "students": w.n_members,
-                   "hll_keys_total": w_all.n_keys,
-                   "hll_keys_per_gpu": w.n_keys, "invalid_frac": w.invalid_frac,
+                   "hll_keys_total": w_all.n_keys, "hll_keys_per_gpu": w.n_keys,
+                   "invalid_frac": w.invalid_frac,
                    "bloom": {"error": w.bf_error, "capacity": w.bf_capacity},
                    "id_bytes": width, "parallelism": f"dp{world} (key-sharded, Bloom replicated)",
                    "k1_variant": {0: "global-bloom", 1: "lds-bloom", 2: "xcd-regions",
                                   3: "partitioned"}[variant],
-                   "tile": args.tile or 2, "layout": args.layout, "streams": args.streams,
-                   "k1_grid": args.k1_grid or "one block per CU",
-                   "launch": "hip-graph" if graph is not None else "host"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": traffic_src,
-                     "kernel": kernel_name, "kernel_ms": kern_ms,
-                     "device_ms_per_step": step_ms,
-                     "achieved_per_step": alg_bytes / (step_ms * 1e-3) / 1e9,
-                     "alg_bytes_per_swipe": alg_bytes / n,
-                     "probes_per_swipe": probes / n, "valid_frac": nvalid / n},
+                   "layout": args.layout, "streams": len(streams),
+                   "launch": "hip-graph" if graph is not None else "host",
+                   "answers": "written (1 B per swipe)"},
+        "roofline": roofline,
         "preload_s": preload_s,
         "host_enqueue_us_per_step": host_enqueue * 1e6 / args.steps,
     }
-    if rank == 0 and not args.no_cpu and args.cpu_seconds > 0:
-        line["cpu_baseline"] = cpu_baseline(engine, pkg, w, p, batches[0], args.cpu_seconds)
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu and args.cpu_seconds > 0
+    if not args.no_check or want_cpu:
+        orc = ge.load_oracle()
+        chain = oracle_chain(engine, orc, w, p)
+        if not args.no_check:
+            line["check"] = verify(engine, orc, chain, w, rank, world, dist, dev)
+        if want_cpu:
+            line["cpu_baseline"] = cpu_baseline(orc, chain, w, batches[0], args.cpu_seconds)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if graph is not None:
         graph.free()
     for b in batches:
         b.free()
+    out.free()
     if world > 1:
         dist.destroy_process_group()
 

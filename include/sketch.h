@@ -230,6 +230,15 @@ int ske_swipes_stats(ske_ctx *ctx, uint32_t fid, const uint8_t *bytes, const uin
 /* which K1 variant the current chain selects: 1 = LDS-staged Bloom, 0 = global */
 int ske_swipes_variant(ske_ctx *ctx, uint32_t fid);
 int ske_set_option(ske_ctx *ctx, const char *name, int64_t value);
+/* Kernel timing for the benchmark's roofline: with option "pass_timing" = 1
+ * every K1 kernel launched outside a capture is bracketed by a HIP event pair
+ * recorded on the stream it runs on.  ske_pass_times waits for them and
+ * returns, per pass kind, the summed milliseconds and the kernel count:
+ * [0] single-kernel K1 (LDS / global / XCD-partitioned variants), [1] [2] [3]
+ * the partitioned K1's passes A (hash + probe records), B (slice probes),
+ * C (answers + register max).  reset != 0 zeroes the sums after reading. */
+#define SKE_PASS_KINDS 4
+int ske_pass_times(ske_ctx *ctx, double *ms_out, uint64_t *count_out, int reset);
 
 /* ---- ingest: JSON event decode + key-slot resolution ----
  * The reference decodes each Pulsar payload on the CPU (attendance_processor.py

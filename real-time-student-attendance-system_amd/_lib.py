@@ -123,6 +123,7 @@ SIGNATURES = {
                                    C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "ske_swipes_variant": (C.c_int, [_CTX, C.c_uint32]),
     "ske_set_option": (C.c_int, [_CTX, C.c_char_p, C.c_int64]),
+    "ske_pass_times": (C.c_int, [_CTX, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.c_int]),
     "ske_ingest_parse": (C.c_int, [_CTX, _u8p, _u32p, C.c_uint64, C.c_int, C.POINTER(IngestCols)]),
     "ske_keytab_lookup": (C.c_int, [_CTX, C.POINTER(IngestCols), C.c_uint64, _u32p,
                                     C.POINTER(C.c_uint64)]),

@@ -28,6 +28,10 @@ hipError_t launch_bf_count_cands(uint64_t n, const uint8_t *state, unsigned long
 
 using namespace ske;
 
+// pass kinds of ske_pass_times: 0 a single-kernel K1 (LDS / global /
+// XCD-partitioned), 1-3 the partitioned K1's passes A, B, C
+constexpr int kPassKinds = SKE_PASS_KINDS;
+
 namespace {
 
 struct Link {
@@ -88,8 +92,18 @@ struct ske_ctx {
     unsigned long long xr_cap = 0;  // capture id xr_done was recorded in (0: none)
     // executable graphs alive (recorded, not yet freed): they hold pointers to
     // the scratch and the register slab, so neither may be reallocated
+    void *hook_arg = nullptr;  // launch_swipes_part's pass hook state
     int live_graphs = 0;
     bool capturing = false;
+    // pass timing (option "pass_timing"): HIP event pairs around every K1
+    // kernel, recorded on the stream the kernel runs on (never inside a
+    // capture); ske_pass_times() sums them per pass
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    struct Mark { int pass; hipEvent_t a, b; };
+    std::vector<Mark> marks;
+    double pass_ms[kPassKinds] = {};
+    uint64_t pass_n[kPassKinds] = {};
     // ske_swipes_many_async: side streams of the fork/join branches (lazy)
     hipStream_t many_st[SKE_MANY_MAX_BRANCHES - 1] = {};
     hipEvent_t many_join[SKE_MANY_MAX_BRANCHES - 1] = {};
@@ -167,6 +181,35 @@ int stage_u32(ske_ctx *c, const uint32_t *p, uint64_t n, int mem, int slot, cons
     HIPCHK(c, hipMemcpyAsync(d, p, n * 4, hipMemcpyHostToDevice, c->st));
     *out = d;
     return SKE_OK;
+}
+
+// ---- pass timing
+hipEvent_t ev_get(ske_ctx *c) {
+    if (!c->ev_pool.empty()) {
+        hipEvent_t e = c->ev_pool.back();
+        c->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// an event pair for one kernel of pass `pass` (nullptrs when not timing)
+struct PassMark {
+    hipEvent_t a = nullptr, b = nullptr;
+};
+PassMark mark_begin(ske_ctx *c, int pass) {
+    PassMark m;
+    if (!c->timing || c->capturing) return m;
+    m.a = ev_get(c);
+    m.b = ev_get(c);
+    if (!m.a || !m.b || hipEventRecord(m.a, c->st) != hipSuccess) return PassMark();
+    c->marks.push_back({pass, m.a, m.b});
+    return m;
+}
+void mark_end(ske_ctx *c, const PassMark &m) {
+    if (m.b) (void)hipEventRecord(m.b, c->st);
 }
 
 // deps/bloom/bloom.c calc_bpe() + bloom_init() with BLOOM_OPT_NOROUND |
@@ -405,7 +448,9 @@ int launch_k1(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32
     if (n == 0) return SKE_OK;
     K1Args A;
     if (k1_fast_args(c, ch, bytes, offs, fixed_w, slot, n, out, &A)) {
+        const PassMark m = mark_begin(c, 0);
         HIPCHK(c, launch_swipes_lds(A, true, c->pb, c->k1_grid ? c->k1_grid : c->cus, c->st));
+        mark_end(c, m);
         return SKE_OK;
     }
     const int var = c->ablate ? 0 : k1_variant(c, ch);
@@ -415,8 +460,18 @@ int launch_k1(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32
         unsigned long long cid = 0;
         int rc = scratch_user_begin(c, &cid);
         if (rc) return rc;
+        // one launch per pass and sub-batch, each bracketed when timing
+        PassMark pm[3];
+        auto hook = [](void *u, int pass, int end) {
+            ske_ctx *cc = static_cast<ske_ctx *>(u);
+            PassMark *marks = reinterpret_cast<PassMark *>(cc->hook_arg);
+            if (end) mark_end(cc, marks[pass]);
+            else marks[pass] = mark_begin(cc, 1 + pass);
+        };
+        c->hook_arg = pm;
         HIPCHK(c, launch_swipes_part(ch, bytes, offs, fixed_w, slot, n, c->regs, c->nslots, out,
-                                     c->scratch, c->err, c->cus, c->part_sub, c->st));
+                                     c->scratch, c->err, c->cus, c->part_sub, c->st,
+                                     c->timing && !c->capturing ? +hook : nullptr, c));
         return scratch_user_end(c, cid);
     }
     if (var == 2) {
@@ -426,8 +481,10 @@ int launch_k1(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32
         unsigned long long cid = 0;
         int rc = scratch_user_begin(c, &cid);
         if (rc) return rc;
+        const PassMark m = mark_begin(c, 0);
         HIPCHK(c, launch_swipes_xr(ch, bytes, offs, fixed_w, slot, n, c->regs, c->nslots, out,
                                    scr, c->err, c->cus, c->xr_region_u, c->xr_finish_u, c->st));
+        mark_end(c, m);
         return scratch_user_end(c, cid);
     }
     if (c->ablate) {
@@ -438,8 +495,10 @@ int launch_k1(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32
                                 c->st));
         return SKE_OK;
     }
+    const PassMark m = mark_begin(c, 0);
     HIPCHK(c, launch_swipes(0, ch, use_lds(c, ch), c->pb, bytes, offs, fixed_w, slot, n, c->regs,
                             c->nslots, out, (unsigned long long *)c->err, c->cus, c->st));
+    mark_end(c, m);
     return SKE_OK;
 }
 
@@ -517,6 +576,11 @@ int ske_close(ske_ctx *c) {
     if (c->err) (void)hipFree(c->err);
     if (c->zero16) (void)hipFree(c->zero16);
     if (c->xr_done) (void)hipEventDestroy(c->xr_done);
+    for (auto &m : c->marks) {
+        (void)hipEventDestroy(m.a);
+        (void)hipEventDestroy(m.b);
+    }
+    for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     for (int i = 0; i < c->many_n; i++) {
         (void)hipStreamDestroy(c->many_st[i]);
         (void)hipEventDestroy(c->many_join[i]);
@@ -546,6 +610,31 @@ int ske_sync(ske_ctx *c) {
 int ske_check_errors(ske_ctx *c) {
     if (!c) return SKE_EINVAL;
     return check_err_flag(c, SKE_ERANGE);
+}
+
+int ske_pass_times(ske_ctx *c, double *ms, uint64_t *count, int reset) {
+    if (!c || !ms || !count) return SKE_EINVAL;
+    if (!c->marks.empty()) {
+        for (auto &m : c->marks) HIPCHK(c, hipEventSynchronize(m.b));
+        for (auto &m : c->marks) {
+            float t = 0;
+            HIPCHK(c, hipEventElapsedTime(&t, m.a, m.b));
+            c->pass_ms[m.pass] += t;
+            c->pass_n[m.pass]++;
+            c->ev_pool.push_back(m.a);
+            c->ev_pool.push_back(m.b);
+        }
+        c->marks.clear();
+    }
+    for (int i = 0; i < kPassKinds; i++) {
+        ms[i] = c->pass_ms[i];
+        count[i] = c->pass_n[i];
+        if (reset) {
+            c->pass_ms[i] = 0;
+            c->pass_n[i] = 0;
+        }
+    }
+    return SKE_OK;
 }
 
 int ske_device_alloc(ske_ctx *c, uint64_t bytes, void **out) {
@@ -587,6 +676,11 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
         const int64_t a = (name[3] == 'r' && value < 0) ? -value : value;
         if (a != 1 && a != 2 && a != 4 && a != 8) return SKE_EINVAL;
         (name[3] == 'r' ? c->xr_region_u : c->xr_finish_u) = int(value);
+        return SKE_OK;
+    }
+    if (!strcmp(name, "pass_timing")) {  // 1: bracket every K1 kernel with HIP events
+        if (value < 0 || value > 1) return SKE_EINVAL;
+        c->timing = value != 0;
         return SKE_OK;
     }
     if (!strcmp(name, "part_sub")) {  // partitioned K1 sub-batch (swipes; 0 = default)

@@ -43,7 +43,8 @@ constexpr uint32_t kPcBlock = 256;
 constexpr uint32_t kPSliceMask = kPSliceBits - 1;
 constexpr uint32_t kPSliceBytes = kPSliceBits / 8;  // 64 KiB
 constexpr uint32_t kPSub = 1u << 24;                // swipes per sub-batch (passes A-B-C)
-constexpr uint32_t kPbGroup = 8;                    // tiles a pass-B wave has in flight
+constexpr uint32_t kPbGroup = 8;                    // tiles a pass-B wave reads at once
+constexpr uint32_t kPbLanes = 64 / kPbGroup;        // lanes per tile run
 
 struct PartLink {
     const uint8_t *bf;
@@ -73,6 +74,18 @@ struct PartArgs {
 
 __device__ __forceinline__ Divisor part_div(const PartLink &L) { return Divisor{L.d, L.m, L.t, L.sh, 0}; }
 
+// Tiles are dealt to kPGroups contiguous groups, and every pass gives the
+// blocks b with b % kPGroups == x the tiles of group x.  Blocks are dealt
+// round-robin over the 8 XCDs, so a group's fail bytes (2 MB at C3) are
+// written by pass A, set by pass B and read by pass C in one XCD's L2.  This
+// is placement for speed only: every tile of a group is handled by exactly one
+// block of the group, whichever XCD it runs on.
+constexpr uint32_t kPGroups = 8;
+__device__ __forceinline__ void part_group(uint32_t ntiles, uint32_t x, uint32_t &t0, uint32_t &t1) {
+    t0 = uint32_t(uint64_t(ntiles) * x / kPGroups);
+    t1 = uint32_t(uint64_t(ntiles) * (x + 1) / kPGroups);
+}
+
 // ---------------------------------------------------------------------------
 // pass A: hash, probe records, counting sort by slice
 // ---------------------------------------------------------------------------
@@ -83,21 +96,41 @@ __device__ __forceinline__ Divisor part_div(const PartLink &L) { return Divisor{
 template <int KM>
 __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const PartArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t srec[kPaBlock * KM];
-    __shared__ uint32_t scnt[kPMaxSlices + 1];  // slice histogram, then run starts
+    // slice histogram, then run starts; two buffers used by alternate tiles,
+    // so the one the next tile counts into is cleared while this tile still
+    // reads its own (four barriers per tile)
+    __shared__ uint32_t scnt2[2][kPMaxSlices + 1];
     __shared__ uint32_t swsum[kPaBlock / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t S = A.nslices;
-    for (uint32_t g = tid; g <= kPMaxSlices; g += kPaBlock) scnt[g] = 0;
+    for (uint32_t g = tid; g <= kPMaxSlices; g += kPaBlock) scnt2[0][g] = scnt2[1][g] = 0;
     __syncthreads();
-    for (uint32_t t = blockIdx.x; t < A.ntiles; t += gridDim.x) {
+    // the next tile's ids are loaded while this tile sorts: its offsets at the
+    // top of the iteration, its id words after the scan
+    auto offsets = [&](uint32_t t, uint32_t &b, uint32_t &e) {
+        const uint32_t i = t * kPaBlock + tid;
+        const uint32_t ic = i < A.n ? i : A.n - 1;
+        b = A.offs ? A.offs[ic] : ic * A.fixed_w;
+        e = A.offs ? A.offs[ic + 1] : b + A.fixed_w;
+    };
+    uint32_t gt0, gt1;
+    part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
+    const uint32_t tstep = gridDim.x / kPGroups;
+    uint32_t par = 0, nb_ = 0, ne_ = 0;
+    Item it;
+    {
+        const uint32_t t = gt0 + blockIdx.x / kPGroups;
+        offsets(t < gt1 ? t : gt0, nb_, ne_);
+        it = load_item(A.bytes, nb_, ne_);
+    }
+    for (uint32_t t = gt0 + blockIdx.x / kPGroups; t < gt1; t += tstep, par ^= 1) {
+        uint32_t *scnt = scnt2[par];
         uint32_t rv[KM], rp[KM];
+        const uint32_t tn = t + tstep < gt1 ? t + tstep : t;
+        offsets(tn, nb_, ne_);
         {
             const uint32_t i = t * kPaBlock + tid;
             const bool act = i < A.n;
-            const uint32_t ic = act ? i : A.n - 1;
-            const uint32_t b = A.offs ? A.offs[ic] : ic * A.fixed_w;
-            const uint32_t e = A.offs ? A.offs[ic + 1] : b + A.fixed_w;
-            const Item it = load_item(A.bytes, b, e);
             const bool sh = it.len <= 8;
             const uint64_t ha = sh ? murmur_short(it.w0, it.len, kBloomSeed) : murmur_item(it, kBloomSeed);
             const uint64_t hb = sh ? murmur_short(it.w0, it.len, ha) : murmur_item(it, ha);
@@ -126,7 +159,7 @@ __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const Par
                     }
                     const uint32_t x = wk.x;
                     const uint32_t g = A.link[l].slice0 + (x >> kPSliceLog);
-                    rv[q] = (x & kPSliceMask) | (tid << kPSliceLog);
+                    rv[q] = (x & kPSliceMask) | (tid << kPSliceLog) | 0x80000000u;
                     if (act) rp[q] = (g << 16) | atomicAdd(&scnt[g], 1u);
                     wk.step(A.link[l].d);
                     jl++;
@@ -134,6 +167,7 @@ __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const Par
             }
         }
         __syncthreads();
+        it = load_item(A.bytes, nb_, ne_);  // the next tile's ids
         // exclusive scan of scnt[0..S] (scnt[S] == 0 becomes the tile's total)
         constexpr int kPer = (kPMaxSlices + 1) / kPaBlock;
         uint32_t v[kPer], s = 0;
@@ -164,72 +198,155 @@ __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const Par
 #pragma unroll
         for (int q = 0; q < KM; q++)
             if (rp[q] != 0xffffffffu) srec[scnt[rp[q] >> 16] + (rp[q] & 0xffffu)] = rv[q];
+        // the next tile's histogram (its previous readers passed two barriers ago)
+        for (uint32_t g = tid; g <= S; g += kPaBlock) scnt2[par ^ 1][g] = 0;
         __syncthreads();
+        // copy-out; the next tile places records only after three more barriers
         const uint32_t total = scnt[S];
         uint4 *dst = reinterpret_cast<uint4 *>(A.rec + size_t(t) * A.stride);
         const uint4 *src = reinterpret_cast<const uint4 *>(srec);
         for (uint32_t j = tid; j * 4 < total; j += kPaBlock) dst[j] = src[j];
-        for (uint32_t g = tid; g <= S; g += kPaBlock) scnt[g] = 0;  // for the next tile
-        __syncthreads();  // srec / scnt are reused by the next tile
     }
 }
 
 // ---------------------------------------------------------------------------
-// pass B: one LDS-resident slice per block, probe its runs
+// pass B: LDS-resident slices, probe their runs
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kPbBlock, 8) k_part_b(const PartArgs A, uint32_t splits) {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t part_rsrc(const void *p, uint32_t nbytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, int(nbytes), 0x00020000);
+}
+constexpr uint32_t kOOR = 0x80000000u;  // a buffer offset past every range: load 0, store dropped
+
+// The (slice, tile) space is cut into gridDim.x equal contiguous ranges, slice
+// major: a block probes one or two slices (restaging the LDS image once) over
+// a range of tiles, so the resident grid is balanced to the tile and no block
+// waits for a tail.
+//
+// Memory instructions are what this pass is made of (PMC: the address unit
+// busy 84 % of the time, stalled behind L1 misses, when lanes read 4-byte
+// pieces), so each one is made to move whole lines: within a slice a wave
+// takes kPbGroup consecutive tiles at a time, 8 lanes per tile run, and a
+// lane loads 16 bytes (4 records) -- one instruction reads 128 aligned-to-16
+// contiguous bytes of each of 8 runs.  Two such rounds cover a run of up to 64
+// records (about 37 at C3); longer runs finish in a tail loop.  The few failing
+// probes (a member never fails; a non-member's probes fail about half the
+// time) are compacted through LDS so a group ends in one fail-byte store
+// instruction.  Loads and stores are buffer operations whose out-of-range
+// lanes read 0 / are dropped, so every wave issues a fixed number per group
+// and the pipeline keeps exact waits: the run boundaries of the group after
+// next and the records of the next group are in flight while a group is
+// tested.
+constexpr uint32_t kPbQueue = 64;  // compacted fail stores per wave and group
+
+__global__ void __launch_bounds__(kPbBlock, 8) k_part_b(const PartArgs A) {
     __shared__ __attribute__((aligned(16))) uint8_t img[kPSliceBytes];
-    const uint32_t g = blockIdx.x / splits, q = blockIdx.x % splits;
-    uint32_t l = 0;
-    while (l + 1 < A.nlinks && g >= A.link[l + 1].slice0) l++;
-    const PartLink &L = A.link[l];
-    const uint32_t b0 = (g - L.slice0) * kPSliceBytes;
-    const uint32_t nb = L.nbytes16 - b0 < kPSliceBytes ? L.nbytes16 - b0 : kPSliceBytes;
-    for (uint32_t o = threadIdx.x * 16; o < nb; o += kPbBlock * 16)
-        *reinterpret_cast<uint4 *>(img + o) = *reinterpret_cast<const uint4 *>(L.bf + b0 + o);
-    __syncthreads();
-    const uint32_t t0 = uint32_t(uint64_t(A.ntiles) * q / splits);
-    const uint32_t t1 = uint32_t(uint64_t(A.ntiles) * (q + 1) / splits);
+    __shared__ uint32_t fq[kPbBlock / 64][kPbQueue];
+    // this block's share of its group's (slice, tile) space, slice major
+    uint32_t gt0, gt1;
+    part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
+    const uint32_t gn = gt1 - gt0, nblk = gridDim.x / kPGroups, bi = blockIdx.x / kPGroups;
+    const uint32_t total = A.nslices * gn;
+    uint32_t w = uint32_t(uint64_t(total) * bi / nblk);
+    const uint32_t wend = uint32_t(uint64_t(total) * (bi + 1) / nblk);
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    constexpr uint32_t kWaves = kPbBlock / 64;
-    uint8_t *fail = A.fail + size_t(l) * A.fail_stride;
-    const uint32_t *obeg = A.off + size_t(g) * A.off_stride;
-    const uint32_t *oend = obeg + A.off_stride;
-    // a wave takes kPbGroup consecutive tiles at a time (wave-uniform): their
-    // run boundaries are two rows of the slice-major table, and two 64-record
-    // rounds of every run are in flight together; longer runs finish in a
-    // tail loop
-    for (uint32_t tg = t0 + wave * kPbGroup; tg < t1; tg += kWaves * kPbGroup) {
-        uint32_t beg[kPbGroup], end[kPbGroup], r[2][kPbGroup];
+    const uint32_t k = lane / kPbLanes, qq = lane % kPbLanes;
+    constexpr uint32_t kWaves = kPbBlock / 64, kStep = kWaves * kPbGroup;
+    const __amdgpu_buffer_rsrc_t rrec = part_rsrc(A.rec, A.ntiles * A.stride * 4);
+    const __amdgpu_buffer_rsrc_t roff = part_rsrc(A.off, (A.nslices + 1) * A.off_stride * 4);
+    uint32_t *q = fq[wave];
+    while (w < wend) {
+        const uint32_t g = w / gn, ta = gt0 + w % gn;
+        const uint32_t tb = gt1 - ta < wend - w ? gt1 : ta + (wend - w);
+        w += tb - ta;
+        uint32_t l = 0;
+        while (l + 1 < A.nlinks && g >= A.link[l + 1].slice0) l++;
+        const PartLink &L = A.link[l];
+        const uint32_t b0 = (g - L.slice0) * kPSliceBytes;
+        const uint32_t nb = L.nbytes16 - b0 < kPSliceBytes ? L.nbytes16 - b0 : kPSliceBytes;
+        __syncthreads();  // every wave is done with the previous slice
+        for (uint32_t o = threadIdx.x * 16; o < nb; o += kPbBlock * 16)
+            *reinterpret_cast<uint4 *>(img + o) = *reinterpret_cast<const uint4 *>(L.bf + b0 + o);
+        __syncthreads();
+        const __amdgpu_buffer_rsrc_t rfail = part_rsrc(A.fail + size_t(l) * A.fail_stride, A.fail_stride);
+        const uint32_t orow = g * A.off_stride;
+        // run boundaries of tile tg + k (0, 0 past tb)
+        auto load_be = [&](uint32_t tg, uint32_t &b, uint32_t &e) {
+            const uint32_t t = tg + k;
+            const bool in = t < tb;
+            b = __builtin_amdgcn_raw_buffer_load_b32(roff, in ? (orow + t) * 4 : kOOR, 0, 0);
+            e = __builtin_amdgcn_raw_buffer_load_b32(roff, in ? (orow + A.off_stride + t) * 4 : kOOR, 0, 0);
+        };
+        // 16-byte pieces qq and qq + 8 of the run from its 16-byte-aligned start
+        auto load_recs = [&](uint32_t tg, uint32_t b, uint32_t e, uint4 (&r)[2]) {
+            const uint32_t base = (tg + k) * A.stride, s0 = b & ~3u;
 #pragma unroll
-        for (uint32_t k = 0; k < kPbGroup; k++) {
-            const bool in = tg + k < t1;
-            beg[k] = in ? obeg[tg + k] : 0;
-            end[k] = in ? oend[tg + k] : 0;
-        }
-#pragma unroll
-        for (uint32_t c = 0; c < 2; c++)
-#pragma unroll
-            for (uint32_t k = 0; k < kPbGroup; k++) {
-                const uint32_t i = beg[k] + c * 64 + lane;
-                r[c][k] = i < end[k] ? __builtin_nontemporal_load(&A.rec[size_t(tg + k) * A.stride + i])
-                                     : 0xffffffffu;
+            for (uint32_t c = 0; c < 2; c++) {
+                const uint32_t i = s0 + c * 32 + qq * 4;
+                r[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     rrec, i < e ? (base + i) * 4 : kOOR, 0, 0));
             }
+        };
+        uint32_t tg = ta + wave * kPbGroup;
+        uint32_t bc, ec, b1, e1;
+        uint4 r[2];
+        load_be(tg, bc, ec);
+        load_be(tg + kStep, b1, e1);
+        load_recs(tg, bc, ec, r);
+        for (; tg < tb; tg += kStep) {
+            uint32_t b2, e2;
+            uint4 rn[2];
+            load_be(tg + 2 * kStep, b2, e2);
+            load_recs(tg + kStep, b1, e1, rn);
+            // test the (up to) 8 records of this lane: bit j of fm = record j fails
+            const uint32_t s0 = bc & ~3u;
+            const uint32_t rec8[8] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w};
+            uint32_t fm = 0;
 #pragma unroll
-        for (uint32_t c = 0; c < 2; c++)
-#pragma unroll
-            for (uint32_t k = 0; k < kPbGroup; k++) {
-                const uint32_t rr = r[c][k];
-                if (rr == 0xffffffffu) continue;
+            for (uint32_t j = 0; j < 8; j++) {
+                const uint32_t i = s0 + (j >> 2) * 32 + qq * 4 + (j & 3);
+                const uint32_t rr = rec8[j];
                 const uint32_t o = rr & kPSliceMask;
-                if (!((img[o >> 3] >> (o & 7)) & 1)) fail[(tg + k) * kPaBlock + (rr >> kPSliceLog)] = 1;
+                const bool fails = i >= bc && i < ec && !((img[o >> 3] >> (o & 7)) & 1);
+                fm |= uint32_t(fails) << j;
             }
-        for (uint32_t k = 0; k < kPbGroup; k++) {
-            for (uint32_t i = beg[k] + 128 + lane; i < end[k]; i += 64) {
-                const uint32_t rr = A.rec[size_t(tg + k) * A.stride + i];
-                const uint32_t o = rr & kPSliceMask;
-                if (!((img[o >> 3] >> (o & 7)) & 1)) fail[(tg + k) * kPaBlock + (rr >> kPSliceLog)] = 1;
+            // compact the failing swipes of the wave, one store per 64 of them
+            const uint32_t tbase = (tg + k) * kPaBlock;
+            uint32_t nq = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 8; j++) {
+                const bool fj = (fm >> j) & 1;
+                const uint64_t m = __ballot(fj);
+                const uint32_t pos = nq + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+                const uint32_t at = tbase + ((rec8[j] >> kPSliceLog) & (kPaBlock - 1));
+                if (fj) {
+                    if (pos < kPbQueue) q[pos] = at;
+                    else __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail, at, 0, 0);  // overflow
+                }
+                nq += uint32_t(__builtin_popcountll(m));
             }
+            __builtin_amdgcn_wave_barrier();
+            if (nq) {
+                const uint32_t at = q[lane];
+                __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail, lane < nq ? at : kOOR, 0, 0);
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (ec - s0 > 64) {  // rare: a long run
+                const uint32_t base = (tg + k) * A.stride;
+                for (uint32_t i = s0 + 64 + qq; i < ec; i += kPbLanes) {
+                    const uint32_t rr = __builtin_amdgcn_raw_buffer_load_b32(rrec, (base + i) * 4, 0, 0);
+                    const uint32_t o = rr & kPSliceMask;
+                    if (!((img[o >> 3] >> (o & 7)) & 1))
+                        __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail,
+                                                             tbase + ((rr >> kPSliceLog) & (kPaBlock - 1)), 0, 0);
+                }
+            }
+            r[0] = rn[0];
+            r[1] = rn[1];
+            bc = b1;
+            ec = e1;
+            b1 = b2;
+            e1 = e2;
         }
     }
 }
@@ -248,8 +365,12 @@ __device__ __forceinline__ void part_reg_max(uint32_t *w, uint32_t sh, uint32_t 
 template <int U>
 __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
     const uint32_t T = kPcBlock, tid = threadIdx.x;
-    const uint64_t stride = uint64_t(gridDim.x) * T * U;
-    for (uint64_t base = uint64_t(blockIdx.x) * T * U; base < A.n; base += stride) {
+    uint32_t gt0, gt1;
+    part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
+    const uint64_t end = uint64_t(gt1) * kPaBlock < A.n ? uint64_t(gt1) * kPaBlock : A.n;
+    const uint64_t stride = uint64_t(gridDim.x / kPGroups) * T * U;
+    for (uint64_t base = uint64_t(gt0) * kPaBlock + uint64_t(blockIdx.x / kPGroups) * T * U; base < end;
+         base += stride) {
         bool valid[U];
         uint32_t *w[U];
         uint32_t rank[U], sh[U], cur[U];
@@ -260,7 +381,7 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
             w[u] = nullptr;
             rank[u] = 0;
             sh[u] = 0;
-            if (i < A.n) {
+            if (i < end) {
                 for (uint32_t l = 0; l < A.nlinks; l++) valid[u] |= A.fail[size_t(l) * A.fail_stride + i] == 0;
                 if (valid[u]) {
                     const uint32_t s = A.slot[i];
@@ -285,7 +406,7 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const uint64_t i = base + uint64_t(u) * T + tid;
-                if (i < A.n) A.out[i] = valid[u];
+                if (i < end) A.out[i] = valid[u];
             }
         }
     }
@@ -371,7 +492,7 @@ hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratc
 hipError_t launch_swipes_part(const ChainDev &ch, const uint8_t *bytes, const uint32_t *offs,
                               uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *regs,
                               uint32_t nslots, uint8_t *out, Scratch *scr, unsigned int *err, int cus,
-                              uint32_t sub_opt, hipStream_t st) {
+                              uint32_t sub_opt, hipStream_t st, PassHook hook, void *hook_user) {
     if (n == 0) return hipSuccess;
     PartArgs A{};
     if (!part_plan(ch, &A)) return hipErrorInvalidValue;
@@ -392,18 +513,22 @@ hipError_t launch_swipes_part(const ChainDev &ch, const uint8_t *bytes, const ui
         A.slot = slot + s0;
         A.out = out ? out + s0 : nullptr;
         const unsigned per_cu = km <= 11 ? 2 : 1;
-        const unsigned ga = A.ntiles < unsigned(cus) * per_cu ? A.ntiles : unsigned(cus) * per_cu;
+        const unsigned ga = unsigned(cus) * per_cu / kPGroups * kPGroups;  // blocks past a group's tiles exit
+        if (hook) hook(hook_user, 0, 0);
         if (km <= 11)
             hipLaunchKernelGGL(k_part_a<11>, dim3(ga), dim3(kPaBlock), 0, st, A);
         else
             hipLaunchKernelGGL(k_part_a<22>, dim3(ga), dim3(kPaBlock), 0, st, A);
-        // about three rounds of 2 blocks per CU, at least one block per slice
-        uint32_t splits = (uint32_t(cus) * 6 + A.nslices - 1) / A.nslices;
-        const uint32_t maxsplit = (A.ntiles + kPbGroup - 1) / kPbGroup;
-        splits = splits < 1 ? 1 : (splits > maxsplit ? maxsplit : splits);
-        hipLaunchKernelGGL(k_part_b, dim3(A.nslices * splits), dim3(kPbBlock), 0, st, A, splits);
-        hipLaunchKernelGGL(k_part_c<2>, dim3(part_grid(ms, kPcBlock * 2, cus * 8)), dim3(kPcBlock), 0,
-                           st, A);
+        if (hook) hook(hook_user, 0, 1);
+        // two blocks per CU, all resident, each an equal share of (slice, tile)
+        const unsigned gb = unsigned(cus) * 2 / kPGroups * kPGroups;
+        if (hook) hook(hook_user, 1, 0);
+        hipLaunchKernelGGL(k_part_b, dim3(gb), dim3(kPbBlock), 0, st, A);
+        if (hook) hook(hook_user, 1, 1);
+        if (hook) hook(hook_user, 2, 0);
+        const unsigned gc = (part_grid(ms, kPcBlock * 2, cus * 8) + kPGroups - 1) / kPGroups * kPGroups;
+        hipLaunchKernelGGL(k_part_c<2>, dim3(gc), dim3(kPcBlock), 0, st, A);
+        if (hook) hook(hook_user, 2, 1);
     }
     return hipGetLastError();
 }

@@ -203,6 +203,15 @@ class SketchEngine:
     def set_option(self, name: str, value: int):
         self.ctx.call("ske_set_option", name.encode(), int(value))
 
+    def pass_times(self, reset: bool = True) -> list[tuple[float, int]]:
+        """(summed ms, kernel count) per K1 pass kind, from the HIP event
+        pairs the library records around each kernel while the option
+        "pass_timing" is on: [single-kernel K1, partitioned A, B, C]."""
+        ms = (C.c_double * 4)()
+        cnt = (C.c_uint64 * 4)()
+        self.ctx.call("ske_pass_times", ms, cnt, 1 if reset else 0)
+        return [(ms[i], cnt[i]) for i in range(4)]
+
     def set_stream(self, stream_ptr: int | None):
         self.ctx.call("ske_set_stream", C.c_void_p(stream_ptr) if stream_ptr else None)
 

@@ -133,7 +133,7 @@ def test_graph_replay_then_direct_launch_other_stream(engine, orc):
     import torch
     from rtsas_amd.engine import DeviceBuffer
     w, p = _c3_small(engine)
-    bs = [engine.swipe_batch(p, j * 500_000, 500_000) for j in range(3)]
+    bs = [engine.swipe_batch(p, j * 1_200_000, 1_200_000) for j in range(3)]  # > 512 tiles each
     outs = [DeviceBuffer(engine.ctx, b.n) for b in bs]
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     engine.set_stream(s1.cuda_stream)
