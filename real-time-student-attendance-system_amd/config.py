@@ -27,5 +27,10 @@ class AttendanceConfig:
     # reproduce _setup_bloom_filter's behaviour (attendance_processor.py:74-92):
     # BF.EXISTS on a missing key answers 0, so BF.RESERVE is never reached.
     faithful_setup: bool = True
+    # the Cassandra INSERT (attendance_processor.py:116-124) runs before PFADD;
+    # its `student_id int` / `lecture_id text` columns refuse other types, so
+    # such a message is nacked and never counted.  False: count any id that
+    # redis-py can encode (the bare redis-py semantics of SketchClient.ingest)
+    cassandra_row_types: bool = True
     device: int = 0
     batch_size: int = 1 << 16

@@ -21,6 +21,7 @@ import numpy as np
 
 from .client import SketchClient
 from .config import AttendanceConfig
+from .encoding import encode
 from .exceptions import ResponseError
 
 logger = logging.getLogger(__name__)
@@ -33,6 +34,9 @@ class AttendanceProcessor:
         self.redis_client = client or SketchClient(decode_responses=True, device=self.config.device)
         self.acked = 0
         self.nacked = 0
+        # lecture_id -> the day keys its valid events were counted into
+        # (README key form), for get_attendance_stats(lecture_id)
+        self._lecture_keys: dict = {}
 
     # attendance_processor.py:74-92
     def _setup_bloom_filter(self):
@@ -66,9 +70,20 @@ class AttendanceProcessor:
     def process_batch(self, messages: Sequence) -> list[dict]:
         """One batch of the loop at attendance_processor.py:100-137.
 
-        Returns one row per decodable message: student_id, lecture_id,
-        timestamp, is_valid (what :121-124 inserts).  Undecodable messages are
-        negatively acknowledged (:134-136) and produce no row."""
+        Returns one row per acknowledged message: student_id, lecture_id,
+        timestamp, is_valid (what :121-124 inserts).  A message is negatively
+        acknowledged (:134-136), produces no row and no PFADD when any step of
+        the reference's loop would raise for it, in the loop's order:
+          - json.loads / a missing field / datetime.fromisoformat (:103-106);
+          - BF.EXISTS: redis-py refuses to encode the id (bool, None, list,
+            dict: DataError, :109-113);
+          - the Cassandra INSERT (:116-124, before PFADD): the table's
+            ``student_id int`` / ``lecture_id text`` columns refuse an id that
+            is not an int in the 32-bit range or a lecture_id that is not a
+            string (``config.cassandra_row_types``; off: any id redis-py can
+            encode is counted).
+        The surviving messages go through one fused device call."""
+        cfg = self.config
         ids, keys, rows = [], [], []
         for m in messages:
             try:
@@ -77,17 +92,28 @@ class AttendanceProcessor:
                 student_id = data["student_id"]
                 lecture_id = data["lecture_id"]
                 ts = datetime.fromisoformat(data["timestamp"])
+                sid = encode(student_id)  # redis-py's Encoder: DataError as BF.EXISTS raises it
+                if cfg.cassandra_row_types:
+                    if type(student_id) is not int or not -2**31 <= student_id < 2**31:
+                        raise TypeError(f"Received an argument of invalid type for column "
+                                        f"\"student_id\": {student_id!r}")
+                    if not isinstance(lecture_id, str):
+                        raise TypeError(f"Received an argument of invalid type for column "
+                                        f"\"lecture_id\": {lecture_id!r}")
+                key = self.hll_key(lecture_id, ts)
             except Exception as e:  # :134-136
                 logger.error(f"Error processing message: {e}")
                 self.nacked += 1
                 continue
-            ids.append(student_id)
-            keys.append(self.hll_key(lecture_id, ts))
+            ids.append(sid)
+            keys.append(key)
             rows.append({"student_id": student_id, "lecture_id": lecture_id, "timestamp": ts})
         if rows:
-            valid = self.redis_client.swipes(self.config.bloom_filter_key, keys, ids)
-            for r, v in zip(rows, valid):
+            valid = self.redis_client.swipes(cfg.bloom_filter_key, keys, ids)
+            for r, k, v in zip(rows, keys, valid):
                 r["is_valid"] = bool(v)
+                if v:
+                    self._lecture_keys.setdefault(r["lecture_id"], set()).add(k)
             self.acked += len(rows)
         return rows
 
@@ -108,11 +134,18 @@ class AttendanceProcessor:
 
     # attendance_processor.py:149-165 (the Cassandra half is out of scope)
     def get_attendance_stats(self, lecture_id: str, day: str | None = None) -> dict:
-        if self.config.hll_key_form == "code" or day is None:
-            key = f"{self.config.hll_key_prefix}{lecture_id}" + (f":{day}" if day else "")
-        else:
-            key = f"{self.config.hll_key_prefix}{lecture_id}:{day}"
-        return {"unique_attendees": self.redis_client.pfcount(key)}
+        """PFCOUNT of the lecture's key (:151-152).  In the README key form a
+        lecture is counted per day: with a day, that day's key; without one
+        (the reference's signature), the union of every day key this
+        processor counted the lecture's valid events into -- PFCOUNT k1 k2 ..."""
+        prefix = self.config.hll_key_prefix
+        if self.config.hll_key_form == "code":
+            key = f"{prefix}{lecture_id}" + (f":{day}" if day else "")
+            return {"unique_attendees": self.redis_client.pfcount(key)}
+        if day is not None:
+            return {"unique_attendees": self.redis_client.pfcount(f"{prefix}{lecture_id}:{day}")}
+        keys = sorted(self._lecture_keys.get(lecture_id, ()))
+        return {"unique_attendees": self.redis_client.pfcount(*keys) if keys else 0}
 
 
 def rank_top_bottom(counts: np.ndarray, keys: Sequence[str], k: int) -> tuple[list, list]:

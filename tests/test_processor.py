@@ -65,9 +65,10 @@ class OracleClient:
         c = self.chains.get(bf_key)
         out = []
         for k, i in zip(keys, ids):
-            v = bool(c.exists(str(i).encode())) if c else False
+            b = i if isinstance(i, bytes) else str(i).encode()
+            v = bool(c.exists(b)) if c else False
             if v:
-                self.hlls.setdefault(k, self.orc.HLL()).add(str(i).encode())
+                self.hlls.setdefault(k, self.orc.HLL()).add(b)
             out.append(v)
         return np.array(out)
 
@@ -98,6 +99,89 @@ def test_setup_quirk_and_batches(pkg, orc):
     assert key in cl.hlls
     assert p.get_attendance_stats("LECTURE_20250317", "2025-03-17")["unique_attendees"] == \
         cl.hlls[key].count()
+
+
+def _per_event_reference(orc, chain, msgs, row_types=True):
+    """attendance_processor.py:100-137 one message at a time: json.loads,
+    fields, fromisoformat, BF.EXISTS (redis-py encoding), the Cassandra INSERT's
+    column types, then PFADD if valid.  Returns (acked, nacked, answers, hlls)."""
+    from rtsas_amd.encoding import encode
+    from rtsas_amd.exceptions import DataError
+    acked = nacked = 0
+    answers, hlls = [], {}
+    for m in msgs:
+        try:
+            data = json.loads(m)
+            sid, lecture = data["student_id"], data["lecture_id"]
+            ts = datetime.fromisoformat(data["timestamp"])
+            b = encode(sid)
+            v = bool(chain.exists(b))
+            if row_types and (type(sid) is not int or not -2**31 <= sid < 2**31
+                              or not isinstance(lecture, str)):
+                raise TypeError("INSERT")
+            if v:
+                hlls.setdefault(f"hll:unique:{lecture}:{ts.date().isoformat()}", orc.HLL()).add(b)
+            answers.append(v)
+            acked += 1
+        except (ValueError, KeyError, TypeError, DataError):
+            nacked += 1
+    return acked, nacked, answers, hlls
+
+
+ODD_IDS = [True, None, {"a": 1}, [1, 2], 12.5, "12345", 2**31, -2**31 - 1, -5, 0, 2**31 - 1]
+
+
+def _odd_messages(valid):
+    """Messages whose student_id redis-py refuses (bool, None, dict, list), or
+    the Cassandra int column refuses (float, str, out of int32), mixed with
+    ordinary ones, plus a non-string lecture_id."""
+    msgs = []
+    for j, sid in enumerate(ODD_IDS + valid[:40]):
+        msgs.append(json.dumps({"student_id": sid, "timestamp": "2025-03-19T09:00:00",
+                                "lecture_id": "LECTURE_20250319", "is_valid": True,
+                                "event_type": "entry"}).encode())
+    msgs.append(json.dumps({"student_id": valid[0], "timestamp": "2025-03-19T09:00:00",
+                            "lecture_id": 20250319}).encode())
+    return msgs
+
+
+@pytest.mark.parametrize("row_types", [True, False])
+def test_process_batch_nacks_per_message(pkg, orc, row_types):
+    """One refused id does not fail the batch: every message gets the per-event
+    loop's ack / nack, answers and registers (attendance_processor.py:134-136)."""
+    cl = OracleClient(orc)
+    valid, _ = reference_messages(n_students=60)
+    for sid in valid:
+        cl.execute_command("BF.ADD", "bf:students", sid)
+    msgs = _odd_messages(valid)
+    p = pkg.AttendanceProcessor(client=cl, config=pkg.AttendanceConfig(cassandra_row_types=row_types))
+    rows = p.process_batch(msgs)
+    acked, nacked, answers, hlls = _per_event_reference(orc, cl.chains["bf:students"], msgs, row_types)
+    assert (p.acked, p.nacked) == (acked, nacked) == (len(rows), len(msgs) - len(rows))
+    assert [r["is_valid"] for r in rows] == answers
+    assert set(cl.hlls) == set(hlls)
+    for k, h in hlls.items():
+        assert np.array_equal(cl.hlls[k].regs, h.regs)
+    if row_types:
+        assert nacked == 4 + 4 + 1  # 4 unencodable, 4 non-int32 ids, 1 int lecture_id
+
+
+def test_stats_without_day_unions_the_lecture_days(pkg, orc):
+    """README key form: get_attendance_stats(lecture_id) -- the reference's
+    signature -- is the PFCOUNT union of the lecture's day keys."""
+    cl = OracleClient(orc)
+    valid, msgs = reference_messages(n_students=150, days=3)
+    for sid in valid:
+        cl.execute_command("BF.ADD", "bf:students", sid)
+    same = [json.loads(m) for m in msgs]
+    for m in same:
+        m["lecture_id"] = "CS101-L1"
+    p = pkg.AttendanceProcessor(client=cl)
+    p.process_batch([json.dumps(m).encode() for m in same])
+    days = sorted(k for k in cl.hlls if k.startswith("hll:unique:CS101-L1:"))
+    assert len(days) == 3
+    assert p.get_attendance_stats("CS101-L1")["unique_attendees"] == cl.pfcount(*days)
+    assert p.get_attendance_stats("CS999")["unique_attendees"] == 0
 
 
 def test_non_faithful_setup_reserves(pkg, orc):
@@ -159,3 +243,67 @@ def test_rank_top_bottom_matches_full_sort(pkg):
         kk = min(k, len(keys))
         assert head == order[:kk]
         assert tail == (order[-kk:] if kk else [])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("row_types", [True, False])
+def test_process_batch_nacks_per_message_on_device(pkg, orc, row_types):
+    """The same odd ids through the real client: acks, nacks, answers and
+    registers equal the per-event loop; the refused ids fail no other
+    message of the batch."""
+    client = pkg.SketchClient(decode_responses=True)
+    valid, _ = reference_messages(n_students=60)
+    ref = OracleClient(orc)
+    for sid in valid:
+        client.execute_command("BF.ADD", "bf:students", sid)
+        ref.execute_command("BF.ADD", "bf:students", sid)
+    msgs = _odd_messages(valid)
+    p = pkg.AttendanceProcessor(client=client,
+                                config=pkg.AttendanceConfig(cassandra_row_types=row_types))
+    rows = p.process_batch(msgs)
+    acked, nacked, answers, hlls = _per_event_reference(orc, ref.chains["bf:students"], msgs,
+                                                        row_types)
+    assert (p.acked, p.nacked) == (acked, nacked)
+    assert [r["is_valid"] for r in rows] == answers
+    for k, h in hlls.items():
+        assert np.array_equal(client.hll_registers(k), h.regs)
+        assert client.pfcount(k) == h.count()
+    client.flushall()
+
+
+@pytest.mark.gpu
+def test_c1_readme_default_exact(pkg, orc):
+    """C1 exactly as BASELINE.json configs[0] states it: bf:students RESERVE
+    0.01 / 100000, 1000 unique 5-digit ids preloaded one BF.ADD each
+    (data_generator.py:53-63), 10k swipes of lecture CS101-L1 on one day with
+    the reference's invalid mix (~7 %, 50 six-digit ids, :80-81), through the
+    processor: every answer, the register array and PFCOUNT == the per-event
+    loop over the oracle."""
+    rng = np.random.default_rng(20251003)
+    client = pkg.SketchClient(decode_responses=True)
+    p = pkg.AttendanceProcessor(client=client, config=pkg.AttendanceConfig(batch_size=4096,
+                                                                           faithful_setup=False))
+    p._setup_bloom_filter()   # BF.RESERVE bf:students 0.01 100000
+    ref = OracleClient(orc)
+    ref.execute_command("BF.RESERVE", "bf:students", 0.01, 100000)
+    members = [int(x) for x in rng.choice(np.arange(10000, 100000), 1000, replace=False)]
+    invalid = [int(x) for x in rng.choice(np.arange(100000, 1000000), 50, replace=False)]
+    adds = [client.execute_command("BF.ADD", "bf:students", sid) for sid in members]
+    assert adds == [ref.execute_command("BF.ADD", "bf:students", sid) for sid in members]
+    info = client.bf_links("bf:students")
+    assert len(info) == 1 and info[0]["bytes"] == 137848 and info[0]["hashes"] == 8
+    bad = rng.random(10_000) < 0.071
+    ids = np.where(bad, rng.choice(invalid, 10_000), rng.choice(members, 10_000))
+    msgs = [json.dumps({"student_id": int(s), "timestamp": f"2025-03-19T{9 + i % 3:02d}:00:00",
+                        "lecture_id": "CS101-L1", "is_valid": not bool(b),
+                        "event_type": "entry"}).encode() for i, (s, b) in enumerate(zip(ids, bad))]
+    rows = [r for batch in p.process_attendance(msgs) for r in batch]
+    acked, nacked, answers, hlls = _per_event_reference(orc, ref.chains["bf:students"], msgs)
+    assert (p.acked, p.nacked) == (acked, nacked) == (10_000, 0)
+    assert [r["is_valid"] for r in rows] == answers
+    key = "hll:unique:CS101-L1:2025-03-19"
+    assert list(hlls) == [key]
+    assert np.array_equal(client.hll_registers(key), hlls[key].regs)
+    assert p.get_attendance_stats("CS101-L1", "2025-03-19")["unique_attendees"] == hlls[key].count()
+    assert p.get_attendance_stats("CS101-L1")["unique_attendees"] == hlls[key].count()
+    client.flushall()
