@@ -107,6 +107,8 @@ struct Scratch;
 bool part_supported(const ChainDev &ch);
 // sizes the context scratch for batches of up to n swipes (no launch)
 // sub: swipes per sub-batch of the three passes (0: the default, 16M)
+// hll_mode: 1 = PFADD by owned register lines (partitioned, no atomics),
+//           0 = per-swipe pre-check + CAS
 hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub, Scratch *scr);
 // hook (may be null): called as hook(user, pass, 0) right before and
 // hook(user, pass, 1) right after each pass's launch (pass 0..2 = A, B, C)
@@ -114,7 +116,7 @@ typedef void (*PassHook)(void *user, int pass, int end);
 hipError_t launch_swipes_part(const ChainDev &ch, const uint8_t *bytes, const uint32_t *offs,
                               uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *regs,
                               uint32_t nslots, uint8_t *out, Scratch *scr, unsigned int *err, int cus,
-                              uint32_t sub, hipStream_t st, PassHook hook = nullptr,
+                              uint32_t sub, int hll_mode, hipStream_t st, PassHook hook = nullptr,
                               void *hook_user = nullptr);
 
 // sketch_order.hip -- order-exact paths (replies that depend on item order)

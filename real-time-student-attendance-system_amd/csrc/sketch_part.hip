@@ -413,6 +413,350 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
 }
 
 // ---------------------------------------------------------------------------
+// PFADD by owned register lines (passes C2, D, E): the valid swipes' register
+// updates are partitioned by register line, each line is owned by one block,
+// gathered once into LDS, raised there and written back whole.  No global
+// atomics: at C3 the CAS form above issues ~8.6M memory-side atomics and
+// 14.4M one-sector pre-checks per 16M-swipe step, while the step touches only
+// ~3.9M distinct 128-B lines.
+//
+//   C2 (k_part_c2)  per group of 8 tiles (8192 swipes): answers, and one 8-B
+//                   record (line | reg-in-line, rank) per valid swipe,
+//                   counting-sorted by level-1 bucket h1 = hash(line) >> 25
+//                   (128 buckets) into the group's region; run starts per
+//                   (bucket, group), bucket major.
+//   S  (k_part_hscan) per bucket: exclusive prefix of its runs over groups.
+//   D  (k_part_hd)  per chunk of kHChunk records of one bucket's stream:
+//                   counting sort by level-2 sub-bucket (64 per bucket).
+//   E  (k_part_he)  per sub-bucket (8192 in all): the distinct lines of its
+//                   records into an LDS table, those lines gathered into LDS
+//                   (kHLines at a time), every record's byte max in LDS
+//                   (ds CAS), the lines that changed stored back whole.  A
+//                   line that does not fit the table takes the CAS path.
+// Every register of a line is updated by the one block owning the line, so
+// the order of updates is free (max is commutative) and the result equals
+// the sequential hllAdd()s of attendance_processor.py:127-129.
+constexpr uint32_t kHGroupTiles = 8;
+constexpr uint32_t kHGroup = kHGroupTiles * kPaBlock;  // swipes per level-1 group
+constexpr uint32_t kH1 = 128;                          // level-1 buckets
+constexpr uint32_t kH2 = 64;                           // level-2 sub-buckets per bucket
+constexpr uint32_t kHChunk = 8192;                     // records per level-2 chunk
+constexpr uint32_t kHTab = 2048;                       // level-3 line table entries
+constexpr uint32_t kHLines = 448;                      // lines gathered per round (56 KiB)
+constexpr uint32_t kHeBlock = 512;
+
+struct HllArgs {
+    uint32_t *r1;      // [ngroups][kHGroup] x 2 u32: (line, reg-in-line | rank << 8)
+    uint32_t *o1;      // [kH1 + 1][o_stride] run starts per group, bucket major
+    uint32_t *p1;      // [kH1][o_stride] exclusive prefix over groups; [h][ngroups] = total
+    uint32_t *r2;      // [maxchunks][kHChunk] x 2 u32
+    uint32_t *o2;      // [maxchunks][kH2 + 1]
+    uint32_t ngroups, o_stride, maxchunks;
+};
+
+__device__ __forceinline__ uint32_t hline_mix(uint32_t line) {
+    uint32_t x = line * 0x9E3779B1u;
+    x ^= x >> 15;
+    x *= 0x85EBCA77u;
+    x ^= x >> 13;
+    return x;
+}
+__device__ __forceinline__ uint32_t hl_b1(uint32_t m) { return m >> 25; }          // 7 bits
+__device__ __forceinline__ uint32_t hl_b2(uint32_t m) { return (m >> 19) & 63u; }  // 6 bits
+__device__ __forceinline__ uint32_t hl_slot(uint32_t m) { return m & (kHTab - 1); }
+
+// exclusive scan of cnt[0..n) in place by one block (n <= 4 * blockDim.x);
+// returns the total; `tmp` holds blockDim.x / 64 words
+__device__ uint32_t block_excl_scan(uint32_t *cnt, uint32_t n, uint32_t *tmp) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x / 64;
+    uint32_t v[4], s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t i = tid * 4 + j;
+        v[j] = i < n ? cnt[i] : 0;
+        s += v[j];
+    }
+    uint32_t incl = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= uint32_t(o)) incl += y;
+    }
+    __syncthreads();
+    if (lane == 63) tmp[wave] = incl;
+    __syncthreads();
+    uint32_t run = incl - s, total = 0;
+    for (uint32_t w = 0; w < nw; w++) {
+        if (w < wave) run += tmp[w];
+        total += tmp[w];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t i = tid * 4 + j;
+        if (i < n) cnt[i] = run;
+        run += v[j];
+    }
+    __syncthreads();
+    return total;
+}
+
+__global__ void __launch_bounds__(kPaBlock) k_part_c2(const PartArgs A, const HllArgs H) {
+    __shared__ __attribute__((aligned(16))) uint2 srec[kHGroup];  // 64 KiB
+    __shared__ uint32_t hcnt[kH1 + 1];
+    __shared__ uint32_t tmp[kPaBlock / 64];
+    const uint32_t tid = threadIdx.x;
+    // groups of this block's XCD group (see part_group), round robin
+    const uint32_t x = blockIdx.x % kPGroups, nbk = gridDim.x / kPGroups;
+    const uint32_t g0 = uint32_t(uint64_t(H.ngroups) * x / kPGroups);
+    const uint32_t g1 = uint32_t(uint64_t(H.ngroups) * (x + 1) / kPGroups);
+    for (uint32_t gg = g0 + blockIdx.x / kPGroups; gg < g1; gg += nbk) {
+        if (tid <= kH1) hcnt[tid] = 0;
+        __syncthreads();
+        uint32_t line[kHGroupTiles], rr[kHGroupTiles], hp[kHGroupTiles];
+#pragma unroll
+        for (uint32_t u = 0; u < kHGroupTiles; u++) {
+            const uint32_t i = gg * kHGroup + u * kPaBlock + tid;
+            hp[u] = 0xffffffffu;
+            if (i >= A.n) continue;
+            bool valid = false;
+            for (uint32_t l = 0; l < A.nlinks; l++) valid |= A.fail[size_t(l) * A.fail_stride + i] == 0;
+            if (A.out) A.out[i] = valid;
+            if (!valid) continue;
+            const uint32_t sl = A.slot[i];
+            if (sl >= A.nslots) {
+                atomicOr(A.err, 1u);
+                continue;
+            }
+            const uint32_t hv = A.hllw[i], reg = hv & 0xffffu;
+            line[u] = sl * (kHllRegs / 128) + (reg >> 7);
+            rr[u] = (reg & 127u) | ((hv >> 16) << 8);
+            const uint32_t h = hl_b1(hline_mix(line[u]));
+            hp[u] = (h << 16) | atomicAdd(&hcnt[h], 1u);
+        }
+        __syncthreads();
+        const uint32_t total = block_excl_scan(hcnt, kH1 + 1, tmp);  // hcnt[kH1] == 0 -> total
+        (void)total;
+        if (tid <= kH1) H.o1[size_t(tid) * H.o_stride + gg] = hcnt[tid];
+#pragma unroll
+        for (uint32_t u = 0; u < kHGroupTiles; u++)
+            if (hp[u] != 0xffffffffu) srec[hcnt[hp[u] >> 16] + (hp[u] & 0xffffu)] = make_uint2(line[u], rr[u]);
+        __syncthreads();
+        const uint32_t cnt = hcnt[kH1];
+        uint4 *dst = reinterpret_cast<uint4 *>(H.r1 + size_t(gg) * kHGroup * 2);
+        const uint4 *src = reinterpret_cast<const uint4 *>(srec);
+        for (uint32_t j = tid; j * 2 < cnt; j += kPaBlock) dst[j] = src[j];
+        __syncthreads();
+    }
+}
+
+// per bucket: exclusive prefix of its run lengths over groups (p1[h][ngroups] = total)
+__global__ void __launch_bounds__(1024) k_part_hscan(const HllArgs H) {
+    __shared__ uint32_t tmp[16];
+    __shared__ uint32_t carry;
+    const uint32_t h = blockIdx.x, tid = threadIdx.x;
+    const uint32_t *ob = H.o1 + size_t(h) * H.o_stride, *oe = ob + H.o_stride;
+    uint32_t *pp = H.p1 + size_t(h) * H.o_stride;
+    if (tid == 0) carry = 0;
+    __shared__ uint32_t buf[4096];
+    for (uint32_t g0 = 0; g0 < H.ngroups; g0 += 4096) {
+        const uint32_t m = H.ngroups - g0 < 4096 ? H.ngroups - g0 : 4096;
+        for (uint32_t j = tid; j < m; j += 1024) buf[j] = oe[g0 + j] - ob[g0 + j];
+        __syncthreads();
+        const uint32_t tot = block_excl_scan(buf, m, tmp);
+        const uint32_t c = carry;
+        for (uint32_t j = tid; j < m; j += 1024) pp[g0 + j] = c + buf[j];
+        __syncthreads();
+        if (tid == 0) carry = c + tot;
+        __syncthreads();
+    }
+    if (tid == 0) pp[H.ngroups] = carry;
+}
+
+// chunk bases of the buckets: nch[h] = ceil(total[h] / kHChunk), cb = prefix
+__device__ void hll_chunks(const HllArgs &H, uint32_t *tot, uint32_t *cb, uint32_t *tmp) {
+    const uint32_t tid = threadIdx.x;
+    if (tid < kH1) {
+        tot[tid] = H.p1[size_t(tid) * H.o_stride + H.ngroups];
+        cb[tid] = (tot[tid] + kHChunk - 1) / kHChunk;
+    }
+    if (tid == kH1) cb[kH1] = 0;
+    __syncthreads();
+    block_excl_scan(cb, kH1 + 1, tmp);  // cb[kH1] = number of chunks
+}
+
+__global__ void __launch_bounds__(1024) k_part_hd(const HllArgs H) {
+    __shared__ __attribute__((aligned(16))) uint2 sa[kHChunk];  // the chunk, stream order
+    __shared__ __attribute__((aligned(16))) uint2 sb[kHChunk];  // sorted by sub-bucket
+    __shared__ uint32_t tot[kH1], cb[kH1 + 1], tmp[16], c2[kH2 + 1];
+    __shared__ uint32_t sg[2];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    hll_chunks(H, tot, cb, tmp);
+    for (uint32_t q = blockIdx.x; q < cb[kH1]; q += gridDim.x) {
+        // bucket h of chunk q, window [w0, w1) of its stream
+        uint32_t h = 0;
+        while (h + 1 < kH1 && cb[h + 1] <= q) h++;
+        const uint32_t w0 = (q - cb[h]) * kHChunk;
+        const uint32_t w1 = tot[h] - w0 < kHChunk ? tot[h] : w0 + kHChunk;
+        const uint32_t *pp = H.p1 + size_t(h) * H.o_stride;
+        const uint32_t *ob = H.o1 + size_t(h) * H.o_stride;
+        if (tid == 0) {  // groups overlapping the window: [ga, gb)
+            uint32_t lo = 0, hi = H.ngroups;  // last g with pp[g] <= w0
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) / 2;
+                if (pp[mid] <= w0) lo = mid; else hi = mid - 1;
+            }
+            sg[0] = lo;
+            uint32_t lo2 = lo, hi2 = H.ngroups;  // first g with pp[g] >= w1
+            while (lo2 < hi2) {
+                const uint32_t mid = (lo2 + hi2) / 2;
+                if (pp[mid] >= w1) hi2 = mid; else lo2 = mid + 1;
+            }
+            sg[1] = lo2;
+        }
+        if (tid <= kH2) c2[tid] = 0;
+        __syncthreads();
+        const uint32_t ga = sg[0], gb = sg[1];
+        // read the window into sa (stream order), count sub-buckets
+        for (uint32_t g = ga + wave; g < gb; g += 16) {
+            const uint32_t s0 = pp[g] > w0 ? pp[g] : w0;
+            const uint32_t s1 = pp[g + 1] < w1 ? pp[g + 1] : w1;
+            // stream position p of group g's run sits at record ob[g] + p - pp[g] of its region
+            const uint2 *rec = reinterpret_cast<const uint2 *>(H.r1) + size_t(g) * kHGroup + ob[g];
+            for (uint32_t p = s0 + lane; p < s1; p += 64) {
+                const uint2 r = rec[p - pp[g]];
+                sa[p - w0] = r;
+                atomicAdd(&c2[hl_b2(hline_mix(r.x))], 1u);
+            }
+        }
+        __syncthreads();
+        block_excl_scan(c2, kH2 + 1, tmp);
+        uint32_t *o2 = H.o2 + size_t(q) * (kH2 + 1);
+        if (tid <= kH2) o2[tid] = c2[tid];
+        __syncthreads();
+        const uint32_t cnt = w1 - w0;
+        for (uint32_t j = tid; j < cnt; j += 1024) {
+            const uint2 r = sa[j];
+            sb[atomicAdd(&c2[hl_b2(hline_mix(r.x))], 1u)] = r;
+        }
+        __syncthreads();
+        uint4 *dst = reinterpret_cast<uint4 *>(H.r2 + size_t(q) * kHChunk * 2);
+        const uint4 *src = reinterpret_cast<const uint4 *>(sb);
+        for (uint32_t j = tid; j * 2 < cnt; j += 1024) dst[j] = src[j];
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ void lds_byte_max(uint32_t *w, uint32_t sh, uint32_t rank, bool *raised) {
+    uint32_t old = *w;
+    while (((old >> sh) & 0xffu) < rank) {
+        const uint32_t prev = atomicCAS(w, old, (old & ~(0xffu << sh)) | (rank << sh));
+        if (prev == old) {
+            *raised = true;
+            return;
+        }
+        old = prev;
+    }
+}
+
+__global__ void __launch_bounds__(kHeBlock) k_part_he(const PartArgs A, const HllArgs H) {
+    __shared__ uint32_t key[kHTab];      // line + 1, 0 = empty
+    __shared__ uint16_t idx[kHTab];      // compact index of an occupied entry
+    __shared__ uint32_t lineof[kHTab];   // compact index -> line
+    __shared__ __attribute__((aligned(16))) uint32_t lines[kHLines * 32];
+    __shared__ uint8_t dirty[kHLines];
+    __shared__ uint32_t tot[kH1], cb[kH1 + 1], tmp[kHeBlock / 64], nl;
+    const uint32_t tid = threadIdx.x;
+    hll_chunks(H, tot, cb, tmp);
+    for (uint32_t sbk = blockIdx.x; sbk < kH1 * kH2; sbk += gridDim.x) {
+        const uint32_t h = sbk / kH2, h2 = sbk % kH2;
+        const uint32_t q0 = cb[h], q1 = cb[h + 1];
+        if (q0 == q1) continue;  // block-uniform
+        for (uint32_t j = tid; j < kHTab; j += kHeBlock) key[j] = 0;
+        __syncthreads();
+        // visit every record of the sub-bucket: f(record)
+        auto visit = [&](auto f) {
+            for (uint32_t q = q0 + tid / 64; q < q1; q += kHeBlock / 64) {
+                const uint32_t *o2 = H.o2 + size_t(q) * (kH2 + 1);
+                const uint32_t b = o2[h2], e = o2[h2 + 1];
+                const uint2 *rec = reinterpret_cast<const uint2 *>(H.r2) + size_t(q) * kHChunk;
+                for (uint32_t p = b + (tid & 63); p < e; p += 64) f(rec[p]);
+            }
+        };
+        // 1. distinct lines into the table (linear probing; a full table
+        //    leaves the line out: its records take the CAS path)
+        visit([&](uint2 r) {
+            uint32_t sl = hl_slot(hline_mix(r.x));
+            for (uint32_t probe = 0; probe < kHTab; probe++) {
+                const uint32_t prev = atomicCAS(&key[sl], 0u, r.x + 1);
+                if (prev == 0 || prev == r.x + 1) break;
+                sl = (sl + 1) & (kHTab - 1);
+            }
+        });
+        __syncthreads();
+        // 2. compact indices of the occupied entries
+        {
+            uint32_t *c = reinterpret_cast<uint32_t *>(lines);  // scratch: kHTab words
+            for (uint32_t j = tid; j < kHTab; j += kHeBlock) c[j] = key[j] != 0;
+            __syncthreads();
+            const uint32_t n = block_excl_scan(c, kHTab, tmp);
+            for (uint32_t j = tid; j < kHTab; j += kHeBlock)
+                if (key[j]) {
+                    idx[j] = uint16_t(c[j]);
+                    lineof[c[j]] = key[j] - 1;
+                }
+            if (tid == 0) nl = n;
+            __syncthreads();
+        }
+        const uint32_t nlines = nl;
+        // 3. rounds of kHLines lines: gather, raise, store back the changed ones
+        for (uint32_t r0 = 0; r0 < nlines || r0 == 0; r0 += kHLines) {
+            const uint32_t rn = nlines - r0 < kHLines ? nlines - r0 : kHLines;
+            for (uint32_t j = tid; j < rn * 8; j += kHeBlock) {  // 8 lanes x 16 B per line
+                const uint32_t li = j / 8, part = j % 8;
+                const uint4 v = *reinterpret_cast<const uint4 *>(A.regs + size_t(lineof[r0 + li]) * 128 + part * 16);
+                *reinterpret_cast<uint4 *>(&lines[li * 32 + part * 4]) = v;
+            }
+            for (uint32_t j = tid; j < kHLines; j += kHeBlock) dirty[j] = 0;
+            __syncthreads();
+            visit([&](uint2 r) {
+                const uint32_t reg = r.y & 127u, rank = r.y >> 8;
+                uint32_t sl = hl_slot(hline_mix(r.x));
+                uint32_t at = 0xffffffffu;
+                for (uint32_t probe = 0; probe < kHTab; probe++) {
+                    const uint32_t k = key[sl];
+                    if (k == r.x + 1) {
+                        at = idx[sl];
+                        break;
+                    }
+                    if (k == 0) break;
+                    sl = (sl + 1) & (kHTab - 1);
+                }
+                if (at == 0xffffffffu) {  // not in the table: CAS on the slab, first round only
+                    if (r0 == 0) {
+                        uint32_t *w = reinterpret_cast<uint32_t *>(A.regs + size_t(r.x) * 128 + (reg & ~3u));
+                        part_reg_max(w, (reg & 3) * 8, rank, *w);
+                    }
+                    return;
+                }
+                if (at < r0 || at >= r0 + rn) return;
+                bool raised = false;
+                lds_byte_max(&lines[(at - r0) * 32 + reg / 4], (reg & 3) * 8, rank, &raised);
+                if (raised) dirty[at - r0] = 1;
+            });
+            __syncthreads();
+            for (uint32_t j = tid; j < rn * 8; j += kHeBlock) {
+                const uint32_t li = j / 8, part = j % 8;
+                if (dirty[li])
+                    *reinterpret_cast<uint4 *>(A.regs + size_t(lineof[r0 + li]) * 128 + part * 16) =
+                        *reinterpret_cast<const uint4 *>(&lines[li * 32 + part * 4]);
+            }
+            __syncthreads();
+            if (nlines == 0) break;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 static inline unsigned part_grid(uint64_t n, unsigned block, unsigned cap) {
@@ -463,6 +807,20 @@ bool part_supported(const ChainDev &ch) {
 
 // the scratch of a sub-batch of up to `sub` swipes (slots 28-31 of the context
 // scratch: probe records, run boundaries, fail bytes, HLL words)
+// the line-owned PFADD's scratch (slots 32-35): level-1 and level-2 records and run tables
+static hipError_t hll_scratch(HllArgs *H, uint32_t m, Scratch *scr) {
+    H->ngroups = (m + kHGroup - 1) / kHGroup;
+    H->o_stride = (H->ngroups + 1 + 15) & ~15u;
+    H->maxchunks = (m + kHChunk - 1) / kHChunk + kH1;
+    hipError_t e = hipSuccess;
+    H->r1 = (uint32_t *)scratch_get(scr, 32, size_t(H->ngroups) * kHGroup * 8, &e);
+    if (e == hipSuccess) H->o1 = (uint32_t *)scratch_get(scr, 33, size_t(kH1 + 1) * H->o_stride * 4, &e);
+    if (e == hipSuccess) H->p1 = (uint32_t *)scratch_get(scr, 34, size_t(kH1) * H->o_stride * 4, &e);
+    if (e == hipSuccess) H->r2 = (uint32_t *)scratch_get(scr, 35, size_t(H->maxchunks) * kHChunk * 8, &e);
+    if (e == hipSuccess) H->o2 = (uint32_t *)scratch_get(scr, 36, size_t(H->maxchunks) * (kH2 + 1) * 4, &e);
+    return e;
+}
+
 static hipError_t part_scratch(PartArgs *A, uint64_t n, uint32_t sub, Scratch *scr) {
     const uint32_t m = n < sub ? uint32_t(n) : sub;
     const uint32_t ntiles_max = (m + kPaBlock - 1) / kPaBlock;
@@ -474,6 +832,10 @@ static hipError_t part_scratch(PartArgs *A, uint64_t n, uint32_t sub, Scratch *s
     if (e == hipSuccess) A->fail = (uint8_t *)scratch_get(scr, 30, size_t(fstride) * A->nlinks, &e);
     if (e == hipSuccess) A->hllw = (uint32_t *)scratch_get(scr, 31, size_t(m) * 4, &e);
     A->fail_stride = fstride;
+    if (e == hipSuccess) {
+        HllArgs H{};
+        e = hll_scratch(&H, m, scr);
+    }
     return e;
 }
 
@@ -492,7 +854,8 @@ hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratc
 hipError_t launch_swipes_part(const ChainDev &ch, const uint8_t *bytes, const uint32_t *offs,
                               uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *regs,
                               uint32_t nslots, uint8_t *out, Scratch *scr, unsigned int *err, int cus,
-                              uint32_t sub_opt, hipStream_t st, PassHook hook, void *hook_user) {
+                              uint32_t sub_opt, int hll_mode, hipStream_t st, PassHook hook,
+                              void *hook_user) {
     if (n == 0) return hipSuccess;
     PartArgs A{};
     if (!part_plan(ch, &A)) return hipErrorInvalidValue;
@@ -526,8 +889,20 @@ hipError_t launch_swipes_part(const ChainDev &ch, const uint8_t *bytes, const ui
         hipLaunchKernelGGL(k_part_b, dim3(gb), dim3(kPbBlock), 0, st, A);
         if (hook) hook(hook_user, 1, 1);
         if (hook) hook(hook_user, 2, 0);
-        const unsigned gc = (part_grid(ms, kPcBlock * 2, cus * 8) + kPGroups - 1) / kPGroups * kPGroups;
-        hipLaunchKernelGGL(k_part_c<2>, dim3(gc), dim3(kPcBlock), 0, st, A);
+        if (hll_mode == 1) {
+            // PFADD by owned register lines: C2, S, D, E (timed together as pass C)
+            HllArgs H{};
+            e = hll_scratch(&H, ms, scr);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(k_part_c2, dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(kPaBlock), 0,
+                               st, A, H);
+            hipLaunchKernelGGL(k_part_hscan, dim3(kH1), dim3(1024), 0, st, H);
+            hipLaunchKernelGGL(k_part_hd, dim3(unsigned(cus)), dim3(1024), 0, st, H);
+            hipLaunchKernelGGL(k_part_he, dim3(unsigned(cus) * 2), dim3(kHeBlock), 0, st, A, H);
+        } else {
+            const unsigned gc = (part_grid(ms, kPcBlock * 2, cus * 8) + kPGroups - 1) / kPGroups * kPGroups;
+            hipLaunchKernelGGL(k_part_c<2>, dim3(gc), dim3(kPcBlock), 0, st, A);
+        }
         if (hook) hook(hook_user, 2, 1);
     }
     return hipGetLastError();

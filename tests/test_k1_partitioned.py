@@ -33,9 +33,11 @@ def _pack(items):
     return buf, offs
 
 
-def test_partitioned_two_link_chain_ragged(engine, orc):
+@pytest.mark.parametrize("hll_mode", [1, 0])
+def test_partitioned_two_link_chain_ragged(engine, orc, hll_mode):
     """RESERVE 0.01 / 20000 grown to two links (k = 8, 9: 17 probes per swipe,
-    tiles of 1024 swipes), ragged ids; the partitioned kernel forced."""
+    tiles of 1024 swipes), ragged ids; the partitioned kernel forced, its
+    PFADD by owned register lines (1) or by CAS (0)."""
     from rtsas_amd.engine import DeviceBatch, DeviceBuffer
     rng = np.random.default_rng(21)
     members = _rand_items(rng, 30000, 40, 1)
@@ -49,6 +51,7 @@ def test_partitioned_two_link_chain_ragged(engine, orc):
     chain.madd_packed(mb, mo)
     assert chain.nlinks == 2
     engine.set_option("variant", 3)
+    engine.set_option("hll_mode", hll_mode)
     assert engine.variant(0) == 3
     items = [members[int(i)] for i in rng.integers(0, len(members), 60000)]
     items += _rand_items(rng, 20000, 40)
@@ -175,3 +178,35 @@ def test_hll_reserve_refused_while_graph_alive(engine):
     engine.sync()
     g.free()
     engine.hll_reserve(cap + 100)  # no graph holds the slab any more
+
+
+@pytest.mark.parametrize("hll_mode", [1, 0])
+def test_partitioned_hot_register_and_many_keys(engine, orc, hll_mode):
+    """Adversarial PFADD shapes for the line-owned apply: 2M swipes where half
+    repeat ONE id into ONE key (one register line takes a million updates) and
+    the rest spread over 40k keys (many lines per sub-bucket); registers ==
+    the oracle."""
+    from rtsas_amd.engine import DeviceBatch, DeviceBuffer
+    w, p = _c3_small(engine)
+    engine.set_option("hll_mode", hll_mode)
+    engine.hll_reserve(40_001)
+    b = engine.swipe_batch(p, 0, 2_000_000)
+    buf, offs, slot = b.to_host()
+    slot = (np.arange(b.n, dtype=np.uint64) * 2654435761 % 40_000).astype(np.uint32)
+    hot = np.arange(0, b.n, 2)
+    first = bytes(buf[offs[0]:offs[1]])
+    assert all(offs[i + 1] - offs[i] == 8 for i in (0, 1))
+    ids = buf[:offs[-1]].reshape(-1, 8).copy()
+    ids[hot] = np.frombuffer(first, np.uint8)
+    slot[hot] = 40_000
+    buf2 = np.concatenate([ids.reshape(-1), np.zeros(16, np.uint8)])
+    d = DeviceBatch.from_host(engine.ctx, buf2, offs, slot)
+    out = DeviceBuffer(engine.ctx, b.n)
+    engine.swipes(0, d, out)
+    chain = orc.Chain(w.bf_capacity, w.bf_error)
+    mb = engine.members_batch(p, 0, w.n_members).to_host()
+    chain.madd_packed(mb[0], mb[1])
+    regs = np.zeros((40_001, 16384), np.uint8)
+    want, _, _ = orc.process_swipes(chain, regs, slot, buf2, offs)
+    assert np.array_equal(out.to_host(np.uint8, b.n), want)
+    assert np.array_equal(engine.registers_all(40_001), regs)
