@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--ablate", type=int, default=0, help="diagnostic: K1 parts removed (bits)")
     ap.add_argument("--part-sub", type=int, default=0,
                     help="partitioned K1: swipes per sub-batch of its three passes (0 = default)")
+    ap.add_argument("--hll-mode", type=int, default=-1,
+                    help="partitioned K1 PFADD: 0 = CAS on the slab, 1 = owned register lines "
+                         "(-1: library default)")
     ap.add_argument("--streams", type=int, default=0,
                     help="HIP streams / graph branches the steps alternate over (0: 16 for the "
                          "LDS K1, 1 otherwise)")
@@ -299,6 +302,8 @@ def main():
             engine.set_option(name, val)
     if args.variant >= 0:
         engine.set_option("variant", args.variant)
+    if args.hll_mode >= 0:
+        engine.set_option("hll_mode", args.hll_mode)
 
     # Bloom preload (replicated on every rank), this rank's HLL key shard, and
     # 64 spare slots for the verification batch

@@ -442,8 +442,9 @@ constexpr uint32_t kH1 = 128;                          // level-1 buckets
 constexpr uint32_t kH2 = 64;                           // level-2 sub-buckets per bucket
 constexpr uint32_t kHChunk = 8192;                     // records per level-2 chunk
 constexpr uint32_t kHTab = 2048;                       // level-3 line table entries
-constexpr uint32_t kHLines = 448;                      // lines gathered per round (56 KiB)
+constexpr uint32_t kHLines = 384;                      // lines gathered per round (48 KiB)
 constexpr uint32_t kHeBlock = 512;
+constexpr uint32_t kHProbe = 32;                       // longest probe chain of the line table
 
 struct HllArgs {
     uint32_t *r1;      // [ngroups][kHGroup] x 2 u32: (line, reg-in-line | rank << 8)
@@ -451,7 +452,8 @@ struct HllArgs {
     uint32_t *p1;      // [kH1][o_stride] exclusive prefix over groups; [h][ngroups] = total
     uint32_t *r2;      // [maxchunks][kHChunk] x 2 u32
     uint32_t *o2;      // [maxchunks][kH2 + 1]
-    uint32_t ngroups, o_stride, maxchunks;
+    uint32_t *cst;     // [kH1][c_stride] group holding the first record of each chunk
+    uint32_t ngroups, o_stride, maxchunks, c_stride;
 };
 
 __device__ __forceinline__ uint32_t hline_mix(uint32_t line) {
@@ -549,22 +551,30 @@ __global__ void __launch_bounds__(kPaBlock) k_part_c2(const PartArgs A, const Hl
     }
 }
 
-// per bucket: exclusive prefix of its run lengths over groups (p1[h][ngroups] = total)
+// per bucket: exclusive prefix of its run lengths over groups (p1[h][ngroups]
+// = total), and the group holding the first record of each of its level-2
+// chunks (cst[h][c], c < ceil(total / kHChunk))
 __global__ void __launch_bounds__(1024) k_part_hscan(const HllArgs H) {
     __shared__ uint32_t tmp[16];
     __shared__ uint32_t carry;
+    __shared__ uint32_t buf[4096];
     const uint32_t h = blockIdx.x, tid = threadIdx.x;
     const uint32_t *ob = H.o1 + size_t(h) * H.o_stride, *oe = ob + H.o_stride;
     uint32_t *pp = H.p1 + size_t(h) * H.o_stride;
+    uint32_t *cst = H.cst + size_t(h) * H.c_stride;
     if (tid == 0) carry = 0;
-    __shared__ uint32_t buf[4096];
     for (uint32_t g0 = 0; g0 < H.ngroups; g0 += 4096) {
         const uint32_t m = H.ngroups - g0 < 4096 ? H.ngroups - g0 : 4096;
         for (uint32_t j = tid; j < m; j += 1024) buf[j] = oe[g0 + j] - ob[g0 + j];
         __syncthreads();
         const uint32_t tot = block_excl_scan(buf, m, tmp);
         const uint32_t c = carry;
-        for (uint32_t j = tid; j < m; j += 1024) pp[g0 + j] = c + buf[j];
+        for (uint32_t j = tid; j < m; j += 1024) {
+            const uint32_t a = c + buf[j], len = oe[g0 + j] - ob[g0 + j];
+            pp[g0 + j] = a;
+            // chunks whose first position falls inside this group's run
+            for (uint32_t q = (a + kHChunk - 1) / kHChunk; q * kHChunk < a + len; q++) cst[q] = g0 + j;
+        }
         __syncthreads();
         if (tid == 0) carry = c + tot;
         __syncthreads();
@@ -584,61 +594,91 @@ __device__ void hll_chunks(const HllArgs &H, uint32_t *tot, uint32_t *cb, uint32
     block_excl_scan(cb, kH1 + 1, tmp);  // cb[kH1] = number of chunks
 }
 
-__global__ void __launch_bounds__(1024) k_part_hd(const HllArgs H) {
-    __shared__ __attribute__((aligned(16))) uint2 sa[kHChunk];  // the chunk, stream order
+// index of the last entry of a[0..n) (ascending) that is <= v (a[0] <= v)
+__device__ __forceinline__ uint32_t lds_last_le(const uint32_t *a, uint32_t n, uint32_t v) {
+    uint32_t lo = 0, len = n;
+    while (len > 1) {
+        const uint32_t half = len / 2;
+        if (a[lo + half] <= v) lo += half;
+        len -= half;
+    }
+    return lo;
+}
+
+// Level 2: one chunk (kHChunk consecutive records of a bucket's stream) per
+// iteration.  Its groups' run starts are staged in LDS; every thread reads 8
+// records of the window at once (a binary search in LDS finds each one's
+// group), counts their sub-buckets, and after the scan places them from its
+// registers.  A window spread over more than kHdGroups groups (only with
+// adversarial key skew) reads group by group.
+constexpr uint32_t kHdGroups = 1536;
+__global__ void __launch_bounds__(1024, 8) k_part_hd(const HllArgs H) {
     __shared__ __attribute__((aligned(16))) uint2 sb[kHChunk];  // sorted by sub-bucket
+    __shared__ uint32_t spp[kHdGroups + 1], sob[kHdGroups];
     __shared__ uint32_t tot[kH1], cb[kH1 + 1], tmp[16], c2[kH2 + 1];
-    __shared__ uint32_t sg[2];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t tid = threadIdx.x;
+    constexpr uint32_t R = kHChunk / 1024;
     hll_chunks(H, tot, cb, tmp);
     for (uint32_t q = blockIdx.x; q < cb[kH1]; q += gridDim.x) {
-        // bucket h of chunk q, window [w0, w1) of its stream
         uint32_t h = 0;
         while (h + 1 < kH1 && cb[h + 1] <= q) h++;
-        const uint32_t w0 = (q - cb[h]) * kHChunk;
+        const uint32_t c = q - cb[h], w0 = c * kHChunk;
         const uint32_t w1 = tot[h] - w0 < kHChunk ? tot[h] : w0 + kHChunk;
         const uint32_t *pp = H.p1 + size_t(h) * H.o_stride;
         const uint32_t *ob = H.o1 + size_t(h) * H.o_stride;
-        if (tid == 0) {  // groups overlapping the window: [ga, gb)
-            uint32_t lo = 0, hi = H.ngroups;  // last g with pp[g] <= w0
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi + 1) / 2;
-                if (pp[mid] <= w0) lo = mid; else hi = mid - 1;
+        const uint32_t *cst = H.cst + size_t(h) * H.c_stride;
+        const uint32_t ga = cst[c];
+        const uint32_t gb = w1 < tot[h] ? cst[c + 1] + 1 : H.ngroups;  // groups [ga, gb)
+        const uint32_t ng = gb - ga;
+        const bool staged = ng <= kHdGroups;  // block-uniform
+        if (staged)
+            for (uint32_t j = tid; j <= ng; j += 1024) {
+                spp[j] = pp[ga + j];
+                if (j < ng) sob[j] = ob[ga + j];
             }
-            sg[0] = lo;
-            uint32_t lo2 = lo, hi2 = H.ngroups;  // first g with pp[g] >= w1
-            while (lo2 < hi2) {
-                const uint32_t mid = (lo2 + hi2) / 2;
-                if (pp[mid] >= w1) hi2 = mid; else lo2 = mid + 1;
-            }
-            sg[1] = lo2;
-        }
         if (tid <= kH2) c2[tid] = 0;
         __syncthreads();
-        const uint32_t ga = sg[0], gb = sg[1];
-        // read the window into sa (stream order), count sub-buckets
-        for (uint32_t g = ga + wave; g < gb; g += 16) {
-            const uint32_t s0 = pp[g] > w0 ? pp[g] : w0;
-            const uint32_t s1 = pp[g + 1] < w1 ? pp[g + 1] : w1;
-            // stream position p of group g's run sits at record ob[g] + p - pp[g] of its region
-            const uint2 *rec = reinterpret_cast<const uint2 *>(H.r1) + size_t(g) * kHGroup + ob[g];
-            for (uint32_t p = s0 + lane; p < s1; p += 64) {
-                const uint2 r = rec[p - pp[g]];
-                sa[p - w0] = r;
-                atomicAdd(&c2[hl_b2(hline_mix(r.x))], 1u);
+        uint2 r[R];
+        uint32_t bp[R];
+        const uint2 *r1 = reinterpret_cast<const uint2 *>(H.r1);
+#pragma unroll
+        for (uint32_t j = 0; j < R; j++) {
+            const uint32_t p = w0 + j * 1024 + tid;
+            bp[j] = 0xffffffffu;
+            if (p >= w1) continue;
+            uint32_t g, a, o;
+            if (staged) {
+                const uint32_t k = lds_last_le(spp, ng, p);
+                g = ga + k;
+                a = spp[k];
+                o = sob[k];
+            } else {
+                uint32_t lo = ga, hi = gb - 1;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi + 1) / 2;
+                    if (pp[mid] <= p) lo = mid; else hi = mid - 1;
+                }
+                g = lo;
+                a = pp[g];
+                o = ob[g];
             }
+            r[j] = r1[size_t(g) * kHGroup + o + (p - a)];
         }
+#pragma unroll
+        for (uint32_t j = 0; j < R; j++)
+            if (w0 + j * 1024 + tid < w1) {
+                const uint32_t b2 = hl_b2(hline_mix(r[j].x));
+                bp[j] = (b2 << 16) | atomicAdd(&c2[b2], 1u);
+            }
         __syncthreads();
         block_excl_scan(c2, kH2 + 1, tmp);
         uint32_t *o2 = H.o2 + size_t(q) * (kH2 + 1);
         if (tid <= kH2) o2[tid] = c2[tid];
+#pragma unroll
+        for (uint32_t j = 0; j < R; j++)
+            if (bp[j] != 0xffffffffu) sb[c2[bp[j] >> 16] + (bp[j] & 0xffffu)] = r[j];
         __syncthreads();
         const uint32_t cnt = w1 - w0;
-        for (uint32_t j = tid; j < cnt; j += 1024) {
-            const uint2 r = sa[j];
-            sb[atomicAdd(&c2[hl_b2(hline_mix(r.x))], 1u)] = r;
-        }
-        __syncthreads();
         uint4 *dst = reinterpret_cast<uint4 *>(H.r2 + size_t(q) * kHChunk * 2);
         const uint4 *src = reinterpret_cast<const uint4 *>(sb);
         for (uint32_t j = tid; j * 2 < cnt; j += 1024) dst[j] = src[j];
@@ -658,100 +698,139 @@ __device__ __forceinline__ void lds_byte_max(uint32_t *w, uint32_t sh, uint32_t 
     }
 }
 
-__global__ void __launch_bounds__(kHeBlock) k_part_he(const PartArgs A, const HllArgs H) {
+// Level 3: one sub-bucket per iteration.  Its records -- the sub-bucket's run
+// of each chunk of the bucket -- are read kHeRec at a time (kHeR per thread,
+// all in flight; a binary search over the runs' prefix in LDS finds each
+// record) and kept in registers.  For every window: its distinct lines into
+// the LDS table, compacted; the lines gathered into LDS kHLines at a time
+// (L1-bypassing loads: a line this block stored for an earlier window is read
+// back from L2), every record's byte max in LDS, the changed lines stored
+// back whole.  A line that misses the full table takes the CAS path.
+constexpr uint32_t kHeR = 8;
+constexpr uint32_t kHeRec = kHeBlock * kHeR;
+constexpr uint32_t kHeRuns = 1024;
+__global__ void __launch_bounds__(kHeBlock, 4) k_part_he(const PartArgs A, const HllArgs H) {
     __shared__ uint32_t key[kHTab];      // line + 1, 0 = empty
     __shared__ uint16_t idx[kHTab];      // compact index of an occupied entry
-    __shared__ uint32_t lineof[kHTab];   // compact index -> line
     __shared__ __attribute__((aligned(16))) uint32_t lines[kHLines * 32];
     __shared__ uint8_t dirty[kHLines];
+    __shared__ uint32_t lof[kHLines];   // lines of the current round
+    __shared__ uint32_t rpre[kHeRuns + 1], rbase[kHeRuns];
     __shared__ uint32_t tot[kH1], cb[kH1 + 1], tmp[kHeBlock / 64], nl;
     const uint32_t tid = threadIdx.x;
+    const uint2 *r2 = reinterpret_cast<const uint2 *>(H.r2);
     hll_chunks(H, tot, cb, tmp);
     for (uint32_t sbk = blockIdx.x; sbk < kH1 * kH2; sbk += gridDim.x) {
         const uint32_t h = sbk / kH2, h2 = sbk % kH2;
         const uint32_t q0 = cb[h], q1 = cb[h + 1];
         if (q0 == q1) continue;  // block-uniform
-        for (uint32_t j = tid; j < kHTab; j += kHeBlock) key[j] = 0;
-        __syncthreads();
-        // visit every record of the sub-bucket: f(record)
-        auto visit = [&](auto f) {
-            for (uint32_t q = q0 + tid / 64; q < q1; q += kHeBlock / 64) {
-                const uint32_t *o2 = H.o2 + size_t(q) * (kH2 + 1);
+        // the runs of this sub-bucket, kHeRuns chunks at a time
+        for (uint32_t qa = q0; qa < q1; qa += kHeRuns) {
+            const uint32_t nq = q1 - qa < kHeRuns ? q1 - qa : kHeRuns;
+            __syncthreads();
+            for (uint32_t j = tid; j < nq; j += kHeBlock) {
+                const uint32_t *o2 = H.o2 + size_t(qa + j) * (kH2 + 1);
                 const uint32_t b = o2[h2], e = o2[h2 + 1];
-                const uint2 *rec = reinterpret_cast<const uint2 *>(H.r2) + size_t(q) * kHChunk;
-                for (uint32_t p = b + (tid & 63); p < e; p += 64) f(rec[p]);
+                rpre[j] = e - b;
+                rbase[j] = (qa + j) * kHChunk + b;
             }
-        };
-        // 1. distinct lines into the table (linear probing; a full table
-        //    leaves the line out: its records take the CAS path)
-        visit([&](uint2 r) {
-            uint32_t sl = hl_slot(hline_mix(r.x));
-            for (uint32_t probe = 0; probe < kHTab; probe++) {
-                const uint32_t prev = atomicCAS(&key[sl], 0u, r.x + 1);
-                if (prev == 0 || prev == r.x + 1) break;
-                sl = (sl + 1) & (kHTab - 1);
-            }
-        });
-        __syncthreads();
-        // 2. compact indices of the occupied entries
-        {
-            uint32_t *c = reinterpret_cast<uint32_t *>(lines);  // scratch: kHTab words
-            for (uint32_t j = tid; j < kHTab; j += kHeBlock) c[j] = key[j] != 0;
+            if (tid == 0) rpre[nq] = 0;
             __syncthreads();
-            const uint32_t n = block_excl_scan(c, kHTab, tmp);
-            for (uint32_t j = tid; j < kHTab; j += kHeBlock)
-                if (key[j]) {
-                    idx[j] = uint16_t(c[j]);
-                    lineof[c[j]] = key[j] - 1;
-                }
-            if (tid == 0) nl = n;
-            __syncthreads();
-        }
-        const uint32_t nlines = nl;
-        // 3. rounds of kHLines lines: gather, raise, store back the changed ones
-        for (uint32_t r0 = 0; r0 < nlines || r0 == 0; r0 += kHLines) {
-            const uint32_t rn = nlines - r0 < kHLines ? nlines - r0 : kHLines;
-            for (uint32_t j = tid; j < rn * 8; j += kHeBlock) {  // 8 lanes x 16 B per line
-                const uint32_t li = j / 8, part = j % 8;
-                const uint4 v = *reinterpret_cast<const uint4 *>(A.regs + size_t(lineof[r0 + li]) * 128 + part * 16);
-                *reinterpret_cast<uint4 *>(&lines[li * 32 + part * 4]) = v;
-            }
-            for (uint32_t j = tid; j < kHLines; j += kHeBlock) dirty[j] = 0;
-            __syncthreads();
-            visit([&](uint2 r) {
-                const uint32_t reg = r.y & 127u, rank = r.y >> 8;
-                uint32_t sl = hl_slot(hline_mix(r.x));
-                uint32_t at = 0xffffffffu;
-                for (uint32_t probe = 0; probe < kHTab; probe++) {
-                    const uint32_t k = key[sl];
-                    if (k == r.x + 1) {
-                        at = idx[sl];
-                        break;
+            const uint32_t nrec = block_excl_scan(rpre, nq + 1, tmp);
+            for (uint32_t w0 = 0; w0 < nrec; w0 += kHeRec) {
+                uint2 r[kHeR];
+#pragma unroll
+                for (uint32_t j = 0; j < kHeR; j++) {
+                    const uint32_t p = w0 + j * kHeBlock + tid;
+                    r[j] = make_uint2(0xffffffffu, 0);
+                    if (p < nrec) {
+                        const uint32_t k = lds_last_le(rpre, nq, p);
+                        r[j] = r2[rbase[k] + (p - rpre[k])];
                     }
-                    if (k == 0) break;
-                    sl = (sl + 1) & (kHTab - 1);
                 }
-                if (at == 0xffffffffu) {  // not in the table: CAS on the slab, first round only
-                    if (r0 == 0) {
-                        uint32_t *w = reinterpret_cast<uint32_t *>(A.regs + size_t(r.x) * 128 + (reg & ~3u));
-                        part_reg_max(w, (reg & 3) * 8, rank, *w);
+                for (uint32_t j = tid; j < kHTab; j += kHeBlock) key[j] = 0;
+                __syncthreads();
+                // 1. distinct lines into the table (linear probing; a full
+                //    table leaves the line out: its records take the CAS path)
+#pragma unroll
+                for (uint32_t j = 0; j < kHeR; j++) {
+                    if (r[j].x == 0xffffffffu) continue;
+                    uint32_t sl = hl_slot(hline_mix(r[j].x));
+                    for (uint32_t probe = 0; probe < kHProbe; probe++) {
+                        const uint32_t prev = atomicCAS(&key[sl], 0u, r[j].x + 1);
+                        if (prev == 0 || prev == r[j].x + 1) break;
+                        sl = (sl + 1) & (kHTab - 1);
                     }
-                    return;
                 }
-                if (at < r0 || at >= r0 + rn) return;
-                bool raised = false;
-                lds_byte_max(&lines[(at - r0) * 32 + reg / 4], (reg & 3) * 8, rank, &raised);
-                if (raised) dirty[at - r0] = 1;
-            });
-            __syncthreads();
-            for (uint32_t j = tid; j < rn * 8; j += kHeBlock) {
-                const uint32_t li = j / 8, part = j % 8;
-                if (dirty[li])
-                    *reinterpret_cast<uint4 *>(A.regs + size_t(lineof[r0 + li]) * 128 + part * 16) =
-                        *reinterpret_cast<const uint4 *>(&lines[li * 32 + part * 4]);
+                __syncthreads();
+                // 2. compact indices of the occupied entries
+                {
+                    uint32_t *cidx = lines;  // scratch: kHTab words
+                    for (uint32_t j = tid; j < kHTab; j += kHeBlock) cidx[j] = key[j] != 0;
+                    __syncthreads();
+                    const uint32_t n = block_excl_scan(cidx, kHTab, tmp);
+                    for (uint32_t j = tid; j < kHTab; j += kHeBlock)
+                        if (key[j]) idx[j] = uint16_t(cidx[j]);
+                    if (tid == 0) nl = n;
+                    __syncthreads();
+                }
+                const uint32_t nlines = nl;
+                // each record's compact line index (or none)
+                uint32_t at[kHeR];
+#pragma unroll
+                for (uint32_t j = 0; j < kHeR; j++) {
+                    at[j] = 0xffffffffu;
+                    if (r[j].x == 0xffffffffu) continue;
+                    uint32_t sl = hl_slot(hline_mix(r[j].x));
+                    for (uint32_t probe = 0; probe < kHProbe; probe++) {
+                        const uint32_t k = key[sl];
+                        if (k == r[j].x + 1) {
+                            at[j] = idx[sl];
+                            break;
+                        }
+                        if (k == 0) break;
+                        sl = (sl + 1) & (kHTab - 1);
+                    }
+                    if (at[j] == 0xffffffffu) {  // not in the table: CAS on the slab
+                        const uint32_t reg = r[j].y & 127u;
+                        uint32_t *w = reinterpret_cast<uint32_t *>(A.regs + size_t(r[j].x) * 128 + (reg & ~3u));
+                        part_reg_max(w, (reg & 3) * 8, r[j].y >> 8,
+                                     __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    }
+                }
+                // 3. rounds of kHLines lines: the round's line list, the
+                //    lines gathered 8 lanes x 16 B each, byte maxes in LDS,
+                //    the changed lines stored back whole (plain loads: a line
+                //    stored by this block for an earlier window is seen after
+                //    the barrier, no other block owns it)
+                for (uint32_t r0 = 0; r0 < nlines; r0 += kHLines) {
+                    const uint32_t rn = nlines - r0 < kHLines ? nlines - r0 : kHLines;
+                    for (uint32_t j = tid; j < kHTab; j += kHeBlock) {
+                        const uint32_t k = key[j];
+                        if (k && idx[j] >= r0 && idx[j] < r0 + rn) lof[idx[j] - r0] = k - 1;
+                    }
+                    for (uint32_t j = tid; j < rn; j += kHeBlock) dirty[j] = 0;
+                    __syncthreads();
+                    const uint4 *src = reinterpret_cast<const uint4 *>(A.regs);
+                    for (uint32_t j = tid; j < rn * 8; j += kHeBlock)
+                        *reinterpret_cast<uint4 *>(&lines[j * 4]) = src[size_t(lof[j / 8]) * 8 + (j % 8)];
+                    __syncthreads();
+#pragma unroll
+                    for (uint32_t j = 0; j < kHeR; j++) {
+                        if (at[j] < r0 || at[j] >= r0 + rn) continue;
+                        const uint32_t reg = r[j].y & 127u;
+                        bool raised = false;
+                        lds_byte_max(&lines[(at[j] - r0) * 32 + reg / 4], (reg & 3) * 8, r[j].y >> 8, &raised);
+                        if (raised) dirty[at[j] - r0] = 1;
+                    }
+                    __syncthreads();
+                    uint4 *dst = reinterpret_cast<uint4 *>(A.regs);
+                    for (uint32_t j = tid; j < rn * 8; j += kHeBlock)
+                        if (dirty[j / 8])
+                            dst[size_t(lof[j / 8]) * 8 + (j % 8)] = *reinterpret_cast<const uint4 *>(&lines[j * 4]);
+                    __syncthreads();
+                }
             }
-            __syncthreads();
-            if (nlines == 0) break;
         }
     }
 }
@@ -818,6 +897,8 @@ static hipError_t hll_scratch(HllArgs *H, uint32_t m, Scratch *scr) {
     if (e == hipSuccess) H->p1 = (uint32_t *)scratch_get(scr, 34, size_t(kH1) * H->o_stride * 4, &e);
     if (e == hipSuccess) H->r2 = (uint32_t *)scratch_get(scr, 35, size_t(H->maxchunks) * kHChunk * 8, &e);
     if (e == hipSuccess) H->o2 = (uint32_t *)scratch_get(scr, 36, size_t(H->maxchunks) * (kH2 + 1) * 4, &e);
+    H->c_stride = (m + kHChunk - 1) / kHChunk + 2;
+    if (e == hipSuccess) H->cst = (uint32_t *)scratch_get(scr, 37, size_t(kH1) * H->c_stride * 4, &e);
     return e;
 }
 
@@ -897,7 +978,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const uint8_t *bytes, const ui
             hipLaunchKernelGGL(k_part_c2, dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(kPaBlock), 0,
                                st, A, H);
             hipLaunchKernelGGL(k_part_hscan, dim3(kH1), dim3(1024), 0, st, H);
-            hipLaunchKernelGGL(k_part_hd, dim3(unsigned(cus)), dim3(1024), 0, st, H);
+            hipLaunchKernelGGL(k_part_hd, dim3(unsigned(cus) * 2), dim3(1024), 0, st, H);
             hipLaunchKernelGGL(k_part_he, dim3(unsigned(cus) * 2), dim3(kHeBlock), 0, st, A, H);
         } else {
             const unsigned gc = (part_grid(ms, kPcBlock * 2, cus * 8) + kPGroups - 1) / kPGroups * kPGroups;
