@@ -85,6 +85,7 @@ struct ske_ctx {
     bool k1_ok = false;       // short-id LDS K1 (sketch_k1.hip) usable
     int k1_legacy = 0;        // 1: always the generic LDS kernel (A/B diagnostics)
     int k1_grid = 0;          // blocks of the short-id LDS K1 (0: one per CU)
+    int k1_persistent = 1;    // ske_swipes_many_async: one LDS K1 launch over all batches
     uint8_t *zero16 = nullptr;  // 16 zero bytes on the device
     // the XCD-partitioned K1 keeps per-launch state in the context scratch:
     // a launch on another stream first waits for the previous one
@@ -704,6 +705,11 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
         c->k1_grid = int(value);
         return SKE_OK;
     }
+    if (!strcmp(name, "k1_persistent")) {  // 0: many-batch calls launch K1 per batch
+        if (value < 0 || value > 1) return SKE_EINVAL;
+        c->k1_persistent = int(value);
+        return SKE_OK;
+    }
     if (!strcmp(name, "k1_legacy")) {
         if (value < 0 || value > 1) return SKE_EINVAL;
         c->k1_legacy = int(value);
@@ -1137,6 +1143,26 @@ static int swipes_many_body(ske_ctx *c, const ChainDev &ch, const ske_swipe_batc
     return rc;
 }
 
+static int swipes_many_persistent(ske_ctx *c, const K1Args &A, const ske_swipe_batch *b, uint32_t nb) {
+    const uint32_t T = k1_many_tile(c->pb);
+    for (uint32_t j0 = 0; j0 < nb; j0 += kK1ManyMax) {
+        K1Many M{};
+        M.nb = nb - j0 < kK1ManyMax ? nb - j0 : kK1ManyMax;
+        M.tpre[0] = 0;
+        for (uint32_t j = 0; j < M.nb; j++) {
+            const ske_swipe_batch &B = b[j0 + j];
+            M.b[j] = K1Batch{B.bytes, B.width ? nullptr : B.offs, B.slot, B.out_valid, uint32_t(B.n), B.width};
+            const uint64_t tp = M.tpre[j] + (B.n + T - 1) / T;
+            if (tp >= (uint64_t(1) << 31)) return SKE_EINVAL;
+            M.tpre[j + 1] = uint32_t(tp);
+        }
+        const PassMark m = mark_begin(c, 0);
+        HIPCHK(c, launch_swipes_lds_many(A, M, c->pb, c->k1_grid ? c->k1_grid : c->cus, c->st));
+        mark_end(c, m);
+    }
+    return SKE_OK;
+}
+
 int ske_swipes_many_async(ske_ctx *c, uint32_t fid, const ske_swipe_batch *b, uint32_t nb,
                           uint32_t branches) {
     if (!c || (nb && !b) || branches > SKE_MANY_MAX_BRANCHES) return SKE_EINVAL;
@@ -1144,6 +1170,18 @@ int ske_swipes_many_async(ske_ctx *c, uint32_t fid, const ske_swipe_batch *b, ui
     if (!F) return SKE_EINVAL;
     for (uint32_t j = 0; j < nb; j++)
         if (!b[j].slot || (b[j].width == 0 && !b[j].offs) || b[j].width > 4096) return SKE_EINVAL;
+    static const ChainDev empty{};
+    const ChainDev &ch = F->exists ? cached_chain(*F) : empty;
+    // the short-id LDS K1: one persistent launch per kK1ManyMax batches, the
+    // branches unused
+    if (nb && c->k1_persistent) {
+        K1Args A;
+        bool ok = true;
+        for (uint32_t j = 0; j < nb && ok; j++)
+            ok = k1_fast_args(c, ch, b[j].bytes, b[j].width ? nullptr : b[j].offs, b[j].width, b[j].slot,
+                              b[j].n, b[j].out_valid, &A);
+        if (ok) return swipes_many_persistent(c, A, b, nb);
+    }
     uint32_t br = branches ? branches : SKE_MANY_DEFAULT_BRANCHES;
     if (nb && br > nb) br = nb;
     if (br > 1) {  // with nb == 0: only prepares the side streams (e.g. before capture)
@@ -1155,8 +1193,6 @@ int ske_swipes_many_async(ske_ctx *c, uint32_t fid, const ske_swipe_batch *b, ui
         }
     }
     if (nb == 0) return SKE_OK;
-    static const ChainDev empty{};
-    const ChainDev &ch = F->exists ? cached_chain(*F) : empty;
     // the scratch of the largest batch before the first launch: batches of
     // different sizes never reallocate it between recorded launches
     uint64_t nmax = 0;

@@ -60,6 +60,25 @@ struct K1Args {
     K1Link link[kK1MaxLinks];
 };
 
+// ske_swipes_many_async through the short-id LDS K1: one persistent launch over
+// up to kK1ManyMax batches (passed by value: the kernel arguments are captured
+// with a graph), tpre[j] = tiles of the batches before j
+constexpr uint32_t kK1ManyMax = 48;
+struct K1Batch {
+    const uint8_t *bytes;
+    const uint32_t *offs;  // nullptr: fixed-width ids
+    const uint32_t *slot;
+    uint8_t *out;          // may be nullptr
+    uint32_t n, fixed_w;
+};
+struct K1Many {
+    K1Batch b[kK1ManyMax];
+    uint32_t tpre[kK1ManyMax + 1];
+    uint32_t nb;
+};
+uint32_t k1_many_tile(int tile);  // swipes per tile of the many kernel
+hipError_t launch_swipes_lds_many(const K1Args &A, const K1Many &M, int tile, int cus, hipStream_t st);
+
 // fills A's chain fields; false when the chain does not fit this variant
 bool k1_lds_plan(const ChainDev &ch, K1Args *A);
 hipError_t launch_swipes_lds(const K1Args &A, bool hll, int tile, int cus, hipStream_t st);

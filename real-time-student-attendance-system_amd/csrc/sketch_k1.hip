@@ -160,32 +160,51 @@ struct K1Pend {  // a committed tile's register CASes, settled one tile later
     bool on[U];
 };
 
-struct K1Rsrc {
+// One batch as the tile loop sees it: 32-bit offsets into its buffers
+// (u32 offsets keep the ids below 4 GiB) and its answer array.
+struct K1View {
     __amdgpu_buffer_rsrc_t offs, slot, bytes;
+    const uint8_t *bytes_p;
+    const uint32_t *offs_p;  // nullptr: fixed-width ids
+    uint8_t *out;            // may be nullptr
+    uint32_t n, fixed_w;
 };
 
+__device__ __forceinline__ K1View k1_view(const uint8_t *bytes, const uint32_t *offs, const uint32_t *slot,
+                                          uint8_t *out, uint32_t n, uint32_t fixed_w) {
+    K1View V;
+    V.offs = k1_rsrc(offs, 0xfffffff0u);
+    V.slot = k1_rsrc(slot, 0xfffffff0u);
+    V.bytes = k1_rsrc(bytes, 0xfffffff0u);
+    V.bytes_p = bytes;
+    V.offs_p = offs;
+    V.out = out;
+    V.n = n;
+    V.fixed_w = fixed_w;
+    return V;
+}
+
 template <bool kHll, int U>
-__device__ __forceinline__ void k1_issue_a(const K1Args &A, const K1Rsrc &R, uint32_t base,
-                                           uint32_t c1, K1In<U> &in) {
+__device__ __forceinline__ void k1_issue_a(const K1View &V, uint32_t base, uint32_t c1, K1In<U> &in) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const uint32_t i = base + uint32_t(u) * kK1Block + threadIdx.x;
         in.act[u] = i < c1;
         in.idx[u] = i;
-        const uint32_t ic = in.act[u] ? i : A.n - 1;  // clamped: every load stays in bounds
-        if (A.offs) {
-            in.b[u] = __builtin_amdgcn_raw_buffer_load_b32(R.offs, ic * 4, 0, 0);
-            in.e[u] = __builtin_amdgcn_raw_buffer_load_b32(R.offs, ic * 4 + 4, 0, 0);
+        const uint32_t ic = in.act[u] ? i : V.n - 1;  // clamped: every load stays in bounds
+        if (V.offs_p) {
+            in.b[u] = __builtin_amdgcn_raw_buffer_load_b32(V.offs, ic * 4, 0, 0);
+            in.e[u] = __builtin_amdgcn_raw_buffer_load_b32(V.offs, ic * 4 + 4, 0, 0);
         } else {
-            in.b[u] = ic * A.fixed_w;
-            in.e[u] = in.b[u] + A.fixed_w;
+            in.b[u] = ic * V.fixed_w;
+            in.e[u] = in.b[u] + V.fixed_w;
         }
-        in.sl[u] = kHll ? __builtin_amdgcn_raw_buffer_load_b32(R.slot, ic * 4, 0, 0) : 0u;
+        in.sl[u] = kHll ? __builtin_amdgcn_raw_buffer_load_b32(V.slot, ic * 4, 0, 0) : 0u;
     }
 }
 
 template <int U>
-__device__ __forceinline__ void k1_issue_b(const K1Rsrc &R, K1In<U> &in) {
+__device__ __forceinline__ void k1_issue_b(const K1View &R, K1In<U> &in) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
         // an empty id reads past the range (zero); a second word only when the
@@ -201,7 +220,7 @@ __device__ __forceinline__ void k1_issue_b(const K1Rsrc &R, K1In<U> &in) {
 // hashes (a = H(x, bloom seed), b = H(x, a), h = H(x, hll seed)), the HLL
 // register and rank with its pre-check load, and the newest link's walk
 template <bool kHll, int U>
-__device__ __forceinline__ void k1_hash(const K1Args &A, const K1In<U> &in, K1Hot<U> &h) {
+__device__ __forceinline__ void k1_hash(const K1Args &A, const K1View &V, const K1In<U> &in, K1Hot<U> &h) {
     uint32_t len[U];
     uint64_t hh[U];
     bool long_ids = false;
@@ -216,9 +235,9 @@ __device__ __forceinline__ void k1_hash(const K1Args &A, const K1In<U> &in, K1Ho
     if (__any(long_ids)) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t i = in.act[u] ? in.idx[u] : A.n - 1;
-            const uint32_t b = A.offs ? A.offs[i] : i * A.fixed_w;
-            const Item it = load_item(A.bytes, b, b + len[u]);
+            const uint32_t i = in.act[u] ? in.idx[u] : V.n - 1;
+            const uint32_t b = V.offs_p ? V.offs_p[i] : i * V.fixed_w;
+            const Item it = load_item(V.bytes_p, b, b + len[u]);
             h.ha[u] = murmur_item(it, kBloomSeed);
             h.hb[u] = murmur_item(it, h.ha[u]);
             hh[u] = kHll ? murmur_item(it, kHllSeed) : 0;
@@ -317,8 +336,8 @@ __device__ __forceinline__ void k1_probe(const K1Args &A, const lds_u8 *img, K1H
 // The pre-check may be stale, never too high (registers only grow): a stale
 // word makes the CAS fail, and k1_settle finishes the byte max in a loop.
 template <bool kHll, int U>
-__device__ __forceinline__ void k1_commit(const K1Args &A, const K1Hot<U> &h, const uint32_t *valid,
-                                          K1Pend<U> &pd) {
+__device__ __forceinline__ void k1_commit(const K1Args &A, const K1View &V, const K1Hot<U> &h,
+                                          const uint32_t *valid, K1Pend<U> &pd) {
     if constexpr (kHll) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -336,8 +355,8 @@ __device__ __forceinline__ void k1_commit(const K1Args &A, const K1Hot<U> &h, co
                                        (h.cur[u] & ~(0xffu << h.sh[u])) | (h.rank[u] << h.sh[u]));
         }
     }
-    if (A.out) {
-        const __amdgpu_buffer_rsrc_t r_out = k1_rsrc(A.out, A.n);
+    if (V.out) {
+        const __amdgpu_buffer_rsrc_t r_out = k1_rsrc(V.out, V.n);
 #pragma unroll
         for (int u = 0; u < U; u++)  // lanes past the chunk store out of range (dropped)
             __builtin_amdgcn_raw_buffer_store_b8(uint8_t(valid[u]), r_out, h.act[u] ? h.idx[u] : 0xffffffffu,
@@ -377,11 +396,7 @@ __global__ void __launch_bounds__(kK1Block) k_swipes_lds(const K1Args A) {
     const uint32_t per_block = (A.n + gridDim.x - 1) / gridDim.x;
     const uint32_t c0 = blockIdx.x * per_block;
     const uint32_t c1 = c0 + per_block < A.n ? c0 + per_block : A.n;
-    // 32-bit offsets into the batch buffers (u32 offsets keep the ids below 4 GiB)
-    K1Rsrc R;
-    R.offs = k1_rsrc(A.offs, 0xfffffff0u);
-    R.slot = k1_rsrc(A.slot, 0xfffffff0u);
-    R.bytes = k1_rsrc(A.bytes, 0xfffffff0u);
+    const K1View V = k1_view(A.bytes, A.offs, A.slot, A.out, A.n, A.fixed_w);
     K1In<U> in;
     K1Hot<U> hot;
     K1_STAMP(0);
@@ -392,13 +407,13 @@ __global__ void __launch_bounds__(kK1Block) k_swipes_lds(const K1Args A) {
     const K1Link &L0 = A.link[A.nlinks - 1];  // the newest link: LDS offset 0
     const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(L0.bf), 0, int(L0.nbytes16), 0x00020000);
-    k1_issue_a<kHll, U>(A, R, c0, c1, in);
+    k1_issue_a<kHll, U>(V, c0, c1, in);
     __builtin_amdgcn_sched_barrier(0);
     k1_stage<P>(A, img, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x & 63, r0);
     __builtin_amdgcn_sched_barrier(0);
-    k1_issue_b<U>(R, in);  // waits for the offsets only (vmcnt(P): the copy is younger)
+    k1_issue_b<U>(V, in);  // waits for the offsets only (vmcnt(P): the copy is younger)
     K1_STAMP(1);
-    k1_hash<kHll, U>(A, in, hot);
+    k1_hash<kHll, U>(A, V, in, hot);
     K1_STAMP(2);
     __syncthreads();  // the image has landed
     K1_STAMP(3);
@@ -409,21 +424,87 @@ __global__ void __launch_bounds__(kK1Block) k_swipes_lds(const K1Args A) {
     for (uint32_t base = c0;; it++) {
         const uint32_t next = base + kK1Block * U;
         const bool more = next < c1;  // block-uniform
-        k1_issue_a<kHll, U>(A, R, next, c1, in);
+        k1_issue_a<kHll, U>(V, next, c1, in);
         uint32_t valid[U];
         k1_probe<U>(A, img, hot, valid);
         K1_STAMP(4 + 3 * it);
-        k1_issue_b<U>(R, in);
+        k1_issue_b<U>(V, in);
         k1_settle<kHll, U>(pend);  // the previous tile's CASes (landed during this tile)
-        k1_commit<kHll, U>(A, hot, valid, pend);
+        k1_commit<kHll, U>(A, V, hot, valid, pend);
         K1_STAMP(5 + 3 * it);
         if (!more) break;
-        k1_hash<kHll, U>(A, in, hot);
+        k1_hash<kHll, U>(A, V, in, hot);
         K1_STAMP(6 + 3 * it);
         base = next;
     }
     k1_settle<kHll, U>(pend);
     K1_STAMP(15);
+}
+
+// Many batches in one launch (ske_swipes_many_async): the batches are cut into
+// tiles of 1024*U swipes (a batch's last tile is partial; no tile spans two
+// batches), the concatenated tile list is dealt to the blocks in contiguous
+// equal shares, and each block stages the LDS image once and runs the same
+// pipelined tile loop across its share, switching batch views (wave-uniform,
+// from the kernel arguments) at batch boundaries.  One launch per call: the
+// per-launch fixed cost -- the image copy, the first tile's loads, the grid
+// ramp and drain -- is paid once for all the call's batches.
+template <bool kHll, int U, int P>
+__global__ void __launch_bounds__(kK1Block) k_swipes_lds_many(const K1Args A, const K1Many M) {
+    __shared__ __attribute__((aligned(16))) uint8_t img_[kLdsBloomMaxBytes];
+    lds_u8 *img = (lds_u8 *)img_;
+    constexpr uint32_t T = kK1Block * U;
+    const uint32_t ntiles = M.tpre[M.nb];
+    uint32_t t = uint32_t(uint64_t(ntiles) * blockIdx.x / gridDim.x);
+    const uint32_t tend = uint32_t(uint64_t(ntiles) * (blockIdx.x + 1) / gridDim.x);
+    // batch of tile t (the block's tiles only move forward)
+    uint32_t j = 0;
+    while (j + 1 < M.nb && t >= M.tpre[j + 1]) j++;
+    auto view = [&](uint32_t jj) {
+        const K1Batch &B = M.b[jj];
+        return k1_view(B.bytes, B.offs, B.slot, B.out, B.n, B.fixed_w);
+    };
+    K1View Vn = view(j);
+    K1In<U> in;
+    K1Hot<U> hot;
+    const K1Link &L0 = A.link[A.nlinks - 1];
+    const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(L0.bf), 0, int(L0.nbytes16), 0x00020000);
+    const bool any = t < tend;  // block-uniform
+    if (any) k1_issue_a<kHll, U>(Vn, (t - M.tpre[j]) * T, Vn.n, in);
+    __builtin_amdgcn_sched_barrier(0);
+    k1_stage<P>(A, img, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x & 63, r0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (any) {
+        k1_issue_b<U>(Vn, in);
+        k1_hash<kHll, U>(A, Vn, in, hot);
+    }
+    __syncthreads();  // the image has landed
+    if (!any) return;
+    K1Pend<U> pend;
+#pragma unroll
+    for (int u = 0; u < U; u++) pend.on[u] = false;
+    K1View Vh = Vn;
+    for (;;) {
+        const bool more = t + 1 < tend;  // block-uniform
+        if (more) {
+            t++;
+            if (t >= M.tpre[j + 1]) {
+                while (t >= M.tpre[j + 1]) j++;  // (skips empty batches)
+                Vn = view(j);
+            }
+            k1_issue_a<kHll, U>(Vn, (t - M.tpre[j]) * T, Vn.n, in);
+        }
+        uint32_t valid[U];
+        k1_probe<U>(A, img, hot, valid);
+        if (more) k1_issue_b<U>(Vn, in);
+        k1_settle<kHll, U>(pend);
+        k1_commit<kHll, U>(A, Vh, hot, valid, pend);
+        if (!more) break;
+        k1_hash<kHll, U>(A, Vn, in, hot);
+        Vh = Vn;
+    }
+    k1_settle<kHll, U>(pend);
 }
 
 // ---------------------------------------------------------------------------
@@ -481,6 +562,33 @@ hipError_t launch_swipes_lds(const K1Args &A, bool hll, int tile, int cus, hipSt
     if (U == 4) return k1_launch_p<false, 4>(A, grid, st);
     if (U == 2) return k1_launch_p<false, 2>(A, grid, st);
     return k1_launch_p<false, 1>(A, grid, st);
+}
+
+template <bool kHll, int U>
+static hipError_t k1_launch_many_p(const K1Args &A, const K1Many &M, unsigned grid, hipStream_t st) {
+    const int P = int((A.npieces + kK1Waves - 1) / kK1Waves);
+#define SKE_P(PP)                                                                                   \
+    case PP:                                                                                        \
+        hipLaunchKernelGGL((k_swipes_lds_many<kHll, U, PP>), dim3(grid), dim3(kK1Block), 0, st, A, M); \
+        break;
+    switch (P) {
+        SKE_P(1) SKE_P(2) SKE_P(3) SKE_P(4) SKE_P(5) SKE_P(6) SKE_P(7) SKE_P(8) SKE_P(9) SKE_P(10)
+    default: return hipErrorInvalidValue;
+    }
+#undef SKE_P
+    return hipGetLastError();
+}
+
+uint32_t k1_many_tile(int tile) { return kK1Block * uint32_t(tile >= 4 ? 4 : (tile >= 2 ? 2 : 1)); }
+
+hipError_t launch_swipes_lds_many(const K1Args &A, const K1Many &M, int tile, int cus, hipStream_t st) {
+    if (M.nb == 0 || M.tpre[M.nb] == 0) return hipSuccess;
+    const int U = tile >= 4 ? 4 : (tile >= 2 ? 2 : 1);
+    const uint32_t nt = M.tpre[M.nb];
+    const unsigned grid = unsigned(nt < uint32_t(cus) ? nt : uint32_t(cus));
+    if (U == 4) return k1_launch_many_p<true, 4>(A, M, grid, st);
+    if (U == 2) return k1_launch_many_p<true, 2>(A, M, grid, st);
+    return k1_launch_many_p<true, 1>(A, M, grid, st);
 }
 
 hipError_t k1_lds_setup() { return hipSuccess; }  // static LDS: nothing to raise

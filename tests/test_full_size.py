@@ -103,13 +103,15 @@ def test_c3_gpu_shard_full_step(engine, orc, variant):
 
 
 @pytest.mark.parametrize("mode,branches", [("capture_branched", 4), ("native", 4),
-                                           ("native-graph", 16), ("native-graph-fixed", 16)])
+                                           ("native-graph", 16), ("native-graph-fixed", 16),
+                                           ("native-forked", 4), ("native-graph-forked", 16)])
 def test_c2_bench_steps_forked_graph(engine, orc, mode, branches):
-    """bench.py's timing: the steps recorded as independent branches (step j
-    on branch j mod B), so consecutive launches overlap and update the same
-    registers concurrently.  capture_branched: torch streams, full-chip grid;
-    native: ske_swipes_many_async (two launches side by side on half the
-    CUs), enqueued directly or recorded into a graph (the bench default)."""
+    """bench.py's timing.  native*: ske_swipes_many_async -- one persistent
+    LDS K1 launch over all the steps (the default), or with k1_persistent = 0
+    the steps on independent branches (step j on branch j mod B, two launches
+    side by side on half the CUs), enqueued directly or recorded into a graph.
+    capture_branched: torch streams, full-chip grid.  Concurrent launches
+    update the same registers."""
     import functools
     import torch
     from rtsas_amd import synthetic
@@ -120,6 +122,8 @@ def test_c2_bench_steps_forked_graph(engine, orc, mode, branches):
     batches = [engine.swipe_batch(p, j * n, n) for j in range(2 * branches)]
     outs = [DeviceBuffer(engine.ctx, n) for _ in batches]
     fixed = mode.endswith("fixed")
+    if mode.endswith("forked"):
+        engine.set_option("k1_persistent", 0)
     main = torch.cuda.Stream()
     engine.set_stream(main.cuda_stream)
     try:
@@ -128,7 +132,7 @@ def test_c2_bench_steps_forked_graph(engine, orc, mode, branches):
             steps = [functools.partial(engine.swipes_async, 0, b, o)
                      for b, o in zip(batches, outs)]
             g = engine.capture_branched(steps, main, side)
-        elif mode == "native":
+        elif mode in ("native", "native-forked"):
             g = None
             engine.swipes_many_async(0, batches, outs, branches=branches)
         else:
@@ -147,6 +151,60 @@ def test_c2_bench_steps_forked_graph(engine, orc, mode, branches):
     _, regs, answers, probes, nvalid = _oracle(orc, engine, w, p, batches, w.n_keys)
     for a, o in zip(answers, outs):
         assert np.array_equal(o.to_host(np.uint8, n), a)
+    assert np.array_equal(engine.registers_all(w.n_keys), regs)
+
+
+class _Slice:
+    """A batch view of the first n swipes of a DeviceBatch (n may be 0)."""
+    def __init__(self, b, n):
+        self.slot, self.bytes, self.offs, self.width, self.n = b.slot, b.bytes, b.offs, b.width, n
+
+
+@pytest.mark.parametrize("mode", ["direct", "graph", "graph-fixed"])
+def test_c2_persistent_many_ragged(engine, orc, mode):
+    """The persistent LDS K1 (one launch over the batch array): 53 batches --
+    more than one launch holds (48), so two launches -- of ragged sizes: empty,
+    1, one tile +- 1 (2048 swipes at U = 2), and up to 200k; tiles never span
+    batches and a block's share crosses many batch boundaries.  Answers and
+    registers == the oracle over the batches in order."""
+    import torch
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import DeviceBuffer
+    w = synthetic.WORKLOADS["c2"]
+    p = _setup(engine, w)
+    rng = np.random.default_rng(53)
+    sizes = [0, 1, 2047, 2048, 2049, 0, 3] + rng.integers(1, 200_000, 46).tolist()
+    full, views, start = [], [], 0
+    for n in sizes:
+        b = engine.swipe_batch(p, start, max(n, 1))
+        start += max(n, 1)
+        full.append(b)
+        views.append(_Slice(b, n))
+    outs = [DeviceBuffer(engine.ctx, max(n, 1)) for n in sizes]
+    fixed = mode.endswith("fixed")
+    main = torch.cuda.Stream()
+    engine.set_stream(main.cuda_stream)
+    try:
+        if mode == "direct":
+            engine.swipes_many_async(0, views, outs)
+        else:
+            g = engine.capture(lambda: engine.swipes_many_async(0, views, outs, fixed=fixed))
+            g.launch()
+        engine.sync()
+        if mode != "direct":
+            g.free()
+    finally:
+        engine.set_stream(None)
+    chain = orc.Chain(w.bf_capacity, w.bf_error)
+    mb = engine.members_batch(p, 0, w.n_members).to_host()
+    chain.madd_packed(mb[0], mb[1])
+    regs = np.zeros((w.n_keys, 16384), np.uint8)
+    for b, n, o in zip(full, sizes, outs):
+        if n == 0:
+            continue
+        buf, offs, slot = b.to_host()
+        v, _, _ = orc.process_swipes(chain, regs, slot[:n].astype(np.uint32), buf, offs[:n + 1])
+        assert np.array_equal(o.to_host(np.uint8, n), v)
     assert np.array_equal(engine.registers_all(w.n_keys), regs)
 
 
