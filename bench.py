@@ -46,6 +46,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # 4-byte read per lane over a 1.6 GB table -- 55 G sectors/s; the register
 # update of pass C is priced against it as well as against the HBM peak
 RANDOM_SECTOR_GPS = 55.3
+# the same tool: one random 32-bit CAS per lane over a 1.6 GB table -- 19.0 G/s
+# (device-scope atomics execute memory-side: TCC_EA0_ATOMIC); pass C's
+# register CASes are priced against it
+RANDOM_CAS_GPS = 19.0
+MALL_BYTES = 256 << 20  # Infinity Cache: a slab this small stays on chip
 METRIC = "swipes/sec (fused BF.EXISTS+PFADD) at 1/2/4/8 GPUs; % of HBM peak"
 PASS_NAMES = ["k1", "k_part_a", "k_part_b", "k_part_c"]
 
@@ -247,9 +252,11 @@ def verify(engine, orc, chain, w, rank, world, dist, dev):
             "backend": dist.get_backend() if world > 1 else "none"}
 
 
-def pass_bytes(n, nvalid, probes, width, fixed, geometry):
+def pass_bytes(n, nvalid, probes, width, fixed, geometry, lds_k1=False, slab_bytes=0, cus=256):
     """Algorithmic bytes per launch of each K1 kernel: streams
-    at their size, every random access at one 64-B HBM sector."""
+    at their size, every random access at one 64-B HBM sector.  The LDS K1
+    (lds_k1) reads the filter once per block (staged into LDS, probes cost no
+    HBM) and its register words only when the slab does not fit on chip."""
     s_off = 0 if fixed else 4
     ksum = sum(k for _, k in geometry)
     nslices = sum(-(-bits // (1 << 19)) for bits, _ in geometry)
@@ -259,7 +266,9 @@ def pass_bytes(n, nvalid, probes, width, fixed, geometry):
     return {
         # one kernel: ids + offsets + slot + answer streamed, one sector per
         # RedisBloom probe, one sector read + one written per valid swipe
-        "k1": n * (width + s_off + 4 + 1) + 64 * probes + 128 * nvalid,
+        "k1": (n * (width + s_off + 4 + 1) + filter_bytes * cus
+               + (128 * nvalid if slab_bytes > MALL_BYTES else 0)) if lds_k1 else
+              n * (width + s_off + 4 + 1) + 64 * probes + 128 * nvalid,
         # ids + offsets in; probe records, run table, HLL word, fail byte out
         "k_part_a": n * (width + s_off) + rec + 4 * (nslices + 1) * ntiles + 4 * n + n * len(geometry),
         # probe records + their run boundaries in, the filter staged once
@@ -406,7 +415,9 @@ def main():
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * n * args.steps / elapsed
-    alg = pass_bytes(n, nvalid, probes, width, fixed, chain_geometry(engine))
+    cus = torch.cuda.get_device_properties(local).multi_processor_count
+    alg = pass_bytes(n, nvalid, probes, width, fixed, chain_geometry(engine), lds_k1=lds_k1,
+                     slab_bytes=(w.n_keys + 64) * 16384, cus=cus)
     passes = {}
     for i, (ms, cnt) in enumerate(pt):
         if cnt:
@@ -424,11 +435,14 @@ def main():
     achieved = dom_bytes / (kern_ms * 1e-3) / 1e9
     # HBM-side bytes per launch of that kernel from the committed rocprofv3 PMC
     # passes of this workload (FETCH_SIZE + WRITE_SIZE, separate passes), or null
-    traffic, traffic_src = None, None
+    traffic, traffic_src, pmc = None, None, None
     pmc_path = os.path.join(ROOT, "profiles", f"r02_pmc_{args.config}_{dom}.json")
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
-            traffic = json.load(f).get("hbm_bytes_per_dispatch")
+            pmc = json.load(f)
+        traffic = pmc.get("hbm_bytes_per_dispatch")
+        if traffic is not None and persistent and dom == "k1":
+            traffic *= args.steps / passes["k1"]["launches"] / pmc.get("steps_per_dispatch", args.steps)
         traffic_src = os.path.relpath(pmc_path, ROOT)
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
@@ -442,6 +456,25 @@ def main():
                     "4-B read rate over a 1.6 GB table (tools/randbench.hip)",
             "achieved_Gsectors_per_s": sectors, "peak_Gsectors_per_s": RANDOM_SECTOR_GPS,
             "frac": sectors / RANDOM_SECTOR_GPS}
+        if pmc and "TCC_EA0_ATOMIC_sum" in pmc.get("mean", {}):
+            cas = pmc["mean"]["TCC_EA0_ATOMIC_sum"] / (kern_ms * 1e-3) / 1e9
+            roofline["binding"] = {
+                "counter": "TCC_EA0_ATOMIC_sum",
+                "what": "register CASes (memory-side device atomics, PMC per dispatch) / this run's "
+                        "kernel time, against the measured random CAS rate over a 1.6 GB table",
+                "atomics_per_dispatch": pmc["mean"]["TCC_EA0_ATOMIC_sum"],
+                "achieved_G_per_s": cas, "peak_G_per_s": RANDOM_CAS_GPS, "frac": cas / RANDOM_CAS_GPS}
+    if dom == "k1" and pmc and "SQ_INSTS_VALU" in pmc.get("mean", {}):
+        m = pmc["mean"]
+        roofline["binding"] = {
+            "counter": "SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_VALU",
+            "what": "the LDS K1 is issue/latency bound, not HBM bound: per wave, the share of its "
+                    "cycles waiting in s_waitcnt and issuing VALU (PMC of this workload's dispatch)",
+            "wait_frac": m["SQ_WAIT_INST_ANY"] / m["SQ_WAVE_CYCLES"],
+            "valu_frac": m["SQ_ACTIVE_INST_VALU"] / m["SQ_WAVE_CYCLES"],
+            "valu_wave_insts_per_64_swipes":
+                m["SQ_INSTS_VALU"] / max(1.0, pmc.get("swipes_per_dispatch", 0) / 64),
+            "lds_bank_conflict_rate": pmc.get("lds_bank_conflict_rate")}
     line = {
         "metric": METRIC,
         "value": value,
