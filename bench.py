@@ -75,6 +75,9 @@ def parse():
     ap.add_argument("--hll-mode", type=int, default=-1,
                     help="partitioned K1 PFADD: 0 = CAS on the slab, 1 = owned register lines "
                          "(-1: library default)")
+    ap.add_argument("--pb-pairs", type=int, default=-1,
+                    help="partitioned K1 pass B: 1 = slice pairs (128 KiB images), 0 = single "
+                         "slices (-1: library default)")
     ap.add_argument("--persistent", type=int, default=-1,
                     help="1 = the K timed steps as ONE ske_swipes_many_async call (one persistent "
                          "LDS K1 launch over the K batches; default for the LDS K1); 0 = a K1 "
@@ -317,6 +320,8 @@ def main():
         engine.set_option("variant", args.variant)
     if args.hll_mode >= 0:
         engine.set_option("hll_mode", args.hll_mode)
+    if args.pb_pairs >= 0:
+        engine.set_option("pb_pairs", args.pb_pairs)
 
     # Bloom preload (replicated on every rank), this rank's HLL key shard, and
     # 64 spare slots for the verification batch

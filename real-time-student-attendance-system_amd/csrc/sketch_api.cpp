@@ -81,6 +81,7 @@ struct ske_ctx {
     int xr_finish_u = 1;  //   and in the finish pass
     uint32_t part_sub = 0;  // partitioned K1: swipes per sub-batch (0: default)
     int hll_mode = 0;       // partitioned K1's PFADD: 1 owned register lines, 0 CAS
+    int pb_pairs = 1;       // partitioned K1 pass B over slice pairs (one-link chains)
     bool lds_ok = false;
     bool k1_ok = false;       // short-id LDS K1 (sketch_k1.hip) usable
     int k1_legacy = 0;        // 1: always the generic LDS kernel (A/B diagnostics)
@@ -472,7 +473,7 @@ int launch_k1(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32
         };
         c->hook_arg = pm;
         HIPCHK(c, launch_swipes_part(ch, bytes, offs, fixed_w, slot, n, c->regs, c->nslots, out,
-                                     c->scratch, c->err, c->cus, c->part_sub, c->hll_mode, c->st,
+                                     c->scratch, c->err, c->cus, c->part_sub, c->hll_mode, c->pb_pairs, c->st,
                                      c->timing && !c->capturing ? +hook : nullptr, c));
         return scratch_user_end(c, cid);
     }
@@ -688,6 +689,11 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
     if (!strcmp(name, "hll_mode")) {  // partitioned K1's PFADD: 1 owned lines, 0 CAS
         if (value < 0 || value > 1) return SKE_EINVAL;
         c->hll_mode = int(value);
+        return SKE_OK;
+    }
+    if (!strcmp(name, "pb_pairs")) {  // partitioned K1: pass B over slice pairs (1) or slices
+        if (value < 0 || value > 1) return SKE_EINVAL;
+        c->pb_pairs = int(value);
         return SKE_OK;
     }
     if (!strcmp(name, "part_sub")) {  // partitioned K1 sub-batch (swipes; 0 = default)

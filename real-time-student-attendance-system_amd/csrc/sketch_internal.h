@@ -135,7 +135,7 @@ typedef void (*PassHook)(void *user, int pass, int end);
 hipError_t launch_swipes_part(const ChainDev &ch, const uint8_t *bytes, const uint32_t *offs,
                               uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *regs,
                               uint32_t nslots, uint8_t *out, Scratch *scr, unsigned int *err, int cus,
-                              uint32_t sub, int hll_mode, hipStream_t st, PassHook hook = nullptr,
+                              uint32_t sub, int hll_mode, int pb_pairs, hipStream_t st, PassHook hook = nullptr,
                               void *hook_user = nullptr);
 
 // sketch_order.hip -- order-exact paths (replies that depend on item order)

@@ -159,7 +159,8 @@ __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const Par
                     }
                     const uint32_t x = wk.x;
                     const uint32_t g = A.link[l].slice0 + (x >> kPSliceLog);
-                    rv[q] = (x & kPSliceMask) | (tid << kPSliceLog) | 0x80000000u;
+                    // bit 29: the slice's parity (pass B's slice pairs)
+                    rv[q] = (x & kPSliceMask) | (tid << kPSliceLog) | ((g & 1u) << 29) | 0x80000000u;
                     if (act) rp[q] = (g << 16) | atomicAdd(&scnt[g], 1u);
                     wk.step(A.link[l].d);
                     jl++;
@@ -238,14 +239,17 @@ constexpr uint32_t kOOR = 0x80000000u;  // a buffer offset past every range: loa
 // tested.
 constexpr uint32_t kPbQueue = 64;  // compacted fail stores per wave and group
 
-__global__ void __launch_bounds__(kPbBlock, 8) k_part_b(const PartArgs A) {
-    __shared__ __attribute__((aligned(16))) uint8_t img[kPSliceBytes];
+template <int SP>
+__global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const PartArgs A) {
+    constexpr uint32_t R = 2 * SP;  // 16-byte pieces per lane and run (runs of SP slices)
+    __shared__ __attribute__((aligned(16))) uint8_t img[kPSliceBytes * SP];
     __shared__ uint32_t fq[kPbBlock / 64][kPbQueue];
     // this block's share of its group's (slice, tile) space, slice major
     uint32_t gt0, gt1;
     part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
     const uint32_t gn = gt1 - gt0, nblk = gridDim.x / kPGroups, bi = blockIdx.x / kPGroups;
-    const uint32_t total = A.nslices * gn;
+    const uint32_t nunits = (A.nslices + SP - 1) / SP;
+    const uint32_t total = nunits * gn;
     uint32_t w = uint32_t(uint64_t(total) * bi / nblk);
     const uint32_t wend = uint32_t(uint64_t(total) * (bi + 1) / nblk);
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -255,75 +259,114 @@ __global__ void __launch_bounds__(kPbBlock, 8) k_part_b(const PartArgs A) {
     const __amdgpu_buffer_rsrc_t roff = part_rsrc(A.off, (A.nslices + 1) * A.off_stride * 4);
     uint32_t *q = fq[wave];
     while (w < wend) {
-        const uint32_t g = w / gn, ta = gt0 + w % gn;
+        // slices g .. g + SP - 1 (SP = 2: one link only, host-checked), so
+        // one run per tile covers them all
+        const uint32_t g = (w / gn) * SP, ta = gt0 + w % gn;
         const uint32_t tb = gt1 - ta < wend - w ? gt1 : ta + (wend - w);
+        const uint32_t ge = g + SP < A.nslices ? g + SP : A.nslices;
         w += tb - ta;
         uint32_t l = 0;
         while (l + 1 < A.nlinks && g >= A.link[l + 1].slice0) l++;
         const PartLink &L = A.link[l];
         const uint32_t b0 = (g - L.slice0) * kPSliceBytes;
-        const uint32_t nb = L.nbytes16 - b0 < kPSliceBytes ? L.nbytes16 - b0 : kPSliceBytes;
+        const uint32_t nb = L.nbytes16 - b0 < kPSliceBytes * SP ? L.nbytes16 - b0 : kPSliceBytes * SP;
         __syncthreads();  // every wave is done with the previous slice
         for (uint32_t o = threadIdx.x * 16; o < nb; o += kPbBlock * 16)
             *reinterpret_cast<uint4 *>(img + o) = *reinterpret_cast<const uint4 *>(L.bf + b0 + o);
         __syncthreads();
         const __amdgpu_buffer_rsrc_t rfail = part_rsrc(A.fail + size_t(l) * A.fail_stride, A.fail_stride);
-        const uint32_t orow = g * A.off_stride;
-        // run boundaries of tile tg + k (0, 0 past tb)
-        auto load_be = [&](uint32_t tg, uint32_t &b, uint32_t &e) {
-            const uint32_t t = tg + k;
+        const uint32_t orow = g * A.off_stride, erow = ge * A.off_stride;
+        // run boundaries of 8 rounds at once: lane L holds those of tile
+        // tg0 + (L / 8) * kStep + L % 8 (0, 0 past tb); a round's lanes take
+        // theirs from it with a cross-lane read, so boundary loads are one
+        // instruction pair per 8 rounds
+        auto load_be8 = [&](uint32_t tg0, uint32_t &B, uint32_t &E) {
+            const uint32_t t = tg0 + (lane / kPbGroup) * kStep + lane % kPbGroup;
             const bool in = t < tb;
-            b = __builtin_amdgcn_raw_buffer_load_b32(roff, in ? (orow + t) * 4 : kOOR, 0, 0);
-            e = __builtin_amdgcn_raw_buffer_load_b32(roff, in ? (orow + A.off_stride + t) * 4 : kOOR, 0, 0);
+            B = __builtin_amdgcn_raw_buffer_load_b32(roff, in ? (orow + t) * 4 : kOOR, 0, 0);
+            E = __builtin_amdgcn_raw_buffer_load_b32(roff, in ? (erow + t) * 4 : kOOR, 0, 0);
         };
-        // 16-byte pieces qq and qq + 8 of the run from its 16-byte-aligned start
-        auto load_recs = [&](uint32_t tg, uint32_t b, uint32_t e, uint4 (&r)[2]) {
+        // 16-byte pieces qq, qq + 8, ... of the run from its 16-byte-aligned start
+        auto load_recs = [&](uint32_t tg, uint32_t b, uint32_t e, uint4 (&r)[R]) {
             const uint32_t base = (tg + k) * A.stride, s0 = b & ~3u;
 #pragma unroll
-            for (uint32_t c = 0; c < 2; c++) {
+            for (uint32_t c = 0; c < R; c++) {
                 const uint32_t i = s0 + c * 32 + qq * 4;
                 r[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
                                                      rrec, i < e ? (base + i) * 4 : kOOR, 0, 0));
             }
         };
         uint32_t tg = ta + wave * kPbGroup;
-        uint32_t bc, ec, b1, e1;
-        uint4 r[2];
-        load_be(tg, bc, ec);
-        load_be(tg + kStep, b1, e1);
+        uint32_t Bc, Ec, Bn, En;  // boundaries of rounds [8q, 8q + 8) and of the 8 after
+        load_be8(tg, Bc, Ec);
+        load_be8(tg + kPbGroup * kStep, Bn, En);
+        uint32_t bc = __shfl(Bc, k, 64), ec = __shfl(Ec, k, 64);
+        uint4 r[R];
         load_recs(tg, bc, ec, r);
-        for (; tg < tb; tg += kStep) {
-            uint32_t b2, e2;
-            uint4 rn[2];
-            load_be(tg + 2 * kStep, b2, e2);
-            load_recs(tg + kStep, b1, e1, rn);
-            // test the (up to) 8 records of this lane: bit j of fm = record j fails
-            const uint32_t s0 = bc & ~3u;
-            const uint32_t rec8[8] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w};
-            uint32_t fm = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < 8; j++) {
-                const uint32_t i = s0 + (j >> 2) * 32 + qq * 4 + (j & 3);
-                const uint32_t rr = rec8[j];
-                const uint32_t o = rr & kPSliceMask;
-                const bool fails = i >= bc && i < ec && !((img[o >> 3] >> (o & 7)) & 1);
-                fm |= uint32_t(fails) << j;
+        for (uint32_t rr = 0; tg < tb; tg += kStep, rr++) {
+            const uint32_t nr = (rr + 1) % kPbGroup;
+            if (nr == 0) {  // wave-uniform
+                Bc = Bn;
+                Ec = En;
+                load_be8(tg + (kPbGroup + 1) * kStep, Bn, En);
             }
-            // compact the failing swipes of the wave, one store per 64 of them
-            const uint32_t tbase = (tg + k) * kPaBlock;
-            uint32_t nq = 0;
+            const uint32_t b1 = __shfl(Bc, nr * kPbGroup + k, 64), e1 = __shfl(Ec, nr * kPbGroup + k, 64);
+            uint4 rn[R];
+            load_recs(tg + kStep, b1, e1, rn);
+            // the (up to) 4R records of this lane: piece c starts at record
+            // lo_c = s0 + c*32 + qq*4; bit j of vm: record j in [bc, ec)
+            const uint32_t s0 = bc & ~3u;
+            uint32_t rec[4 * R];
 #pragma unroll
-            for (uint32_t j = 0; j < 8; j++) {
-                const bool fj = (fm >> j) & 1;
-                const uint64_t m = __ballot(fj);
-                const uint32_t pos = nq + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-                const uint32_t at = tbase + ((rec8[j] >> kPSliceLog) & (kPaBlock - 1));
-                if (fj) {
-                    if (pos < kPbQueue) q[pos] = at;
-                    else __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail, at, 0, 0);  // overflow
-                }
-                nq += uint32_t(__builtin_popcountll(m));
+            for (uint32_t c = 0; c < R; c++) {
+                rec[4 * c] = r[c].x;
+                rec[4 * c + 1] = r[c].y;
+                rec[4 * c + 2] = r[c].z;
+                rec[4 * c + 3] = r[c].w;
+            }
+            auto in_run = [&](uint32_t lo) {  // 4-bit mask of lo + j in [bc, ec), j < 4
+                const int32_t hi = int32_t(ec) - int32_t(lo), lw = int32_t(bc) - int32_t(lo);
+                const uint32_t nh = uint32_t(hi < 0 ? 0 : (hi > 4 ? 4 : hi));
+                const uint32_t nl = uint32_t(lw < 0 ? 0 : (lw > 4 ? 4 : lw));
+                return ((1u << nh) - 1u) & ~((1u << nl) - 1u);
+            };
+            const uint32_t lo0 = s0 + qq * 4;
+            uint32_t vm = 0;
+#pragma unroll
+            for (uint32_t c = 0; c < R; c++) vm |= in_run(lo0 + c * 32) << (4 * c);
+            // bit set in the image: its 32-bit word, bit (offset & 31); with
+            // slice pairs the record's parity bit selects the image half
+            const uint32_t *img32 = reinterpret_cast<const uint32_t *>(img);
+            uint32_t okm = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 4 * R; j++) {
+                const uint32_t rr = rec[j];
+                const uint32_t o = SP == 1 ? (rr & kPSliceMask) : ((rr & kPSliceMask) | ((rr >> 10) & kPSliceBits));
+                okm |= __builtin_amdgcn_ubfe(img32[o >> 5], rr & 31, 1) << j;
+            }
+            uint32_t fm = vm & ~okm;
+            // compact the failing swipes of the wave: this lane's count, the
+            // wave's exclusive prefix, one store instruction per 64 of them
+            const uint32_t tbase = (tg + k) * kPaBlock;
+            const uint32_t cnt = __builtin_popcount(fm);
+            uint32_t incl = cnt;
+#pragma unroll
+            for (uint32_t o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
+            }
+            const uint32_t nq = __shfl(incl, 63, 64);
+            uint32_t pos = incl - cnt;
+            while (fm) {
+                const uint32_t j = __builtin_ctz(fm);
+                fm &= fm - 1;
+                uint32_t rr = rec[0];
+#pragma unroll
+                for (uint32_t jj = 1; jj < 4 * R; jj++) rr = j == jj ? rec[jj] : rr;
+                const uint32_t at = tbase + ((rr >> kPSliceLog) & (kPaBlock - 1));
+                if (pos < kPbQueue) q[pos] = at;
+                else __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail, at, 0, 0);  // overflow
+                pos++;
             }
             __builtin_amdgcn_wave_barrier();
             if (nq) {
@@ -331,22 +374,20 @@ __global__ void __launch_bounds__(kPbBlock, 8) k_part_b(const PartArgs A) {
                 __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail, lane < nq ? at : kOOR, 0, 0);
             }
             __builtin_amdgcn_wave_barrier();
-            if (ec - s0 > 64) {  // rare: a long run
+            if (ec - s0 > 32 * R) {  // rare: a long run
                 const uint32_t base = (tg + k) * A.stride;
-                for (uint32_t i = s0 + 64 + qq; i < ec; i += kPbLanes) {
+                for (uint32_t i = s0 + 32 * R + qq; i < ec; i += kPbLanes) {
                     const uint32_t rr = __builtin_amdgcn_raw_buffer_load_b32(rrec, (base + i) * 4, 0, 0);
-                    const uint32_t o = rr & kPSliceMask;
+                    const uint32_t o = SP == 1 ? (rr & kPSliceMask) : ((rr & kPSliceMask) | ((rr >> 10) & kPSliceBits));
                     if (!((img[o >> 3] >> (o & 7)) & 1))
                         __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail,
                                                              tbase + ((rr >> kPSliceLog) & (kPaBlock - 1)), 0, 0);
                 }
             }
-            r[0] = rn[0];
-            r[1] = rn[1];
+#pragma unroll
+            for (uint32_t c = 0; c < R; c++) r[c] = rn[c];
             bc = b1;
             ec = e1;
-            b1 = b2;
-            e1 = e2;
         }
     }
 }
@@ -935,7 +976,7 @@ hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratc
 hipError_t launch_swipes_part(const ChainDev &ch, const uint8_t *bytes, const uint32_t *offs,
                               uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *regs,
                               uint32_t nslots, uint8_t *out, Scratch *scr, unsigned int *err, int cus,
-                              uint32_t sub_opt, int hll_mode, hipStream_t st, PassHook hook,
+                              uint32_t sub_opt, int hll_mode, int pb_pairs, hipStream_t st, PassHook hook,
                               void *hook_user) {
     if (n == 0) return hipSuccess;
     PartArgs A{};
@@ -964,10 +1005,16 @@ hipError_t launch_swipes_part(const ChainDev &ch, const uint8_t *bytes, const ui
         else
             hipLaunchKernelGGL(k_part_a<22>, dim3(ga), dim3(kPaBlock), 0, st, A);
         if (hook) hook(hook_user, 0, 1);
-        // two blocks per CU, all resident, each an equal share of (slice, tile)
-        const unsigned gb = unsigned(cus) * 2 / kPGroups * kPGroups;
+        // all blocks resident, each an equal share of (slice unit, tile); a
+        // one-link chain is probed in slice pairs (128 KiB images, one block
+        // per CU): runs twice as long per tile
+        const bool pairs = A.nlinks == 1 && pb_pairs;
+        const unsigned gb = unsigned(cus) * (pairs ? 1 : 2) / kPGroups * kPGroups;
         if (hook) hook(hook_user, 1, 0);
-        hipLaunchKernelGGL(k_part_b, dim3(gb), dim3(kPbBlock), 0, st, A);
+        if (pairs)
+            hipLaunchKernelGGL(k_part_b<2>, dim3(gb), dim3(kPbBlock), 0, st, A);
+        else
+            hipLaunchKernelGGL(k_part_b<1>, dim3(gb), dim3(kPbBlock), 0, st, A);
         if (hook) hook(hook_user, 1, 1);
         if (hook) hook(hook_user, 2, 0);
         if (hll_mode == 1) {
