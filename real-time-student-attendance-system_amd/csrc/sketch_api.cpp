@@ -82,6 +82,8 @@ struct ske_ctx {
     uint32_t part_sub = 0;  // partitioned K1: swipes per sub-batch (0: default)
     int hll_mode = 0;       // partitioned K1's PFADD: 1 owned register lines, 0 CAS
     int pb_pairs = 1;       // partitioned K1 pass B over slice pairs (one-link chains)
+    int part_overlap = 1;   // many-batch calls: partitioned K1 pass C on a side stream
+    hipEvent_t part_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool lds_ok = false;
     bool k1_ok = false;       // short-id LDS K1 (sketch_k1.hip) usable
     int k1_legacy = 0;        // 1: always the generic LDS kernel (A/B diagnostics)
@@ -201,18 +203,21 @@ hipEvent_t ev_get(ske_ctx *c) {
 // an event pair for one kernel of pass `pass` (nullptrs when not timing)
 struct PassMark {
     hipEvent_t a = nullptr, b = nullptr;
+    hipStream_t st = nullptr;  // the stream the kernel runs on
 };
-PassMark mark_begin(ske_ctx *c, int pass) {
+PassMark mark_begin(ske_ctx *c, int pass, hipStream_t st) {
     PassMark m;
     if (!c->timing || c->capturing) return m;
     m.a = ev_get(c);
     m.b = ev_get(c);
-    if (!m.a || !m.b || hipEventRecord(m.a, c->st) != hipSuccess) return PassMark();
+    m.st = st;
+    if (!m.a || !m.b || hipEventRecord(m.a, st) != hipSuccess) return PassMark();
     c->marks.push_back({pass, m.a, m.b});
     return m;
 }
+PassMark mark_begin(ske_ctx *c, int pass) { return mark_begin(c, pass, c->st); }
 void mark_end(ske_ctx *c, const PassMark &m) {
-    if (m.b) (void)hipEventRecord(m.b, c->st);
+    if (m.b) (void)hipEventRecord(m.b, m.st);
 }
 
 // deps/bloom/bloom.c calc_bpe() + bloom_init() with BLOOM_OPT_NOROUND |
@@ -445,6 +450,48 @@ bool k1_fast_args(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const ui
     return true;
 }
 
+// The partitioned K1 over nb batches; `pipelined`: pass C of each unit on a
+// side stream, overlapping the next unit's passes A / B (launch_swipes_part).
+int launch_part(ske_ctx *c, const ChainDev &ch, const PartBatch *bt, uint32_t nb, bool pipelined) {
+    uint64_t nmax = 0;
+    for (uint32_t j = 0; j < nb; j++) nmax = bt[j].n > nmax ? bt[j].n : nmax;
+    if (nmax == 0) return SKE_OK;
+    hipError_t e = pipelined ? part_reserve_pipelined(ch, nmax, c->part_sub, c->scratch)
+                             : part_reserve(ch, nmax, c->part_sub, c->scratch);
+    if (e != hipSuccess) return scratch_error(c, e);
+    hipStream_t side = nullptr;
+    if (pipelined) {
+        if (c->many_n < 1) {
+            HIPCHK(c, hipStreamCreateWithFlags(&c->many_st[0], hipStreamNonBlocking));
+            HIPCHK(c, hipEventCreateWithFlags(&c->many_join[0], hipEventDisableTiming));
+            c->many_n = 1;
+        }
+        for (int i = 0; i < 4; i++)
+            if (!c->part_ev[i]) HIPCHK(c, hipEventCreateWithFlags(&c->part_ev[i], hipEventDisableTiming));
+        side = c->many_st[0];
+    }
+    unsigned long long cid = 0;
+    int rc = scratch_user_begin(c, &cid);
+    if (rc) return rc;
+    // one event pair per kernel and unit, bracketed on the kernel's stream
+    PassMark pm[3];
+    auto hook = [](void *u, int pass, int end, hipStream_t st) {
+        ske_ctx *cc = static_cast<ske_ctx *>(u);
+        PassMark *marks = reinterpret_cast<PassMark *>(cc->hook_arg);
+        if (end) mark_end(cc, marks[pass]);
+        else marks[pass] = mark_begin(cc, 1 + pass, st);
+    };
+    c->hook_arg = pm;
+    e = launch_swipes_part(ch, bt, nb, c->regs, c->nslots, c->scratch, c->err, c->cus, c->part_sub, c->hll_mode,
+                           c->pb_pairs, c->st, side, c->part_ev, c->timing && !c->capturing ? +hook : nullptr, c);
+    if (e != hipSuccess) {
+        c->last_hip = std::string("launch_swipes_part: ") + hipGetErrorString(e);
+        scratch_user_end(c, cid);
+        return SKE_EHIP;
+    }
+    return scratch_user_end(c, cid);
+}
+
 // Enqueue K1 (mode swipes) with the variant the chain selects.
 int launch_k1(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32_t *offs,
               uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *out) {
@@ -458,24 +505,8 @@ int launch_k1(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32
     }
     const int var = c->ablate ? 0 : k1_variant(c, ch);
     if (var == 3) {
-        hipError_t e = part_reserve(ch, n, c->part_sub, c->scratch);
-        if (e != hipSuccess) return scratch_error(c, e);
-        unsigned long long cid = 0;
-        int rc = scratch_user_begin(c, &cid);
-        if (rc) return rc;
-        // one launch per pass and sub-batch, each bracketed when timing
-        PassMark pm[3];
-        auto hook = [](void *u, int pass, int end) {
-            ske_ctx *cc = static_cast<ske_ctx *>(u);
-            PassMark *marks = reinterpret_cast<PassMark *>(cc->hook_arg);
-            if (end) mark_end(cc, marks[pass]);
-            else marks[pass] = mark_begin(cc, 1 + pass);
-        };
-        c->hook_arg = pm;
-        HIPCHK(c, launch_swipes_part(ch, bytes, offs, fixed_w, slot, n, c->regs, c->nslots, out,
-                                     c->scratch, c->err, c->cus, c->part_sub, c->hll_mode, c->pb_pairs, c->st,
-                                     c->timing && !c->capturing ? +hook : nullptr, c));
-        return scratch_user_end(c, cid);
+        const PartBatch pb{bytes, offs, fixed_w, slot, n, out};
+        return launch_part(c, ch, &pb, 1, false);
     }
     if (var == 2) {
         hipError_t e = hipSuccess;
@@ -589,6 +620,8 @@ int ske_close(ske_ctx *c) {
         (void)hipEventDestroy(c->many_join[i]);
     }
     if (c->many_fork) (void)hipEventDestroy(c->many_fork);
+    for (hipEvent_t e : c->part_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->kt_key) (void)hipFree(c->kt_key);
     if (c->kt_slot) (void)hipFree(c->kt_slot);
     if (c->stats) (void)hipFree(c->stats);
@@ -689,6 +722,11 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
     if (!strcmp(name, "hll_mode")) {  // partitioned K1's PFADD: 1 owned lines, 0 CAS
         if (value < 0 || value > 1) return SKE_EINVAL;
         c->hll_mode = int(value);
+        return SKE_OK;
+    }
+    if (!strcmp(name, "part_overlap")) {  // many-batch calls: overlap pass C with the next A / B
+        if (value < 0 || value > 1) return SKE_EINVAL;
+        c->part_overlap = int(value);
         return SKE_OK;
     }
     if (!strcmp(name, "pb_pairs")) {  // partitioned K1: pass B over slice pairs (1) or slices
@@ -1204,10 +1242,14 @@ int ske_swipes_many_async(ske_ctx *c, uint32_t fid, const ske_swipe_batch *b, ui
     uint64_t nmax = 0;
     for (uint32_t j = 0; j < nb; j++) nmax = b[j].n > nmax ? b[j].n : nmax;
     const int var = c->ablate ? 0 : k1_variant(c, ch);
-    if (var == 3 && nmax) {
-        hipError_t e = part_reserve(ch, nmax, c->part_sub, c->scratch);
-        if (e != hipSuccess) return scratch_error(c, e);
-    } else if (var == 2 && nmax) {
+    if (var == 3) {  // one pipelined call over every batch (pass C beside the next A / B)
+        std::vector<PartBatch> pb(nb);
+        for (uint32_t j = 0; j < nb; j++)
+            pb[j] = PartBatch{b[j].bytes, b[j].width ? nullptr : b[j].offs, b[j].width, b[j].slot, b[j].n,
+                              b[j].out_valid};
+        return launch_part(c, ch, pb.data(), nb, c->part_overlap != 0 && nb > 1);
+    }
+    if (var == 2 && nmax) {
         hipError_t e = hipSuccess;
         (void)scratch_get(c->scratch, 16, xr_scratch_bytes(nmax, ch.nlinks), &e);
         if (e != hipSuccess) return scratch_error(c, e);

@@ -131,12 +131,21 @@ bool part_supported(const ChainDev &ch);
 hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub, Scratch *scr);
 // hook (may be null): called as hook(user, pass, 0) right before and
 // hook(user, pass, 1) right after each pass's launch (pass 0..2 = A, B, C)
-typedef void (*PassHook)(void *user, int pass, int end);
-hipError_t launch_swipes_part(const ChainDev &ch, const uint8_t *bytes, const uint32_t *offs,
-                              uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *regs,
-                              uint32_t nslots, uint8_t *out, Scratch *scr, unsigned int *err, int cus,
-                              uint32_t sub, int hll_mode, int pb_pairs, hipStream_t st, PassHook hook = nullptr,
-                              void *hook_user = nullptr);
+typedef void (*PassHook)(void *user, int pass, int end, hipStream_t st);
+struct PartBatch {
+    const uint8_t *bytes;
+    const uint32_t *offs;  // nullptr: fixed-width ids
+    uint32_t fixed_w;
+    const uint32_t *slot;
+    uint64_t n;
+    uint8_t *out;          // may be nullptr
+};
+// side == nullptr: every pass on st; else pass C on `side` (ev: 4 events)
+hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t nb, uint8_t *regs,
+                              uint32_t nslots, Scratch *scr, unsigned int *err, int cus, uint32_t sub,
+                              int hll_mode, int pb_pairs, hipStream_t st, hipStream_t side, hipEvent_t *ev,
+                              PassHook hook = nullptr, void *hook_user = nullptr);
+hipError_t part_reserve_pipelined(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratch *scr);
 
 // sketch_order.hip -- order-exact paths (replies that depend on item order)
 struct Scratch;  // growable device scratch, owned by the context

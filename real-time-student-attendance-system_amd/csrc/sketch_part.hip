@@ -87,13 +87,73 @@ __device__ __forceinline__ void part_group(uint32_t ntiles, uint32_t x, uint32_t
 }
 
 // ---------------------------------------------------------------------------
+// ids of at most 8 bytes (every config's student ids), read and hashed the way
+// the LDS K1 does (sketch_k1.hip): the one or two aligned 64-bit words holding
+// the id (an empty or long id reads zeros past the range), a funnel shift and
+// a length mask, MurmurHash64A in closed form h = ((seed ^ len*m) ^ t) * m then
+// the finaliser, t the id word or (len 8) its mixed block, mixed once for the
+// three hashes.  A wave holding a longer id takes the generic routines.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t part_rsrc(const void *p, uint32_t nbytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, int(nbytes), 0x00020000);
+}
+
+struct PartId {
+    uint32_t b, len;
+    uint64_t w0, w1;
+};
+
+__device__ __forceinline__ void part_id_load(const __amdgpu_buffer_rsrc_t &rb, uint32_t b, uint32_t e,
+                                             PartId &d) {
+    d.b = b;
+    d.len = e - b;
+    const uint32_t s8 = b & 7;
+    const bool sh = d.len && d.len <= 8;
+    const uint32_t o0 = sh ? (b & ~7u) : 0xfffffff8u;
+    const uint32_t o1 = (sh && s8 + d.len > 8) ? o0 + 8 : o0;
+    d.w0 = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rb, o0, 0, 0));
+    d.w1 = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rb, o1, 0, 0));
+}
+
+__device__ __forceinline__ void part_hash3(const uint8_t *bytes, const PartId &d, uint64_t &ha, uint64_t &hb,
+                                           uint64_t &hh) {
+    if (__any(d.len > 8)) {
+        const Item it = load_item(bytes, d.b, d.b + d.len);
+        ha = murmur_item(it, kBloomSeed);
+        hb = murmur_item(it, ha);
+        hh = murmur_item(it, kHllSeed);
+        return;
+    }
+    const uint32_t sh = (d.b & 7) * 8;
+    const bool hi = sh >= 32;
+    const uint32_t a = hi ? uint32_t(d.w0 >> 32) : uint32_t(d.w0);
+    const uint32_t bb = hi ? uint32_t(d.w1) : uint32_t(d.w0 >> 32);
+    const uint32_t c = hi ? uint32_t(d.w1 >> 32) : uint32_t(d.w1);
+    const uint64_t v = (uint64_t(__builtin_amdgcn_alignbit(c, bb, sh & 31)) << 32) |
+                       __builtin_amdgcn_alignbit(bb, a, sh & 31);
+    const uint32_t drop = (64 - d.len * 8) & 63;
+    uint64_t tw = (v << drop) >> drop;
+    if (__any(d.len == 8)) {
+        uint64_t k = tw * kMurmurM;
+        k ^= k >> 47;
+        k *= kMurmurM;
+        tw = d.len == 8 ? k : tw;
+    }
+    const uint64_t t = tw ^ (uint64_t(d.len) * kMurmurM);
+    const bool nz = d.len != 0;
+    ha = mm_final(nz ? (kBloomSeed ^ t) * kMurmurM : kBloomSeed);
+    hb = mm_final(nz ? (ha ^ t) * kMurmurM : ha);
+    hh = mm_final(nz ? (kHllSeed ^ t) * kMurmurM : kHllSeed);
+}
+
+// ---------------------------------------------------------------------------
 // pass A: hash, probe records, counting sort by slice
 // ---------------------------------------------------------------------------
 // One tile = 1024 swipes, one per thread.  KM: the most probes per swipe the
 // instantiation holds (every link's k summed); records of a tile live in LDS
 // (KM = 11: 44 KiB, two blocks per CU, so one block's hashing overlaps the
 // other's sort and copy-out).
-template <int KM>
+template <int KM, bool kOneLink>
 __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const PartArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t srec[kPaBlock * KM];
     // slice histogram, then run starts; two buffers used by alternate tiles,
@@ -116,12 +176,13 @@ __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const Par
     uint32_t gt0, gt1;
     part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
     const uint32_t tstep = gridDim.x / kPGroups;
+    const __amdgpu_buffer_rsrc_t rbytes = part_rsrc(A.bytes, 0xfffffff0u);
     uint32_t par = 0, nb_ = 0, ne_ = 0;
-    Item it;
+    PartId it;
     {
         const uint32_t t = gt0 + blockIdx.x / kPGroups;
         offsets(t < gt1 ? t : gt0, nb_, ne_);
-        it = load_item(A.bytes, nb_, ne_);
+        part_id_load(rbytes, nb_, ne_, it);
     }
     for (uint32_t t = gt0 + blockIdx.x / kPGroups; t < gt1; t += tstep, par ^= 1) {
         uint32_t *scnt = scnt2[par];
@@ -131,10 +192,8 @@ __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const Par
         {
             const uint32_t i = t * kPaBlock + tid;
             const bool act = i < A.n;
-            const bool sh = it.len <= 8;
-            const uint64_t ha = sh ? murmur_short(it.w0, it.len, kBloomSeed) : murmur_item(it, kBloomSeed);
-            const uint64_t hb = sh ? murmur_short(it.w0, it.len, ha) : murmur_item(it, ha);
-            const uint64_t hh = sh ? murmur_short(it.w0, it.len, kHllSeed) : murmur_item(it, kHllSeed);
+            uint64_t ha, hb, hh;
+            part_hash3(A.bytes, it, ha, hb, hh);
             if (act) {
                 uint32_t idx, rank;
                 hll_patlen(hh, idx, rank);
@@ -144,31 +203,50 @@ __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const Par
             // every link's k probes in RedisBloom's order, newest link first
             // (the order is immaterial to the answer; records carry no link:
             // a slice belongs to one link)
-            uint32_t l = A.nlinks - 1, jl = 0;
-            ProbeWalk32 wk;
-            wk.init(ha, hb, part_div(A.link[l]));
+            // bit 29 of a record: its slice's parity (pass B's slice pairs)
+            const uint32_t rbase = (tid << kPSliceLog) | 0x80000000u;
+            if constexpr (kOneLink) {  // one link of k = ksum <= KM probes, slices from 0
+                const PartLink &L = A.link[0];
+                ProbeWalk32 wk;
+                wk.init(ha, hb, part_div(L));
 #pragma unroll
-            for (int q = 0; q < KM; q++) {
-                rp[q] = 0xffffffffu;
-                rv[q] = 0;
-                if (uint32_t(q) < A.ksum) {  // block-uniform
-                    if (jl == A.link[l].k) {
-                        l--;
-                        jl = 0;
-                        wk.init(ha, hb, part_div(A.link[l]));
+                for (int q = 0; q < KM; q++) {
+                    rp[q] = 0xffffffffu;
+                    rv[q] = 0;
+                    if (uint32_t(q) < A.ksum) {  // block-uniform
+                        const uint32_t x = wk.x;
+                        const uint32_t g = x >> kPSliceLog;
+                        rv[q] = (x & kPSliceMask) | ((g & 1u) << 29) | rbase;
+                        if (act) rp[q] = (g << 16) | atomicAdd(&scnt[g], 1u);
+                        wk.step(L.d);
                     }
-                    const uint32_t x = wk.x;
-                    const uint32_t g = A.link[l].slice0 + (x >> kPSliceLog);
-                    // bit 29: the slice's parity (pass B's slice pairs)
-                    rv[q] = (x & kPSliceMask) | (tid << kPSliceLog) | ((g & 1u) << 29) | 0x80000000u;
-                    if (act) rp[q] = (g << 16) | atomicAdd(&scnt[g], 1u);
-                    wk.step(A.link[l].d);
-                    jl++;
+                }
+            } else {
+                uint32_t l = A.nlinks - 1, jl = 0;
+                ProbeWalk32 wk;
+                wk.init(ha, hb, part_div(A.link[l]));
+#pragma unroll
+                for (int q = 0; q < KM; q++) {
+                    rp[q] = 0xffffffffu;
+                    rv[q] = 0;
+                    if (uint32_t(q) < A.ksum) {  // block-uniform
+                        if (jl == A.link[l].k) {
+                            l--;
+                            jl = 0;
+                            wk.init(ha, hb, part_div(A.link[l]));
+                        }
+                        const uint32_t x = wk.x;
+                        const uint32_t g = A.link[l].slice0 + (x >> kPSliceLog);
+                        rv[q] = (x & kPSliceMask) | ((g & 1u) << 29) | rbase;
+                        if (act) rp[q] = (g << 16) | atomicAdd(&scnt[g], 1u);
+                        wk.step(A.link[l].d);
+                        jl++;
+                    }
                 }
             }
         }
         __syncthreads();
-        it = load_item(A.bytes, nb_, ne_);  // the next tile's ids
+        part_id_load(rbytes, nb_, ne_, it);  // the next tile's ids
         // exclusive scan of scnt[0..S] (scnt[S] == 0 becomes the tile's total)
         constexpr int kPer = (kPMaxSlices + 1) / kPaBlock;
         uint32_t v[kPer], s = 0;
@@ -213,9 +291,6 @@ __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const Par
 // ---------------------------------------------------------------------------
 // pass B: LDS-resident slices, probe their runs
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t part_rsrc(const void *p, uint32_t nbytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, int(nbytes), 0x00020000);
-}
 constexpr uint32_t kOOR = 0x80000000u;  // a buffer offset past every range: load 0, store dropped
 
 // The (slice, tile) space is cut into gridDim.x equal contiguous ranges, slice
@@ -973,66 +1048,129 @@ hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratc
     return part_scratch(&A, n ? n : 1, part_sub(sub_opt), scr);
 }
 
-hipError_t launch_swipes_part(const ChainDev &ch, const uint8_t *bytes, const uint32_t *offs,
-                              uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *regs,
-                              uint32_t nslots, uint8_t *out, Scratch *scr, unsigned int *err, int cus,
-                              uint32_t sub_opt, int hll_mode, int pb_pairs, hipStream_t st, PassHook hook,
-                              void *hook_user) {
-    if (n == 0) return hipSuccess;
+// The fail bytes and HLL words pass C reads: two sets, so that with pass C on
+// a side stream the next unit's pass A (which writes them) does not wait for
+// it (set 1: slots 38, 39)
+static hipError_t part_scratch_c(PartArgs *A, uint32_t m, int set, Scratch *scr) {
+    if (set == 0) return hipSuccess;  // part_scratch's slots 30, 31
+    hipError_t e = hipSuccess;
+    A->fail = (uint8_t *)scratch_get(scr, 38, size_t(A->fail_stride) * A->nlinks, &e);
+    if (e == hipSuccess) A->hllw = (uint32_t *)scratch_get(scr, 39, size_t(m) * 4, &e);
+    return e;
+}
+
+hipError_t part_reserve_pipelined(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratch *scr) {
     PartArgs A{};
     if (!part_plan(ch, &A)) return hipErrorInvalidValue;
     const uint32_t sub = part_sub(sub_opt);
-    hipError_t e = part_scratch(&A, n, sub, scr);
+    hipError_t e = part_scratch(&A, n ? n : 1, sub, scr);
+    if (e == hipSuccess) e = part_scratch_c(&A, uint32_t(n < sub ? (n ? n : 1) : sub), 1, scr);
+    return e;
+}
+
+// Units = (batch, sub-batch of at most `sub` swipes), in order.  Without a
+// side stream every pass runs on st.  With one (`side`, events ev[0..3]):
+// passes A and B of unit u on st, its pass C on `side` behind B (event
+// ev[u & 1]); unit u's pass A first waits for pass C of unit u - 2 (event
+// ev[2 + (u & 1)]), the last reader of the scratch set it writes; st joins
+// `side` at the end.  So pass C of one unit (memory-side register atomics)
+// overlaps passes A / B of the next (hashing, slice probes).  Results equal
+// the serial order: units touch disjoint answers and PFADD is a max.
+hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t nb, uint8_t *regs,
+                              uint32_t nslots, Scratch *scr, unsigned int *err, int cus, uint32_t sub_opt,
+                              int hll_mode, int pb_pairs, hipStream_t st, hipStream_t side, hipEvent_t *ev,
+                              PassHook hook, void *hook_user) {
+    PartArgs A{};
+    if (!part_plan(ch, &A)) return hipErrorInvalidValue;
+    const uint32_t sub = part_sub(sub_opt);
+    uint64_t nmax = 0;
+    for (uint32_t j = 0; j < nb; j++) nmax = bt[j].n > nmax ? bt[j].n : nmax;
+    if (nmax == 0) return hipSuccess;
+    hipError_t e = part_scratch(&A, nmax, sub, scr);
     if (e != hipSuccess) return e;
+    uint8_t *fail0 = A.fail;
+    uint32_t *hllw0 = A.hllw;
+    uint8_t *fail1 = nullptr;
+    uint32_t *hllw1 = nullptr;
+    if (side) {
+        e = part_scratch_c(&A, uint32_t(nmax < sub ? nmax : sub), 1, scr);
+        if (e != hipSuccess) return e;
+        fail1 = A.fail;
+        hllw1 = A.hllw;
+    }
     A.regs = regs;
     A.nslots = nslots;
     A.err = err;
-    A.fixed_w = fixed_w;
     const uint32_t km = part_km(A.ksum);
-    for (uint64_t s0 = 0; s0 < n; s0 += sub) {
-        const uint32_t ms = n - s0 < sub ? uint32_t(n - s0) : sub;
-        A.n = ms;
-        A.ntiles = (ms + kPaBlock - 1) / kPaBlock;
-        A.bytes = offs ? bytes : bytes + s0 * fixed_w;
-        A.offs = offs ? offs + s0 : nullptr;
-        A.slot = slot + s0;
-        A.out = out ? out + s0 : nullptr;
-        const unsigned per_cu = km <= 11 ? 2 : 1;
-        const unsigned ga = unsigned(cus) * per_cu / kPGroups * kPGroups;  // blocks past a group's tiles exit
-        if (hook) hook(hook_user, 0, 0);
-        if (km <= 11)
-            hipLaunchKernelGGL(k_part_a<11>, dim3(ga), dim3(kPaBlock), 0, st, A);
-        else
-            hipLaunchKernelGGL(k_part_a<22>, dim3(ga), dim3(kPaBlock), 0, st, A);
-        if (hook) hook(hook_user, 0, 1);
-        // all blocks resident, each an equal share of (slice unit, tile); a
-        // one-link chain is probed in slice pairs (128 KiB images, one block
-        // per CU): runs twice as long per tile
-        const bool pairs = A.nlinks == 1 && pb_pairs;
-        const unsigned gb = unsigned(cus) * (pairs ? 1 : 2) / kPGroups * kPGroups;
-        if (hook) hook(hook_user, 1, 0);
-        if (pairs)
-            hipLaunchKernelGGL(k_part_b<2>, dim3(gb), dim3(kPbBlock), 0, st, A);
-        else
-            hipLaunchKernelGGL(k_part_b<1>, dim3(gb), dim3(kPbBlock), 0, st, A);
-        if (hook) hook(hook_user, 1, 1);
-        if (hook) hook(hook_user, 2, 0);
-        if (hll_mode == 1) {
-            // PFADD by owned register lines: C2, S, D, E (timed together as pass C)
-            HllArgs H{};
-            e = hll_scratch(&H, ms, scr);
-            if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(k_part_c2, dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(kPaBlock), 0,
-                               st, A, H);
-            hipLaunchKernelGGL(k_part_hscan, dim3(kH1), dim3(1024), 0, st, H);
-            hipLaunchKernelGGL(k_part_hd, dim3(unsigned(cus) * 2), dim3(1024), 0, st, H);
-            hipLaunchKernelGGL(k_part_he, dim3(unsigned(cus) * 2), dim3(kHeBlock), 0, st, A, H);
-        } else {
-            const unsigned gc = (part_grid(ms, kPcBlock * 2, cus * 8) + kPGroups - 1) / kPGroups * kPGroups;
-            hipLaunchKernelGGL(k_part_c<2>, dim3(gc), dim3(kPcBlock), 0, st, A);
+    uint32_t u = 0;
+#define SKE_CK(x)                        \
+    do {                                 \
+        hipError_t e_ = (x);             \
+        if (e_ != hipSuccess) return e_; \
+    } while (0)
+    for (uint32_t j = 0; j < nb; j++) {
+        const PartBatch &B = bt[j];
+        for (uint64_t s0 = 0; s0 < B.n; s0 += sub, u++) {
+            const uint32_t ms = B.n - s0 < sub ? uint32_t(B.n - s0) : sub;
+            const int set = side ? int(u & 1) : 0;
+            A.fail = set ? fail1 : fail0;
+            A.hllw = set ? hllw1 : hllw0;
+            A.fixed_w = B.fixed_w;
+            A.n = ms;
+            A.ntiles = (ms + kPaBlock - 1) / kPaBlock;
+            A.bytes = B.offs ? B.bytes : B.bytes + s0 * B.fixed_w;
+            A.offs = B.offs ? B.offs + s0 : nullptr;
+            A.slot = B.slot + s0;
+            A.out = B.out ? B.out + s0 : nullptr;
+            if (side && u >= 2) SKE_CK(hipStreamWaitEvent(st, ev[2 + set], 0));
+            const unsigned per_cu = km <= 11 ? 2 : 1;
+            const unsigned ga = unsigned(cus) * per_cu / kPGroups * kPGroups;  // blocks past a group's tiles exit
+            if (hook) hook(hook_user, 0, 0, st);
+            if (km <= 11 && A.nlinks == 1)
+                hipLaunchKernelGGL((k_part_a<11, true>), dim3(ga), dim3(kPaBlock), 0, st, A);
+            else if (km <= 11)
+                hipLaunchKernelGGL((k_part_a<11, false>), dim3(ga), dim3(kPaBlock), 0, st, A);
+            else
+                hipLaunchKernelGGL((k_part_a<22, false>), dim3(ga), dim3(kPaBlock), 0, st, A);
+            if (hook) hook(hook_user, 0, 1, st);
+            // all blocks resident, each an equal share of (slice unit, tile); a
+            // one-link chain is probed in slice pairs (128 KiB images, one block
+            // per CU): runs twice as long per tile
+            const bool pairs = A.nlinks == 1 && pb_pairs;
+            const unsigned gb = unsigned(cus) * (pairs ? 1 : 2) / kPGroups * kPGroups;
+            if (hook) hook(hook_user, 1, 0, st);
+            if (pairs)
+                hipLaunchKernelGGL(k_part_b<2>, dim3(gb), dim3(kPbBlock), 0, st, A);
+            else
+                hipLaunchKernelGGL(k_part_b<1>, dim3(gb), dim3(kPbBlock), 0, st, A);
+            if (hook) hook(hook_user, 1, 1, st);
+            hipStream_t sc = st;
+            if (side) {
+                SKE_CK(hipEventRecord(ev[set], st));
+                SKE_CK(hipStreamWaitEvent(side, ev[set], 0));
+                sc = side;
+            }
+            if (hook) hook(hook_user, 2, 0, sc);
+            if (hll_mode == 1) {
+                // PFADD by owned register lines: C2, S, D, E (timed together as pass C)
+                HllArgs H{};
+                SKE_CK(hll_scratch(&H, ms, scr));
+                hipLaunchKernelGGL(k_part_c2, dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(kPaBlock), 0,
+                                   sc, A, H);
+                hipLaunchKernelGGL(k_part_hscan, dim3(kH1), dim3(1024), 0, sc, H);
+                hipLaunchKernelGGL(k_part_hd, dim3(unsigned(cus) * 2), dim3(1024), 0, sc, H);
+                hipLaunchKernelGGL(k_part_he, dim3(unsigned(cus) * 2), dim3(kHeBlock), 0, sc, A, H);
+            } else {
+                const unsigned gc = (part_grid(ms, kPcBlock * 2, cus * 8) + kPGroups - 1) / kPGroups * kPGroups;
+                hipLaunchKernelGGL(k_part_c<2>, dim3(gc), dim3(kPcBlock), 0, sc, A);
+            }
+            if (hook) hook(hook_user, 2, 1, sc);
+            if (side) SKE_CK(hipEventRecord(ev[2 + set], side));
+            SKE_CK(hipGetLastError());
         }
-        if (hook) hook(hook_user, 2, 1);
     }
+    if (side && u) SKE_CK(hipStreamWaitEvent(st, ev[2 + ((u - 1) & 1)], 0));
+#undef SKE_CK
     return hipGetLastError();
 }
 

@@ -210,3 +210,46 @@ def test_partitioned_hot_register_and_many_keys(engine, orc, hll_mode):
     want, _, _ = orc.process_swipes(chain, regs, slot, buf2, offs)
     assert np.array_equal(out.to_host(np.uint8, b.n), want)
     assert np.array_equal(engine.registers_all(40_001), regs)
+
+
+@pytest.mark.parametrize("mode", ["direct", "graph"])
+def test_many_pipelined_small_units(engine, orc, mode):
+    """ske_swipes_many_async through the partitioned K1 with pass C of every
+    unit on a side stream beside the next unit's passes A / B: sub-batches of
+    64k swipes make ~25 units over 7 ragged batches (incl. 1 swipe and a
+    partial tile), so the two scratch sets alternate many times; answers and
+    registers == the oracle over the batches in order."""
+    import torch
+    from rtsas_amd.engine import DeviceBuffer
+    w, p = _c3_small(engine)
+    engine.set_option("part_sub", 65536)
+    sizes = [300_000, 1, 70_001, 300_000, 250_000, 2048, 400_000]
+    bs, start = [], 0
+    for n in sizes:
+        bs.append(engine.swipe_batch(p, start, n))
+        start += n
+    outs = [DeviceBuffer(engine.ctx, b.n) for b in bs]
+    main = torch.cuda.Stream()
+    engine.set_stream(main.cuda_stream)
+    try:
+        if mode == "direct":
+            engine.swipes_many_async(0, bs, outs)
+        else:
+            engine.swipes_many_async(0, bs[:2], outs[:2])  # side stream, scratch sets
+            torch.cuda.synchronize()
+            g = engine.capture(lambda: engine.swipes_many_async(0, bs, outs))
+            g.launch()
+        engine.sync()  # the context stream alone: the side stream was joined into it
+        if mode == "graph":
+            g.free()
+    finally:
+        engine.set_stream(None)
+    chain = orc.Chain(w.bf_capacity, w.bf_error)
+    mb = engine.members_batch(p, 0, w.n_members).to_host()
+    chain.madd_packed(mb[0], mb[1])
+    regs = np.zeros((w.n_keys, 16384), np.uint8)
+    for b, o in zip(bs, outs):
+        buf, offs, slot = b.to_host()
+        v, _, _ = orc.process_swipes(chain, regs, slot.astype(np.uint32), buf, offs)
+        assert np.array_equal(o.to_host(np.uint8, b.n), v)
+    assert np.array_equal(engine.registers_all(w.n_keys), regs)
