@@ -79,9 +79,9 @@ def parse():
                     help="partitioned K1 pass B: 1 = slice pairs (128 KiB images), 0 = single "
                          "slices (-1: library default)")
     ap.add_argument("--persistent", type=int, default=-1,
-                    help="1 = the K timed steps as ONE ske_swipes_many_async call (default): for "
-                         "the partitioned K1 each step's pass C on a side stream beside the next "
-                         "step's passes A / B; for the LDS K1 one persistent "
+                    help="1 = the K timed steps as ONE ske_swipes_many_async call (for the "
+                         "partitioned K1 with the part_overlap option: each step's pass C on a side "
+                         "stream beside the next step's pass B); for the LDS K1 one persistent "
                          "LDS K1 launch over the K batches; default for the LDS K1); 0 = a K1 "
                          "launch per step")
     ap.add_argument("--streams", type=int, default=0,
@@ -335,7 +335,7 @@ def main():
     engine.hll_reserve(w.n_keys + 64)
     variant = engine.variant(0)
     lds_k1 = variant == 1
-    persistent = bool(args.persistent if args.persistent >= 0 else (lds_k1 or variant == 3))
+    persistent = bool(args.persistent if args.persistent >= 0 else lds_k1)
     if lds_k1:
         engine.set_option("k1_persistent", 1 if persistent else 0)
     streams_n = 1 if persistent else (args.streams or (16 if lds_k1 else 1))

@@ -82,7 +82,7 @@ struct ske_ctx {
     uint32_t part_sub = 0;  // partitioned K1: swipes per sub-batch (0: default)
     int hll_mode = 0;       // partitioned K1's PFADD: 1 owned register lines, 0 CAS
     int pb_pairs = 1;       // partitioned K1 pass B over slice pairs (one-link chains)
-    int part_overlap = 1;   // many-batch calls: partitioned K1 pass C on a side stream
+    int part_overlap = 0;   // many-batch calls: partitioned K1 pass C on a side stream (measured slower)
     hipEvent_t part_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool lds_ok = false;
     bool k1_ok = false;       // short-id LDS K1 (sketch_k1.hip) usable
@@ -456,8 +456,7 @@ int launch_part(ske_ctx *c, const ChainDev &ch, const PartBatch *bt, uint32_t nb
     uint64_t nmax = 0;
     for (uint32_t j = 0; j < nb; j++) nmax = bt[j].n > nmax ? bt[j].n : nmax;
     if (nmax == 0) return SKE_OK;
-    hipError_t e = pipelined ? part_reserve_pipelined(ch, nmax, c->part_sub, c->scratch)
-                             : part_reserve(ch, nmax, c->part_sub, c->scratch);
+    hipError_t e = part_reserve(ch, nmax, c->part_sub, c->scratch);
     if (e != hipSuccess) return scratch_error(c, e);
     hipStream_t side = nullptr;
     if (pipelined) {

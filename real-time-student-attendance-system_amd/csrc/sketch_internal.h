@@ -145,7 +145,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
                               uint32_t nslots, Scratch *scr, unsigned int *err, int cus, uint32_t sub,
                               int hll_mode, int pb_pairs, hipStream_t st, hipStream_t side, hipEvent_t *ev,
                               PassHook hook = nullptr, void *hook_user = nullptr);
-hipError_t part_reserve_pipelined(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratch *scr);
+
 
 // sketch_order.hip -- order-exact paths (replies that depend on item order)
 struct Scratch;  // growable device scratch, owned by the context

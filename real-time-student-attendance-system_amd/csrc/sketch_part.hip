@@ -1042,11 +1042,7 @@ static uint32_t part_sub(uint32_t sub_opt) {
     return sub < kPaBlock ? kPaBlock : (sub > kPSub ? kPSub : sub);
 }
 
-hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratch *scr) {
-    PartArgs A{};
-    if (!part_plan(ch, &A)) return hipErrorInvalidValue;
-    return part_scratch(&A, n ? n : 1, part_sub(sub_opt), scr);
-}
+
 
 // The fail bytes and HLL words pass C reads: two sets, so that with pass C on
 // a side stream the next unit's pass A (which writes them) does not wait for
@@ -1059,7 +1055,9 @@ static hipError_t part_scratch_c(PartArgs *A, uint32_t m, int set, Scratch *scr)
     return e;
 }
 
-hipError_t part_reserve_pipelined(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratch *scr) {
+// both scratch sets, so a graph recorded after a single-batch warm-up can hold
+// pipelined many-batch calls too
+hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratch *scr) {
     PartArgs A{};
     if (!part_plan(ch, &A)) return hipErrorInvalidValue;
     const uint32_t sub = part_sub(sub_opt);
@@ -1070,12 +1068,12 @@ hipError_t part_reserve_pipelined(const ChainDev &ch, uint64_t n, uint32_t sub_o
 
 // Units = (batch, sub-batch of at most `sub` swipes), in order.  Without a
 // side stream every pass runs on st.  With one (`side`, events ev[0..3]):
-// passes A and B of unit u on st, its pass C on `side` behind B (event
-// ev[u & 1]); unit u's pass A first waits for pass C of unit u - 2 (event
-// ev[2 + (u & 1)]), the last reader of the scratch set it writes; st joins
-// `side` at the end.  So pass C of one unit (memory-side register atomics)
-// overlaps passes A / B of the next (hashing, slice probes).  Results equal
-// the serial order: units touch disjoint answers and PFADD is a max.
+// passes A and B of unit u on st, its pass C on `side` once pass A of unit
+// u + 1 is done (event ev[(u + 1) & 1]); unit u's pass A first waits for pass
+// C of unit u - 2 (event ev[2 + (u & 1)]), the last reader of the scratch set
+// it writes; st joins `side` at the end.  So pass C of one unit (memory-side
+// register atomics) runs beside pass B of the next (slice probes).  Results
+// equal the serial order: units touch disjoint answers and PFADD is a max.
 hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t nb, uint8_t *regs,
                               uint32_t nslots, Scratch *scr, unsigned int *err, int cus, uint32_t sub_opt,
                               int hll_mode, int pb_pairs, hipStream_t st, hipStream_t side, hipEvent_t *ev,
@@ -1088,26 +1086,50 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
     if (nmax == 0) return hipSuccess;
     hipError_t e = part_scratch(&A, nmax, sub, scr);
     if (e != hipSuccess) return e;
+    // (set 1 too, even when not pipelined: see part_reserve)
     uint8_t *fail0 = A.fail;
     uint32_t *hllw0 = A.hllw;
     uint8_t *fail1 = nullptr;
     uint32_t *hllw1 = nullptr;
-    if (side) {
-        e = part_scratch_c(&A, uint32_t(nmax < sub ? nmax : sub), 1, scr);
-        if (e != hipSuccess) return e;
-        fail1 = A.fail;
-        hllw1 = A.hllw;
-    }
+    e = part_scratch_c(&A, uint32_t(nmax < sub ? nmax : sub), 1, scr);
+    if (e != hipSuccess) return e;
+    fail1 = A.fail;
+    hllw1 = A.hllw;
     A.regs = regs;
     A.nslots = nslots;
     A.err = err;
     const uint32_t km = part_km(A.ksum);
-    uint32_t u = 0;
 #define SKE_CK(x)                        \
     do {                                 \
         hipError_t e_ = (x);             \
         if (e_ != hipSuccess) return e_; \
     } while (0)
+    // pass C of unit u - 1 (with its arguments) waits for pass A of unit u:
+    // it then runs beside pass B of unit u (slice probes, one block per CU)
+    // and not beside pass A (whose two blocks per CU fill the register file)
+    PartArgs prev{};
+    uint32_t prev_ms = 0;
+    bool have_prev = false;
+    auto launch_c = [&](const PartArgs &P, uint32_t ms, hipStream_t sc) -> hipError_t {
+        if (hook) hook(hook_user, 2, 0, sc);
+        if (hll_mode == 1) {
+            // PFADD by owned register lines: C2, S, D, E (timed together as pass C)
+            HllArgs H{};
+            hipError_t e2 = hll_scratch(&H, ms, scr);
+            if (e2 != hipSuccess) return e2;
+            hipLaunchKernelGGL(k_part_c2, dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(kPaBlock), 0,
+                               sc, P, H);
+            hipLaunchKernelGGL(k_part_hscan, dim3(kH1), dim3(1024), 0, sc, H);
+            hipLaunchKernelGGL(k_part_hd, dim3(unsigned(cus) * 2), dim3(1024), 0, sc, H);
+            hipLaunchKernelGGL(k_part_he, dim3(unsigned(cus) * 2), dim3(kHeBlock), 0, sc, P, H);
+        } else {
+            const unsigned gc = (part_grid(ms, kPcBlock * 2, cus * 8) + kPGroups - 1) / kPGroups * kPGroups;
+            hipLaunchKernelGGL(k_part_c<2>, dim3(gc), dim3(kPcBlock), 0, sc, P);
+        }
+        if (hook) hook(hook_user, 2, 1, sc);
+        return hipGetLastError();
+    };
+    uint32_t u = 0;
     for (uint32_t j = 0; j < nb; j++) {
         const PartBatch &B = bt[j];
         for (uint64_t s0 = 0; s0 < B.n; s0 += sub, u++) {
@@ -1122,6 +1144,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             A.offs = B.offs ? B.offs + s0 : nullptr;
             A.slot = B.slot + s0;
             A.out = B.out ? B.out + s0 : nullptr;
+            // pass C of unit u - 2 was the last reader of this scratch set
             if (side && u >= 2) SKE_CK(hipStreamWaitEvent(st, ev[2 + set], 0));
             const unsigned per_cu = km <= 11 ? 2 : 1;
             const unsigned ga = unsigned(cus) * per_cu / kPGroups * kPGroups;  // blocks past a group's tiles exit
@@ -1133,6 +1156,12 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             else
                 hipLaunchKernelGGL((k_part_a<22, false>), dim3(ga), dim3(kPaBlock), 0, st, A);
             if (hook) hook(hook_user, 0, 1, st);
+            if (side && have_prev) {  // C(u - 1) behind A(u) (and so behind B(u - 1))
+                SKE_CK(hipEventRecord(ev[set], st));
+                SKE_CK(hipStreamWaitEvent(side, ev[set], 0));
+                SKE_CK(launch_c(prev, prev_ms, side));
+                SKE_CK(hipEventRecord(ev[2 + (set ^ 1)], side));
+            }
             // all blocks resident, each an equal share of (slice unit, tile); a
             // one-link chain is probed in slice pairs (128 KiB images, one block
             // per CU): runs twice as long per tile
@@ -1144,32 +1173,24 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             else
                 hipLaunchKernelGGL(k_part_b<1>, dim3(gb), dim3(kPbBlock), 0, st, A);
             if (hook) hook(hook_user, 1, 1, st);
-            hipStream_t sc = st;
             if (side) {
-                SKE_CK(hipEventRecord(ev[set], st));
-                SKE_CK(hipStreamWaitEvent(side, ev[set], 0));
-                sc = side;
-            }
-            if (hook) hook(hook_user, 2, 0, sc);
-            if (hll_mode == 1) {
-                // PFADD by owned register lines: C2, S, D, E (timed together as pass C)
-                HllArgs H{};
-                SKE_CK(hll_scratch(&H, ms, scr));
-                hipLaunchKernelGGL(k_part_c2, dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(kPaBlock), 0,
-                                   sc, A, H);
-                hipLaunchKernelGGL(k_part_hscan, dim3(kH1), dim3(1024), 0, sc, H);
-                hipLaunchKernelGGL(k_part_hd, dim3(unsigned(cus) * 2), dim3(1024), 0, sc, H);
-                hipLaunchKernelGGL(k_part_he, dim3(unsigned(cus) * 2), dim3(kHeBlock), 0, sc, A, H);
+                prev = A;
+                prev_ms = ms;
+                have_prev = true;
             } else {
-                const unsigned gc = (part_grid(ms, kPcBlock * 2, cus * 8) + kPGroups - 1) / kPGroups * kPGroups;
-                hipLaunchKernelGGL(k_part_c<2>, dim3(gc), dim3(kPcBlock), 0, sc, A);
+                SKE_CK(launch_c(A, ms, st));
             }
-            if (hook) hook(hook_user, 2, 1, sc);
-            if (side) SKE_CK(hipEventRecord(ev[2 + set], side));
             SKE_CK(hipGetLastError());
         }
     }
-    if (side && u) SKE_CK(hipStreamWaitEvent(st, ev[2 + ((u - 1) & 1)], 0));
+    if (side && have_prev) {  // the last unit's pass C behind its pass B, then join
+        const int set = int((u - 1) & 1);
+        SKE_CK(hipEventRecord(ev[set], st));
+        SKE_CK(hipStreamWaitEvent(side, ev[set], 0));
+        SKE_CK(launch_c(prev, prev_ms, side));
+        SKE_CK(hipEventRecord(ev[2 + set], side));
+        SKE_CK(hipStreamWaitEvent(st, ev[2 + set], 0));
+    }
 #undef SKE_CK
     return hipGetLastError();
 }

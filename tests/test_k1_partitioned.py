@@ -215,7 +215,8 @@ def test_partitioned_hot_register_and_many_keys(engine, orc, hll_mode):
 @pytest.mark.parametrize("mode", ["direct", "graph"])
 def test_many_pipelined_small_units(engine, orc, mode):
     """ske_swipes_many_async through the partitioned K1 with pass C of every
-    unit on a side stream beside the next unit's passes A / B: sub-batches of
+    unit on a side stream beside the next unit's pass B (option part_overlap):
+    sub-batches of
     64k swipes make ~25 units over 7 ragged batches (incl. 1 swipe and a
     partial tile), so the two scratch sets alternate many times; answers and
     registers == the oracle over the batches in order."""
@@ -223,6 +224,7 @@ def test_many_pipelined_small_units(engine, orc, mode):
     from rtsas_amd.engine import DeviceBuffer
     w, p = _c3_small(engine)
     engine.set_option("part_sub", 65536)
+    engine.set_option("part_overlap", 1)
     sizes = [300_000, 1, 70_001, 300_000, 250_000, 2048, 400_000]
     bs, start = [], 0
     for n in sizes:
