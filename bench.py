@@ -271,9 +271,11 @@ def pass_bytes(n, nvalid, probes, width, fixed, geometry, lds_k1=False, slab_byt
     return {
         # one kernel: ids + offsets + slot + answer streamed, one sector per
         # RedisBloom probe, one sector read + one written per valid swipe
-        "k1": (n * (width + s_off + 4 + 1) + filter_bytes * cus
+        "k1": (n * (width + s_off + 4 + 1)
                + (128 * nvalid if slab_bytes > MALL_BYTES else 0)) if lds_k1 else
               n * (width + s_off + 4 + 1) + 64 * probes + 128 * nvalid,
+        # the LDS K1 stages the filter into every block's LDS once per launch
+        "k1_stage": filter_bytes * cus if lds_k1 else 0,
         # ids + offsets in; probe records, run table, HLL word, fail byte out
         "k_part_a": n * (width + s_off) + rec + 4 * (nslices + 1) * ntiles + 4 * n + n * len(geometry),
         # probe records + their run boundaries in, the filter staged once
@@ -430,15 +432,16 @@ def main():
         if cnt:
             mean = ms / cnt
             name = PASS_NAMES[i]
-            # a persistent launch covers several steps
-            ab = alg[name] * (args.steps / cnt if (persistent and name == "k1") else 1)
+            # a persistent launch covers several steps and stages the filter once
+            ab = (alg[name] * (args.steps / cnt if (persistent and name == "k1") else 1)
+                  + (alg["k1_stage"] if name == "k1" else 0))
             passes[name] = {"ms": mean, "launches": cnt, "alg_bytes": ab,
                             "GBps": ab / (mean * 1e-3) / 1e9}
     if passes:
         dom = max(passes, key=lambda k: passes[k]["ms"])
         kern_ms, dom_bytes = passes[dom]["ms"], passes[dom]["alg_bytes"]
     else:  # graph replay: the launch time is the replay's events / steps
-        dom, kern_ms, dom_bytes = "k1", step_ms, alg["k1"]
+        dom, kern_ms, dom_bytes = "k1", step_ms, alg["k1"] + alg["k1_stage"]
     achieved = dom_bytes / (kern_ms * 1e-3) / 1e9
     # HBM-side bytes per launch of that kernel from the committed rocprofv3 PMC
     # passes of this workload (FETCH_SIZE + WRITE_SIZE, separate passes), or null
