@@ -12,7 +12,6 @@ run() {  # name, env
   python -c "import json;d=json.load(open('gpurun_out/ab3_$1.json'));r=d['roofline'];print('$1', round(d['value']/1e9,2), 'G/s ms/step', round(d['ms_per_step'],4), {k:round(v['ms'],4) for k,v in r['passes'].items()})"
 }
 for rep in 1 2; do
-  run base$rep "SKE_LIB=tools/ab/libsketch_base.so" "--persistent 0"
-  run new$rep "X=1" "--persistent 0"
-  run pipe$rep "X=1" ""
+  run base$rep "SKE_LIB=tools/ab/libsketch_base.so" ""
+  run new$rep "X=1" ""
 done
