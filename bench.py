@@ -75,6 +75,10 @@ def parse():
     ap.add_argument("--hll-mode", type=int, default=-1,
                     help="partitioned K1 PFADD: 0 = CAS on the slab, 1 = owned register lines "
                          "(-1: library default)")
+    ap.add_argument("--exchange", type=int, default=0,
+                    help="1 = unpartitioned input: every rank's batches span ALL keys and a step "
+                         "routes them to the key owners with all_to_all_single "
+                         "(distributed.SwipeExchange), runs K1 there and returns the answers")
     ap.add_argument("--pb-pairs", type=int, default=-1,
                     help="partitioned K1 pass B: 1 = slice pairs (128 KiB images), 0 = single "
                          "slices (-1: library default)")
@@ -312,6 +316,12 @@ def main():
 
     w_all = synthetic.WORKLOADS[args.config]
     w = synthetic.shard(w_all, world)
+    w_gen = w
+    if args.exchange:
+        # unpartitioned input: the stream spans every key; this rank's slab
+        # holds the keys it owns (slot s -> rank s % world, local slot s // world)
+        w_gen = synthetic.Workload(**{**w_all.__dict__, "step_swipes": w.step_swipes})
+        w = synthetic.Workload(**{**w.__dict__, "n_keys": -(-w_all.n_keys // world)})
     n = args.batch or w.step_swipes
     engine = SketchEngine(local)
     stream = torch.cuda.Stream()  # a dedicated stream shared by libsketch and torch
@@ -330,14 +340,14 @@ def main():
     # Bloom preload (replicated on every rank), this rank's HLL key shard, and
     # 64 spare slots for the verification batch
     engine.reserve(0, w.bf_error, w.bf_capacity)
-    p = engine.gen_params(w)
+    p = engine.gen_params(w_gen)
     t0 = time.perf_counter()
     engine.preload(0, p, w.n_members)
     preload_s = time.perf_counter() - t0
     engine.hll_reserve(w.n_keys + 64)
     variant = engine.variant(0)
     lds_k1 = variant == 1
-    persistent = bool(args.persistent if args.persistent >= 0 else lds_k1)
+    persistent = bool(args.persistent if args.persistent >= 0 else lds_k1) and not args.exchange
     if lds_k1:
         engine.set_option("k1_persistent", 1 if persistent else 0)
     streams_n = 1 if persistent else (args.streams or (16 if lds_k1 else 1))
@@ -356,7 +366,22 @@ def main():
     fixed = args.layout == "fixed"
     streams = [stream] + [torch.cuda.Stream() for _ in range(max(0, streams_n - 1))]
 
+    ex, xviews = None, []
+    if args.exchange:
+        from rtsas_amd.distributed import SwipeExchange, engine_k1
+
+        def tview(ptr, shape, typestr):  # zero-copy torch view of a library buffer
+            class _V:
+                __cuda_array_interface__ = {"shape": shape, "typestr": typestr, "data": (ptr, False),
+                                            "version": 3, "strides": None}
+            return torch.as_tensor(_V(), device=dev)
+        ex = SwipeExchange(rank, world, engine_k1(engine), engine=engine)
+        xviews = [(tview(b.bytes.ptr, (n, width), "|u1"), tview(b.slot.ptr, (n,), "<i4")) for b in batches]
+
     def step(j):
+        if ex is not None:
+            ex.swipes(*xviews[j % nb])
+            return
         if len(streams) > 1:
             engine.set_stream(streams[j % len(streams)].cuda_stream)
         if fixed:
@@ -506,6 +531,8 @@ def main():
                    "k1_variant": {0: "global-bloom", 1: "lds-bloom", 2: "xcd-regions",
                                   3: "partitioned"}[variant],
                    "layout": args.layout, "streams": len(streams),
+                   "input": ("unpartitioned: alltoallv to the key owners per step"
+                             if args.exchange else "routed to the key owners at ingest"),
                    "launch": ("hip-graph" if graph is not None else
                               ("persistent (one K1 launch per 48 steps)" if lds_k1 else
                                "one many-batch call (pass C of a step beside passes A/B of the next)")

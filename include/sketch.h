@@ -199,6 +199,21 @@ int ske_swipes_fixed(ske_ctx *ctx, uint32_t fid, const uint32_t *slot, const uin
                      uint32_t width, uint64_t n, uint8_t *out_valid, int mem);
 int ske_swipes_fixed_async(ske_ctx *ctx, uint32_t fid, const uint32_t *slot,
                            const uint8_t *bytes, uint32_t width, uint64_t n, uint8_t *out_valid);
+/* Swipes that arrive NOT partitioned by key owner (one
+ * alltoallv per batch; distributed.SwipeExchange; no reference counterpart --
+ * the reference's Shared subscription hands any event to any consumer,
+ * attendance_processor.py:30-34).  Device pointers.  Swipe i (fixed-width id,
+ * GLOBAL key slot s) goes to rank s % world as local slot s / world:
+ * send_ids / send_slots are filled owner by owner (the alltoallv input),
+ * pos[i] = the swipe's position there, counts[o] (host) = swipes for owner o
+ * (the split sizes; the call synchronizes the context stream for them).
+ * world <= 64, n < 2^32. */
+int ske_route_swipes(ske_ctx *ctx, const uint8_t *ids, uint32_t width, const uint32_t *slot, uint64_t n,
+                     uint32_t world, uint8_t *send_ids, uint32_t *send_slots, uint32_t *pos, uint64_t *counts);
+/* out[i] = answers[pos[i]]: the owners' BF.EXISTS answers, received back in
+ * send order, into input order (enqueue only). */
+int ske_route_return_async(ske_ctx *ctx, const uint8_t *answers, const uint32_t *pos, uint64_t n,
+                           uint8_t *out);
 /* Several device-resident batches in one call (enqueue only, graph-capturable):
  * batch j runs on branch j mod `branches` (0: SKE_MANY_DEFAULT_BRANCHES), each
  * branch a side stream forked from and joined back into the context stream.

@@ -1270,6 +1270,29 @@ int ske_swipes_many_async(ske_ctx *c, uint32_t fid, const ske_swipe_batch *b, ui
     return rc;
 }
 
+int ske_route_swipes(ske_ctx *c, const uint8_t *ids, uint32_t width, const uint32_t *slot, uint64_t n,
+                     uint32_t world, uint8_t *send_ids, uint32_t *send_slots, uint32_t *pos, uint64_t *counts) {
+    if (!c || !counts || world == 0 || world > 64 || width == 0 || width > 4096 || n >= (uint64_t(1) << 32))
+        return SKE_EINVAL;
+    if (n && (!ids || !slot || !send_ids || !send_slots || !pos)) return SKE_EINVAL;
+    hipError_t e = hipSuccess;
+    uint32_t *hist = (uint32_t *)scratch_get(c->scratch, 40, route_hist_words(n, world) * 4 + 4, &e);
+    uint32_t *tot = e == hipSuccess ? (uint32_t *)scratch_get(c->scratch, 41, size_t(world) * 4, &e) : nullptr;
+    if (e != hipSuccess) return scratch_error(c, e);
+    HIPCHK(c, launch_route(ids, width, slot, n, world, send_ids, send_slots, pos, hist, tot, c->st));
+    uint32_t h[64];
+    HIPCHK(c, hipMemcpyAsync(h, tot, size_t(world) * 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    for (uint32_t o = 0; o < world; o++) counts[o] = h[o];
+    return SKE_OK;
+}
+
+int ske_route_return_async(ske_ctx *c, const uint8_t *answers, const uint32_t *pos, uint64_t n, uint8_t *out) {
+    if (!c || (n && (!answers || !pos || !out))) return SKE_EINVAL;
+    HIPCHK(c, launch_route_return(answers, pos, n, out, c->cus, c->st));
+    return SKE_OK;
+}
+
 int ske_swipes_fixed_async(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *bytes,
                            uint32_t width, uint64_t n, uint8_t *out_valid) {
     if (!c || !slot || width == 0 || width > 4096) return SKE_EINVAL;

@@ -79,6 +79,14 @@ struct K1Many {
 uint32_t k1_many_tile(int tile);  // swipes per tile of the many kernel
 hipError_t launch_swipes_lds_many(const K1Args &A, const K1Many &M, int tile, int cus, hipStream_t st);
 
+// sketch_route.hip -- unpartitioned swipes to their key owners (alltoallv halves)
+hipError_t launch_route(const uint8_t *ids, uint32_t width, const uint32_t *slot, uint64_t n, uint32_t world,
+                        uint8_t *sids, uint32_t *sslot, uint32_t *pos, uint32_t *hist, uint32_t *tot,
+                        hipStream_t st);
+uint64_t route_hist_words(uint64_t n, uint32_t world);
+hipError_t launch_route_return(const uint8_t *ans, const uint32_t *pos, uint64_t n, uint8_t *out, int cus,
+                               hipStream_t st);
+
 // fills A's chain fields; false when the chain does not fit this variant
 bool k1_lds_plan(const ChainDev &ch, K1Args *A);
 hipError_t launch_swipes_lds(const K1Args &A, bool hll, int tile, int cus, hipStream_t st);
@@ -149,7 +157,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
 
 // sketch_order.hip -- order-exact paths (replies that depend on item order)
 struct Scratch;  // growable device scratch, owned by the context
-constexpr int kScratchSlots = 40;
+constexpr int kScratchSlots = 44;
 void *scratch_get(Scratch *s, int slot, size_t bytes, hipError_t *err);
 void scratch_set_recording(Scratch *s, bool on);  // slots handed out now get pinned
 void scratch_unpin(Scratch *s);                    // every graph freed: slots may grow

@@ -1,0 +1,152 @@
+// sketch_route.hip -- routing of unpartitioned swipes to their key owners
+// ("if input is not pre-partitioned, use one alltoallv per
+// batch"), the device half of distributed.SwipeExchange.
+//
+// Key slot s is owned by rank s % world as its local slot s / world.  A batch
+// of fixed-width ids and global slots is counting-sorted by owner into send
+// buffers laid out owner by owner (the alltoallv input), remembering every
+// swipe's position; after K1 on the owners and the reverse alltoallv, the
+// answers are gathered back into input order through those positions.
+//
+//   k_route_count   per block of kRtTile swipes: owner histogram -> hist[o][b]
+//   k_route_scan    exclusive scan over (owner, block), owner major -> base[o][b]
+//                   (and the per-owner totals)
+//   k_route_scatter per block: the same swipes, a rank within (owner, block)
+//                   from LDS atomics, position = base[o][b] + rank; ids and
+//                   local slots scattered there, pos[i] recorded
+//   k_route_return  out[i] = answers[pos[i]]
+//
+// The order inside an (owner, block) segment is whatever the LDS atomics
+// give -- immaterial: every swipe keeps its position, and the registers are
+// a max.  Streams of bytes, HBM bound: per swipe the id, the slot, the
+// scattered id and slot, the position (2w + 12 B), and 1 + 4 + 1 B to return.
+#include "sketch_common.h"
+#include "sketch_internal.h"
+
+namespace ske {
+
+constexpr uint32_t kRtBlock = 256;
+constexpr uint32_t kRtItems = 16;
+constexpr uint32_t kRtTile = kRtBlock * kRtItems;  // swipes per block
+constexpr uint32_t kRtMaxWorld = 64;
+
+struct RouteArgs {
+    const uint8_t *ids;    // n x width
+    const uint32_t *slot;  // global key slots
+    uint8_t *sids;         // n x width, owner major
+    uint32_t *sslot;       // local slots, owner major
+    uint32_t *pos;         // input swipe -> position in the send buffers
+    uint32_t *hist;        // [world][nblocks] counts, then bases
+    uint32_t *tot;         // [world] swipes per owner
+    uint64_t n;
+    uint32_t width, world, nblocks;
+};
+
+__global__ void __launch_bounds__(kRtBlock) k_route_count(const RouteArgs R) {
+    __shared__ uint32_t c[kRtMaxWorld];
+    const uint32_t tid = threadIdx.x;
+    if (tid < R.world) c[tid] = 0;
+    __syncthreads();
+    const uint64_t b0 = uint64_t(blockIdx.x) * kRtTile;
+#pragma unroll
+    for (uint32_t j = 0; j < kRtItems; j++) {
+        const uint64_t i = b0 + j * kRtBlock + tid;
+        if (i < R.n) atomicAdd(&c[R.slot[i] % R.world], 1u);
+    }
+    __syncthreads();
+    if (tid < R.world) R.hist[size_t(tid) * R.nblocks + blockIdx.x] = c[tid];
+}
+
+// one block: exclusive scan of hist (owner major), totals per owner
+__global__ void __launch_bounds__(1024) k_route_scan(const RouteArgs R) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t total = uint64_t(R.world) * R.nblocks;
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    for (uint64_t c0 = 0; c0 < total; c0 += 1024) {
+        const uint64_t i = c0 + tid;
+        const uint32_t v = i < total ? R.hist[i] : 0;
+        uint32_t incl = v;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wsum[wave] = incl;
+        __syncthreads();
+        uint32_t pre = carry;
+        for (uint32_t w = 0; w < wave; w++) pre += wsum[w];
+        if (i < total) R.hist[i] = pre + incl - v;
+        __syncthreads();
+        if (tid == 1023) carry = pre + incl;
+        __syncthreads();
+    }
+    // per-owner totals: the base of the next owner minus this one's
+    if (tid < R.world) {
+        const uint32_t b = R.hist[size_t(tid) * R.nblocks];
+        const uint32_t e = tid + 1 < R.world ? R.hist[size_t(tid + 1) * R.nblocks] : uint32_t(R.n);
+        R.tot[tid] = e - b;
+    }
+}
+
+__global__ void __launch_bounds__(kRtBlock) k_route_scatter(const RouteArgs R) {
+    __shared__ uint32_t c[kRtMaxWorld], base[kRtMaxWorld];
+    const uint32_t tid = threadIdx.x;
+    if (tid < R.world) {
+        c[tid] = 0;
+        base[tid] = R.hist[size_t(tid) * R.nblocks + blockIdx.x];
+    }
+    __syncthreads();
+    const uint64_t b0 = uint64_t(blockIdx.x) * kRtTile;
+#pragma unroll 4
+    for (uint32_t j = 0; j < kRtItems; j++) {
+        const uint64_t i = b0 + j * kRtBlock + tid;
+        if (i >= R.n) continue;
+        const uint32_t s = R.slot[i];
+        const uint32_t o = s % R.world;
+        const uint32_t p = base[o] + atomicAdd(&c[o], 1u);
+        R.pos[i] = p;
+        R.sslot[p] = s / R.world;
+        const uint8_t *src = R.ids + i * R.width;
+        uint8_t *dst = R.sids + uint64_t(p) * R.width;
+        if (R.width == 8) {
+            *reinterpret_cast<uint64_t *>(dst) = *reinterpret_cast<const uint64_t *>(src);
+        } else {
+            for (uint32_t k = 0; k < R.width; k++) dst[k] = src[k];
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_route_return(const uint8_t *ans, const uint32_t *pos, uint64_t n,
+                                                      uint8_t *out) {
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256)
+        out[i] = ans[pos[i]];
+}
+
+hipError_t launch_route(const uint8_t *ids, uint32_t width, const uint32_t *slot, uint64_t n, uint32_t world,
+                        uint8_t *sids, uint32_t *sslot, uint32_t *pos, uint32_t *hist, uint32_t *tot,
+                        hipStream_t st) {
+    if (world == 0 || world > kRtMaxWorld || width == 0 || n >= (uint64_t(1) << 32)) return hipErrorInvalidValue;
+    RouteArgs R{ids, slot, sids, sslot, pos, hist, tot, n, width, world,
+                uint32_t((n + kRtTile - 1) / kRtTile)};
+    if (n == 0) return hipMemsetAsync(tot, 0, size_t(world) * 4, st);
+    hipLaunchKernelGGL(k_route_count, dim3(R.nblocks), dim3(kRtBlock), 0, st, R);
+    hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(1024), 0, st, R);
+    hipLaunchKernelGGL(k_route_scatter, dim3(R.nblocks), dim3(kRtBlock), 0, st, R);
+    return hipGetLastError();
+}
+
+uint64_t route_hist_words(uint64_t n, uint32_t world) { return uint64_t(world) * ((n + kRtTile - 1) / kRtTile); }
+
+hipError_t launch_route_return(const uint8_t *ans, const uint32_t *pos, uint64_t n, uint8_t *out, int cus,
+                               hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint64_t g = (n + 255) / 256;
+    const unsigned grid = unsigned(g < uint64_t(cus) * 8 ? g : uint64_t(cus) * 8);
+    hipLaunchKernelGGL(k_route_return, dim3(grid), dim3(256), 0, st, ans, pos, n, out);
+    return hipGetLastError();
+}
+
+}  // namespace ske

@@ -157,3 +157,146 @@ class ShardedSketch:
         gathered = [torch.zeros_like(local) for _ in range(self.world)]
         self.dist.all_gather(gathered, local, group=self.group)
         return torch.cat([g.cpu() for g in gathered]).numpy()[:G].astype(np.uint64)
+
+
+class SwipeExchange:
+    """Swipes that arrive NOT partitioned by key owner ("if
+    input is not pre-partitioned, use one alltoallv per batch").
+
+    Every rank holds an arbitrary slice of the stream: fixed-width ids and
+    GLOBAL key slots.  Key slot ``s`` is owned by rank ``s % world`` as its
+    local slot ``s // world`` (dense slots spread round-robin, so Zipf-hot
+    low slots land on different ranks).  One call:
+
+      1. counting sort of the batch by owner (device: ``argsort`` of
+         ``slot % world``, ``bincount``);
+      2. ``all_to_all_single`` of the per-owner counts, then of the ids and
+         of the local slots (RCCL over xGMI; variable splits = alltoallv);
+      3. K1 on the received swipes (``k1(ids, local_slots) -> answers``);
+      4. the answers back to their origin with the reverse splits, then
+         un-permuted, so the caller gets BF.EXISTS per swipe in its own order.
+
+    The registers end up exactly as if every swipe had been sent to its
+    owner at ingest (PFADD is a per-register max).  With ``gloo`` (CPU tests,
+    or ranks rehearsed on one GPU) the collectives run on host copies.
+    """
+
+    def __init__(self, rank: int, world: int, k1, group=None, engine=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.rank, self.world, self.k1, self.group = rank, world, k1, group
+        # with an engine, device batches are sorted / returned by the native
+        # routing kernels (ske_route_swipes / ske_route_return_async,
+        # sketch_route.hip); without one (CPU tensors) by torch ops
+        self.engine = engine
+        backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
+        self.device_collectives = backend == "nccl"
+
+    def local_slot(self, slots):
+        return slots // self.world
+
+    def _a2a(self, out, inp, out_splits, in_splits):
+        if self.world == 1:  # one rank (no process group): everything is local
+            out.copy_(inp)
+            return out
+        if self.device_collectives or inp.device.type == "cpu":
+            self.dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+            return out
+        o = out.cpu()
+        self.dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
+        out.copy_(o)
+        return out
+
+    def swipes(self, ids, slots):
+        """ids: uint8 [n, w] tensor, slots: integer [n] tensor of global key
+        slots (same device).  Returns uint8 [n] answers in the input order."""
+        if self.engine is not None and ids.is_cuda:
+            return self._swipes_native(ids, slots)
+        torch = self.torch
+        n, w = ids.shape
+        dest = (slots % self.world).to(torch.int64)
+        order = torch.argsort(dest, stable=True)
+        send = torch.bincount(dest, minlength=self.world)
+        recv = self._a2a(torch.empty_like(send), send, None, None)
+        ins = send.cpu().tolist()
+        outs = recv.cpu().tolist()
+        m = int(sum(outs))
+        # (16 zero bytes past the received ids: K1's short-id loads may read them)
+        r_flat = torch.zeros(m * w + 16, dtype=torch.uint8, device=ids.device)
+        r_ids = r_flat[:m * w].view(m, w)
+        self._a2a(r_flat[:m * w], ids[order].reshape(-1), [c * w for c in outs], [c * w for c in ins])
+        r_slots = torch.empty(m, dtype=torch.int32, device=ids.device)
+        self._a2a(r_slots, self.local_slot(slots[order]).to(torch.int32), outs, ins)
+        r_ans = self.k1(r_ids, r_slots)
+        back = torch.empty(n, dtype=torch.uint8, device=ids.device)
+        self._a2a(back, r_ans.to(torch.uint8), ins, outs)
+        ans = torch.empty_like(back)
+        ans[order] = back
+        return ans
+
+    def _swipes_native(self, ids, slots):
+        torch = self.torch
+        n, w = ids.shape
+        dev = ids.device
+        ids = ids.contiguous()
+        slots32 = slots.to(torch.int32).contiguous()
+        sids = torch.empty(n * w, dtype=torch.uint8, device=dev)
+        sslot = torch.empty(n, dtype=torch.int32, device=dev)
+        pos = torch.empty(n, dtype=torch.int32, device=dev)
+        counts = np.zeros(self.world, np.uint64)
+        eng = self.engine
+        eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        eng.ctx.call("ske_route_swipes", C.c_void_p(ids.data_ptr()), w, C.c_void_p(slots32.data_ptr()), n,
+                     self.world, C.c_void_p(sids.data_ptr()), C.c_void_p(sslot.data_ptr()),
+                     C.c_void_p(pos.data_ptr()), counts.ctypes.data_as(C.c_void_p))
+        send = torch.from_numpy(counts.astype(np.int64))
+        if self.device_collectives:
+            send = send.to(dev)
+        recv = self._a2a(torch.empty_like(send), send, None, None)
+        ins = [int(c) for c in counts]
+        outs = recv.cpu().tolist()
+        m = int(sum(outs))
+        r_flat = torch.zeros(m * w + 16, dtype=torch.uint8, device=dev)
+        r_ids = r_flat[:m * w].view(m, w)
+        self._a2a(r_flat[:m * w], sids, [c * w for c in outs], [c * w for c in ins])
+        r_slots = torch.empty(m, dtype=torch.int32, device=dev)
+        self._a2a(r_slots, sslot, outs, ins)
+        r_ans = self.k1(r_ids, r_slots)
+        back = torch.empty(n, dtype=torch.uint8, device=dev)
+        self._a2a(back, r_ans.to(torch.uint8), ins, outs)
+        ans = torch.empty(n, dtype=torch.uint8, device=dev)
+        eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        eng.ctx.call("ske_route_return_async", C.c_void_p(back.data_ptr()), C.c_void_p(pos.data_ptr()), n,
+                     C.c_void_p(ans.data_ptr()))
+        return ans
+
+
+class _Ptr:
+    def __init__(self, p: int):
+        self.ptr = p
+
+
+class _FixedBatch:
+    """A fixed-width batch over torch tensors, as the engine's K1 calls read it."""
+
+    def __init__(self, ids, slots):
+        self.n, self.width = int(ids.shape[0]), int(ids.shape[1])
+        self.bytes, self.slot = _Ptr(ids.data_ptr()), _Ptr(slots.data_ptr())
+
+
+def engine_k1(engine, fid: int = 0):
+    """``SwipeExchange``'s K1 on this rank's GPU: the received fixed-width ids
+    and local slots (device tensors; the ids' storage has 16 readable bytes
+    past the last id) through ske_swipes_fixed_async on torch's current
+    stream."""
+    import torch
+
+    def k1(ids, slots):
+        out = torch.empty(ids.shape[0], dtype=torch.uint8, device=ids.device)
+        if ids.shape[0]:
+            engine.set_stream(torch.cuda.current_stream(ids.device).cuda_stream)
+            engine.swipes_fixed_async(fid, _FixedBatch(ids, slots.contiguous()), _Ptr(out.data_ptr()))
+        return out
+
+    return k1

@@ -1,0 +1,57 @@
+"""One rank of test_exchange_gpu.py (run under torch.distributed.run, gloo,
+every rank on this box's GPU): a slice of a C2-shaped stream over GLOBAL key
+slots, routed to the key owners by distributed.SwipeExchange, K1 on the
+device per rank.  Saves the answers (input order), this rank's registers and
+its stream for the parent's oracle check."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+NK, N = 37, 400_000
+
+
+def workload():
+    from rtsas_amd import synthetic
+    w = synthetic.WORKLOADS["c2"]
+    return synthetic.Workload(**{**w.__dict__, "n_keys": NK})
+
+
+def main(out_dir):
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__ as ge
+    ge.load_package()
+    from rtsas_amd.distributed import SwipeExchange, engine_k1
+    from rtsas_amd.engine import SketchEngine
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    w = workload()
+    eng = SketchEngine(0)
+    eng.reserve(0, w.bf_error, w.bf_capacity)
+    p = eng.gen_params(w)
+    eng.preload(0, p, w.n_members)
+    nlocal = -(-NK // world)
+    eng.hll_reserve(nlocal)
+    n = N - 1000 * rank                      # uneven slices
+    b = eng.swipe_batch(p, rank * N, n)
+    buf, offs, slot = b.to_host()
+    width = int(offs[1] - offs[0])
+    assert (np.diff(offs.astype(np.int64)) == width).all()
+    ids = torch.from_numpy(buf[:n * width].reshape(n, width).copy()).cuda()
+    slots = torch.from_numpy(slot.astype(np.int64)).cuda()
+    ex = SwipeExchange(rank, world, engine_k1(eng), engine=eng)
+    ans = ex.swipes(ids, slots)
+    torch.cuda.synchronize()
+    eng.sync()
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), ans=ans.cpu().numpy(), regs=eng.registers_all(nlocal),
+             buf=buf, offs=offs, slot=slot)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -1,0 +1,41 @@
+"""Unpartitioned swipes routed by alltoallv on the device path (SURVEY.md
+§8e): W ranks on this box's GPU (gloo transport; RCCL on a node), each with
+its own slice of the stream over global key slots.  distributed.SwipeExchange
+sends every swipe to its key's owner, K1 runs there, the answers come back in
+the input order.  Answers == the oracle's BF.EXISTS; every rank's registers ==
+the single-process registers of the keys it owns."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_on_device_equals_oracle(orc, engine, tmp_path, world):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from exchange_worker import NK, workload
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
+                        "--master-port", str(29650 + world), os.path.join(ROOT, "tests", "exchange_worker.py"),
+                        str(tmp_path)], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    w = workload()
+    engine.reserve(0, w.bf_error, w.bf_capacity)
+    p = engine.gen_params(w)
+    mb = engine.members_batch(p, 0, w.n_members).to_host()
+    chain = orc.Chain(w.bf_capacity, w.bf_error)
+    chain.madd_packed(mb[0], mb[1])
+    regs = np.zeros((NK, 16384), np.uint8)
+    for rk in range(world):
+        d = np.load(tmp_path / f"r{rk}.npz")
+        want, _, _ = orc.process_swipes(chain, regs, d["slot"].astype(np.uint32), d["buf"], d["offs"])
+        assert np.array_equal(d["ans"], want.astype(np.uint8)), f"rank {rk} answers"
+    for s in range(NK):
+        rr = np.load(tmp_path / f"r{s % world}.npz")["regs"]
+        assert np.array_equal(rr[s // world], regs[s]), f"slot {s}"
