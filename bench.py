@@ -46,10 +46,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # 4-byte read per lane over a 1.6 GB table -- 55 G sectors/s; the register
 # update of pass C is priced against it as well as against the HBM peak
 RANDOM_SECTOR_GPS = 55.3
-# the same tool: one random 32-bit CAS per lane over a 1.6 GB table -- 19.0 G/s
-# (device-scope atomics execute memory-side: TCC_EA0_ATOMIC); pass C's
-# register CASes are priced against it
-RANDOM_CAS_GPS = 19.0
+# tools/casbench.hip (profiles/r02_casbench.json): pass C's own operation in
+# isolation -- load a random word of a 1.6 GB table, raise one byte by a CAS on
+# it -- 21.1 G ops/s at 7.3 M ops (device-scope atomics execute memory-side:
+# TCC_EA0_ATOMIC); pass C's register CASes are priced against it
+RANDOM_CAS_GPS = 21.1
 MALL_BYTES = 256 << 20  # Infinity Cache: a slab this small stays on chip
 METRIC = "swipes/sec (fused BF.EXISTS+PFADD) at 1/2/4/8 GPUs; % of HBM peak"
 PASS_NAMES = ["k1", "k_part_a", "k_part_b", "k_part_c"]
@@ -496,7 +497,8 @@ def main():
             roofline["binding"] = {
                 "counter": "TCC_EA0_ATOMIC_sum",
                 "what": "register CASes (memory-side device atomics, PMC per dispatch) / this run's "
-                        "kernel time, against the measured random CAS rate over a 1.6 GB table",
+                        "kernel time, against the measured rate of the same load + raising CAS "
+                        "over a 1.6 GB table (tools/casbench.hip, profiles/r02_casbench.json)",
                 "atomics_per_dispatch": pmc["mean"]["TCC_EA0_ATOMIC_sum"],
                 "achieved_G_per_s": cas, "peak_G_per_s": RANDOM_CAS_GPS, "frac": cas / RANDOM_CAS_GPS}
     if dom == "k1" and pmc and "SQ_INSTS_VALU" in pmc.get("mean", {}):
