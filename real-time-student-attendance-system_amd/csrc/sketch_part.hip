@@ -300,11 +300,13 @@ constexpr uint32_t kOOR = 0x80000000u;  // a buffer offset past every range: loa
 //
 // Memory instructions are what this pass is made of (PMC: the address unit
 // busy 84 % of the time, stalled behind L1 misses, when lanes read 4-byte
-// pieces), so each one is made to move whole lines: within a slice a wave
-// takes kPbGroup consecutive tiles at a time, 8 lanes per tile run, and a
-// lane loads 16 bytes (4 records) -- one instruction reads 128 aligned-to-16
-// contiguous bytes of each of 8 runs.  Two such rounds cover a run of up to 64
-// records (about 37 at C3); longer runs finish in a tail loop.  The few failing
+// pieces), so each one is made to move whole lines: within a slice (or slice
+// pair) a wave takes kPbGroup consecutive tiles at a time, 8 lanes per tile
+// run, and a lane loads 16 bytes (4 records) -- one instruction reads one
+// whole 128-B line of each of 8 runs (pieces start at the line holding the
+// run's first record).  2*SP such pieces cover a run of up to 64*SP records
+// from its line (37 / 74 at C3 for single slices / pairs); longer runs finish
+// in a tail loop.  The few failing
 // probes (a member never fails; a non-member's probes fail about half the
 // time) are compacted through LDS so a group ends in one fail-byte store
 // instruction.  Loads and stores are buffer operations whose out-of-range
@@ -361,9 +363,10 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
             B = __builtin_amdgcn_raw_buffer_load_b32(roff, in ? (orow + t) * 4 : kOOR, 0, 0);
             E = __builtin_amdgcn_raw_buffer_load_b32(roff, in ? (erow + t) * 4 : kOOR, 0, 0);
         };
-        // 16-byte pieces qq, qq + 8, ... of the run from its 16-byte-aligned start
+        // 16-byte pieces qq, qq + 8, ... of the run from the 128-B line holding
+        // its start: every piece is one whole line (one request, not two)
         auto load_recs = [&](uint32_t tg, uint32_t b, uint32_t e, uint4 (&r)[R]) {
-            const uint32_t base = (tg + k) * A.stride, s0 = b & ~3u;
+            const uint32_t base = (tg + k) * A.stride, s0 = b & ~31u;
 #pragma unroll
             for (uint32_t c = 0; c < R; c++) {
                 const uint32_t i = s0 + c * 32 + qq * 4;
@@ -390,7 +393,7 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
             load_recs(tg + kStep, b1, e1, rn);
             // the (up to) 4R records of this lane: piece c starts at record
             // lo_c = s0 + c*32 + qq*4; bit j of vm: record j in [bc, ec)
-            const uint32_t s0 = bc & ~3u;
+            const uint32_t s0 = bc & ~31u;
             uint32_t rec[4 * R];
 #pragma unroll
             for (uint32_t c = 0; c < R; c++) {
@@ -991,7 +994,7 @@ static bool part_plan(const ChainDev &ch, PartArgs *A) {
     A->nlinks = uint32_t(ch.nlinks);
     A->nslices = slices;
     A->ksum = ksum;
-    A->stride = (kPaBlock * ksum + 3) & ~3u;
+    A->stride = (kPaBlock * ksum + 31) & ~31u;  // tiles start on 128-B lines
     return true;
 }
 
