@@ -1135,8 +1135,14 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
     uint32_t u = 0;
     for (uint32_t j = 0; j < nb; j++) {
         const PartBatch &B = bt[j];
-        for (uint64_t s0 = 0; s0 < B.n; s0 += sub, u++) {
-            const uint32_t ms = B.n - s0 < sub ? uint32_t(B.n - s0) : sub;
+        // fixed-width ids: a sub-batch's byte offsets (swipe * width) stay 32-bit
+        uint32_t subj = sub;
+        if (!B.offs && B.fixed_w) {
+            const uint64_t cap = (0xffffff00ull / B.fixed_w) / kPaBlock * kPaBlock;
+            subj = cap < sub ? uint32_t(cap < kPaBlock ? kPaBlock : cap) : sub;
+        }
+        for (uint64_t s0 = 0; s0 < B.n; s0 += subj, u++) {
+            const uint32_t ms = B.n - s0 < subj ? uint32_t(B.n - s0) : subj;
             const int set = side ? int(u & 1) : 0;
             A.fail = set ? fail1 : fail0;
             A.hllw = set ? hllw1 : hllw0;
