@@ -152,8 +152,9 @@ __device__ __forceinline__ void part_hash3(const uint8_t *bytes, const PartId &d
 // One tile = 1024 swipes, one per thread.  KM: the most probes per swipe the
 // instantiation holds (every link's k summed); records of a tile live in LDS
 // (KM = 11: 44 KiB, two blocks per CU, so one block's hashing overlaps the
-// other's sort and copy-out).
-template <int KM, bool kOneLink>
+// other's sort and copy-out).  One-link chains of k = 11 (C3/C5) take
+// k_part_a2 below.
+template <int KM>
 __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const PartArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t srec[kPaBlock * KM];
     // slice histogram, then run starts; two buffers used by alternate tiles,
@@ -205,23 +206,7 @@ __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const Par
             // a slice belongs to one link)
             // bit 29 of a record: its slice's parity (pass B's slice pairs)
             const uint32_t rbase = (tid << kPSliceLog) | 0x80000000u;
-            if constexpr (kOneLink) {  // one link of k = ksum <= KM probes, slices from 0
-                const PartLink &L = A.link[0];
-                ProbeWalk32 wk;
-                wk.init(ha, hb, part_div(L));
-#pragma unroll
-                for (int q = 0; q < KM; q++) {
-                    rp[q] = 0xffffffffu;
-                    rv[q] = 0;
-                    if (uint32_t(q) < A.ksum) {  // block-uniform
-                        const uint32_t x = wk.x;
-                        const uint32_t g = x >> kPSliceLog;
-                        rv[q] = (x & kPSliceMask) | ((g & 1u) << 29) | rbase;
-                        if (act) rp[q] = (g << 16) | atomicAdd(&scnt[g], 1u);
-                        wk.step(L.d);
-                    }
-                }
-            } else {
+            {
                 uint32_t l = A.nlinks - 1, jl = 0;
                 ProbeWalk32 wk;
                 wk.init(ha, hb, part_div(A.link[l]));
@@ -285,6 +270,120 @@ __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const Par
         uint4 *dst = reinterpret_cast<uint4 *>(A.rec + size_t(t) * A.stride);
         const uint4 *src = reinterpret_cast<const uint4 *>(srec);
         for (uint32_t j = tid; j * 4 < total; j += kPaBlock) dst[j] = src[j];
+    }
+}
+
+// The same pass A for one-link chains of exactly KM probes with half the
+// threads: a 512-thread block owns the 1024-swipe tile, two swipes per
+// thread (swipes tid and tid + 512 of the tile, the same record layout), so a
+// thread has twice the independent work between barriers and 128 VGPRs
+// (two blocks per CU, 16 waves) instead of 64 -- no spills, half the barrier
+// width.  C3: 0.315 -> 0.273 ms per 16M swipes (A/B on one box); 256 threads x
+// 4 swipes (208 VGPRs, 8 waves per CU) was slower again, 0.323 ms.
+constexpr uint32_t kA2Threads = 512;
+template <int KM, uint32_t kA2Threads = kA2Threads, uint32_t kA2U = kPaBlock / kA2Threads>
+__global__ void __launch_bounds__(kA2Threads, 2) k_part_a2(const PartArgs A) {
+    __shared__ __attribute__((aligned(16))) uint32_t srec[kPaBlock * KM];
+    __shared__ uint32_t scnt2[2][kPMaxSlices + 1];
+    __shared__ uint32_t swsum[kA2Threads / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t S = A.nslices;
+    for (uint32_t g = tid; g <= kPMaxSlices; g += kA2Threads) scnt2[0][g] = scnt2[1][g] = 0;
+    __syncthreads();
+    auto offsets = [&](uint32_t t, uint32_t u, uint32_t &b, uint32_t &e) {
+        const uint32_t i = t * kPaBlock + u * kA2Threads + tid;
+        const uint32_t ic = i < A.n ? i : A.n - 1;
+        b = A.offs ? A.offs[ic] : ic * A.fixed_w;
+        e = A.offs ? A.offs[ic + 1] : b + A.fixed_w;
+    };
+    uint32_t gt0, gt1;
+    part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
+    const uint32_t tstep = gridDim.x / kPGroups;
+    const __amdgpu_buffer_rsrc_t rbytes = part_rsrc(A.bytes, 0xfffffff0u);
+    const PartLink &L = A.link[0];
+    uint32_t par = 0, nb_[kA2U], ne_[kA2U];
+    PartId it[kA2U];
+    {
+        const uint32_t t = gt0 + blockIdx.x / kPGroups;
+#pragma unroll
+        for (uint32_t u = 0; u < kA2U; u++) {
+            offsets(t < gt1 ? t : gt0, u, nb_[u], ne_[u]);
+            part_id_load(rbytes, nb_[u], ne_[u], it[u]);
+        }
+    }
+    for (uint32_t t = gt0 + blockIdx.x / kPGroups; t < gt1; t += tstep, par ^= 1) {
+        uint32_t *scnt = scnt2[par];
+        uint32_t rv[kA2U][KM], rp[kA2U][KM];
+        bool act[kA2U];
+        const uint32_t tn = t + tstep < gt1 ? t + tstep : t;
+#pragma unroll
+        for (uint32_t u = 0; u < kA2U; u++) offsets(tn, u, nb_[u], ne_[u]);
+#pragma unroll
+        for (uint32_t u = 0; u < kA2U; u++) {
+            const uint32_t lu = u * kA2Threads + tid;
+            const uint32_t i = t * kPaBlock + lu;
+            act[u] = i < A.n;
+            uint64_t ha, hb, hh;
+            part_hash3(A.bytes, it[u], ha, hb, hh);
+            if (act[u]) {
+                uint32_t idx, rank;
+                hll_patlen(hh, idx, rank);
+                A.hllw[i] = idx | (rank << 16);
+                A.fail[i] = 0;
+            }
+            // bit 29 of a record: its slice's parity (pass B's slice pairs)
+            const uint32_t rbase = (lu << kPSliceLog) | 0x80000000u;
+            ProbeWalk32 wk;
+            wk.init(ha, hb, part_div(L));
+#pragma unroll
+            for (int q = 0; q < KM; q++) {
+                const uint32_t x = wk.x;
+                const uint32_t g = x >> kPSliceLog;
+                rv[u][q] = (x & kPSliceMask) | ((g & 1u) << 29) | rbase;
+                rp[u][q] = 0xffffffffu;
+                if (act[u]) rp[u][q] = (g << 16) | atomicAdd(&scnt[g], 1u);
+                if (q + 1 < KM) wk.step(L.d);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t u = 0; u < kA2U; u++) part_id_load(rbytes, nb_[u], ne_[u], it[u]);  // the next tile's ids
+        // exclusive scan of scnt[0..S] (scnt[S] == 0 becomes the tile's total)
+        constexpr int kPer = (kPMaxSlices + 1) / kA2Threads;
+        uint32_t v[kPer], s = 0;
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+            v[j] = scnt[tid * kPer + j];
+            s += v[j];
+        }
+        uint32_t incl = s;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= uint32_t(o)) incl += y;
+        }
+        if (lane == 63) swsum[wave] = incl;
+        __syncthreads();
+        uint32_t run = incl - s;
+        for (uint32_t w = 0; w < wave; w++) run += swsum[w];
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+            scnt[tid * kPer + j] = run;
+            run += v[j];
+        }
+        __syncthreads();
+        for (uint32_t g = tid; g <= S; g += kA2Threads) A.off[size_t(g) * A.off_stride + t] = scnt[g];
+#pragma unroll
+        for (uint32_t u = 0; u < kA2U; u++)
+#pragma unroll
+            for (int q = 0; q < KM; q++)
+                if (rp[u][q] != 0xffffffffu) srec[scnt[rp[u][q] >> 16] + (rp[u][q] & 0xffffu)] = rv[u][q];
+        for (uint32_t g = tid; g <= S; g += kA2Threads) scnt2[par ^ 1][g] = 0;
+        __syncthreads();
+        const uint32_t total = scnt[S];
+        uint4 *dst = reinterpret_cast<uint4 *>(A.rec + size_t(t) * A.stride);
+        const uint4 *src = reinterpret_cast<const uint4 *>(srec);
+        for (uint32_t j = tid; j * 4 < total; j += kA2Threads) dst[j] = src[j];
     }
 }
 
@@ -1158,12 +1257,13 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             const unsigned per_cu = km <= 11 ? 2 : 1;
             const unsigned ga = unsigned(cus) * per_cu / kPGroups * kPGroups;  // blocks past a group's tiles exit
             if (hook) hook(hook_user, 0, 0, st);
-            if (km <= 11 && A.nlinks == 1)
-                hipLaunchKernelGGL((k_part_a<11, true>), dim3(ga), dim3(kPaBlock), 0, st, A);
+            if (A.nlinks == 1 && A.ksum == 11)  // RESERVE 0.001 (C3/C5): one link, k = 11
+                hipLaunchKernelGGL((k_part_a2<11>), dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(kA2Threads),
+                                   0, st, A);
             else if (km <= 11)
-                hipLaunchKernelGGL((k_part_a<11, false>), dim3(ga), dim3(kPaBlock), 0, st, A);
+                hipLaunchKernelGGL(k_part_a<11>, dim3(ga), dim3(kPaBlock), 0, st, A);
             else
-                hipLaunchKernelGGL((k_part_a<22, false>), dim3(ga), dim3(kPaBlock), 0, st, A);
+                hipLaunchKernelGGL(k_part_a<22>, dim3(ga), dim3(kPaBlock), 0, st, A);
             if (hook) hook(hook_user, 0, 1, st);
             if (side && have_prev) {  // C(u - 1) behind A(u) (and so behind B(u - 1))
                 SKE_CK(hipEventRecord(ev[set], st));
