@@ -80,6 +80,9 @@ def parse():
                     help="1 = unpartitioned input: every rank's batches span ALL keys and a step "
                          "routes them to the key owners with all_to_all_single "
                          "(distributed.SwipeExchange), runs K1 there and returns the answers")
+    ap.add_argument("--pa-tile", type=int, default=-1,
+                    help="partitioned K1 tile: 10 = 1024 swipes, 11 = 2048 (one-link k = 11 "
+                         "chains; -1: library default)")
     ap.add_argument("--pb-pairs", type=int, default=-1,
                     help="partitioned K1 pass B: 1 = slice pairs (128 KiB images), 0 = single "
                          "slices (-1: library default)")
@@ -337,6 +340,8 @@ def main():
         engine.set_option("hll_mode", args.hll_mode)
     if args.pb_pairs >= 0:
         engine.set_option("pb_pairs", args.pb_pairs)
+    if args.pa_tile >= 0:
+        engine.set_option("pa_tile", args.pa_tile)
 
     # Bloom preload (replicated on every rank), this rank's HLL key shard, and
     # 64 spare slots for the verification batch

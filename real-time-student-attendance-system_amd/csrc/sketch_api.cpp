@@ -82,6 +82,7 @@ struct ske_ctx {
     uint32_t part_sub = 0;  // partitioned K1: swipes per sub-batch (0: default)
     int hll_mode = 0;       // partitioned K1's PFADD: 1 owned register lines, 0 CAS
     int pb_pairs = 1;       // partitioned K1 pass B over slice pairs (one-link chains)
+    int pa_tile = 10;       // partitioned K1 tile: 10 = 1024 swipes, 11 = 2048 (one-link k = 11 only)
     int part_overlap = 0;   // many-batch calls: partitioned K1 pass C on a side stream (measured slower)
     hipEvent_t part_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool lds_ok = false;
@@ -482,7 +483,7 @@ int launch_part(ske_ctx *c, const ChainDev &ch, const PartBatch *bt, uint32_t nb
     };
     c->hook_arg = pm;
     e = launch_swipes_part(ch, bt, nb, c->regs, c->nslots, c->scratch, c->err, c->cus, c->part_sub, c->hll_mode,
-                           c->pb_pairs, c->st, side, c->part_ev, c->timing && !c->capturing ? +hook : nullptr, c);
+                           c->pb_pairs, c->pa_tile, c->st, side, c->part_ev, c->timing && !c->capturing ? +hook : nullptr, c);
     if (e != hipSuccess) {
         c->last_hip = std::string("launch_swipes_part: ") + hipGetErrorString(e);
         scratch_user_end(c, cid);
@@ -726,6 +727,11 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
     if (!strcmp(name, "part_overlap")) {  // many-batch calls: overlap pass C with the next A / B
         if (value < 0 || value > 1) return SKE_EINVAL;
         c->part_overlap = int(value);
+        return SKE_OK;
+    }
+    if (!strcmp(name, "pa_tile")) {  // partitioned K1 tile: log2 swipes, 10 or 11
+        if (value != 10 && value != 11) return SKE_EINVAL;
+        c->pa_tile = int(value);
         return SKE_OK;
     }
     if (!strcmp(name, "pb_pairs")) {  // partitioned K1: pass B over slice pairs (1) or slices

@@ -32,6 +32,8 @@
 //
 // Placement of blocks on XCDs is a speed matter only; every (tile, slice) run
 // is read by exactly one block, and fail bytes are only ever set to 1.
+#include <algorithm>
+
 #include "sketch_common.h"
 #include "sketch_internal.h"
 
@@ -69,6 +71,7 @@ struct PartArgs {
     uint8_t *fail;         // [nlinks][fail_stride]
     uint32_t *hllw;        // [n] register | rank << 16
     uint32_t fixed_w, n, stride, ntiles, nslices, nlinks, ksum, nslots, fail_stride, off_stride;
+    uint32_t tile_log;     // swipes per tile = 1 << tile_log (10, or 11 for k_part_a2<11, 1024>)
     PartLink link[kPMaxLinks];
 };
 
@@ -281,9 +284,12 @@ __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const Par
 // width.  C3: 0.315 -> 0.273 ms per 16M swipes (A/B on one box); 256 threads x
 // 4 swipes (208 VGPRs, 8 waves per CU) was slower again, 0.323 ms.
 constexpr uint32_t kA2Threads = 512;
-template <int KM, uint32_t kA2Threads = kA2Threads, uint32_t kA2U = kPaBlock / kA2Threads>
-__global__ void __launch_bounds__(kA2Threads, 2) k_part_a2(const PartArgs A) {
-    __shared__ __attribute__((aligned(16))) uint32_t srec[kPaBlock * KM];
+template <int KM, uint32_t kA2Threads = kA2Threads, uint32_t kA2U = 2>
+__global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part_a2(const PartArgs A) {
+    constexpr uint32_t kTile = kA2Threads * kA2U;  // swipes per tile (1 << A.tile_log)
+    constexpr uint32_t kTileLog = kTile == 2048 ? 11 : 10;
+    static_assert(kTile == 1024 || kTile == 2048, "tile");
+    __shared__ __attribute__((aligned(16))) uint32_t srec[kTile * KM];
     __shared__ uint32_t scnt2[2][kPMaxSlices + 1];
     __shared__ uint32_t swsum[kA2Threads / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -291,7 +297,7 @@ __global__ void __launch_bounds__(kA2Threads, 2) k_part_a2(const PartArgs A) {
     for (uint32_t g = tid; g <= kPMaxSlices; g += kA2Threads) scnt2[0][g] = scnt2[1][g] = 0;
     __syncthreads();
     auto offsets = [&](uint32_t t, uint32_t u, uint32_t &b, uint32_t &e) {
-        const uint32_t i = t * kPaBlock + u * kA2Threads + tid;
+        const uint32_t i = t * kTile + u * kA2Threads + tid;
         const uint32_t ic = i < A.n ? i : A.n - 1;
         b = A.offs ? A.offs[ic] : ic * A.fixed_w;
         e = A.offs ? A.offs[ic + 1] : b + A.fixed_w;
@@ -321,7 +327,7 @@ __global__ void __launch_bounds__(kA2Threads, 2) k_part_a2(const PartArgs A) {
 #pragma unroll
         for (uint32_t u = 0; u < kA2U; u++) {
             const uint32_t lu = u * kA2Threads + tid;
-            const uint32_t i = t * kPaBlock + lu;
+            const uint32_t i = t * kTile + lu;
             act[u] = i < A.n;
             uint64_t ha, hb, hh;
             part_hash3(A.bytes, it[u], ha, hb, hh);
@@ -331,7 +337,7 @@ __global__ void __launch_bounds__(kA2Threads, 2) k_part_a2(const PartArgs A) {
                 A.hllw[i] = idx | (rank << 16);
                 A.fail[i] = 0;
             }
-            // bit 29 of a record: its slice's parity (pass B's slice pairs)
+            // bit 19 + tile_log of a record: its slice's parity (pass B's pairs)
             const uint32_t rbase = (lu << kPSliceLog) | 0x80000000u;
             ProbeWalk32 wk;
             wk.init(ha, hb, part_div(L));
@@ -339,7 +345,7 @@ __global__ void __launch_bounds__(kA2Threads, 2) k_part_a2(const PartArgs A) {
             for (int q = 0; q < KM; q++) {
                 const uint32_t x = wk.x;
                 const uint32_t g = x >> kPSliceLog;
-                rv[u][q] = (x & kPSliceMask) | ((g & 1u) << 29) | rbase;
+                rv[u][q] = (x & kPSliceMask) | ((g & 1u) << (kPSliceLog + kTileLog)) | rbase;
                 rp[u][q] = 0xffffffffu;
                 if (act[u]) rp[u][q] = (g << 16) | atomicAdd(&scnt[g], 1u);
                 if (q + 1 < KM) wk.step(L.d);
@@ -415,9 +421,9 @@ constexpr uint32_t kOOR = 0x80000000u;  // a buffer offset past every range: loa
 // tested.
 constexpr uint32_t kPbQueue = 64;  // compacted fail stores per wave and group
 
-template <int SP>
+template <int SP, int R = 2 * SP>  // R: 16-byte pieces per lane and run (runs of SP slices)
 __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const PartArgs A) {
-    constexpr uint32_t R = 2 * SP;  // 16-byte pieces per lane and run (runs of SP slices)
+    const uint32_t tmask = (1u << A.tile_log) - 1;
     __shared__ __attribute__((aligned(16))) uint8_t img[kPSliceBytes * SP];
     __shared__ uint32_t fq[kPbBlock / 64][kPbQueue];
     // this block's share of its group's (slice, tile) space, slice major
@@ -518,13 +524,13 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
 #pragma unroll
             for (uint32_t j = 0; j < 4 * R; j++) {
                 const uint32_t rr = rec[j];
-                const uint32_t o = SP == 1 ? (rr & kPSliceMask) : ((rr & kPSliceMask) | ((rr >> 10) & kPSliceBits));
+                const uint32_t o = SP == 1 ? (rr & kPSliceMask) : ((rr & kPSliceMask) | ((rr >> A.tile_log) & kPSliceBits));
                 okm |= __builtin_amdgcn_ubfe(img32[o >> 5], rr & 31, 1) << j;
             }
             uint32_t fm = vm & ~okm;
             // compact the failing swipes of the wave: this lane's count, the
             // wave's exclusive prefix, one store instruction per 64 of them
-            const uint32_t tbase = (tg + k) * kPaBlock;
+            const uint32_t tbase = (tg + k) << A.tile_log;
             const uint32_t cnt = __builtin_popcount(fm);
             uint32_t incl = cnt;
 #pragma unroll
@@ -540,7 +546,7 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                 uint32_t rr = rec[0];
 #pragma unroll
                 for (uint32_t jj = 1; jj < 4 * R; jj++) rr = j == jj ? rec[jj] : rr;
-                const uint32_t at = tbase + ((rr >> kPSliceLog) & (kPaBlock - 1));
+                const uint32_t at = tbase + ((rr >> kPSliceLog) & tmask);
                 if (pos < kPbQueue) q[pos] = at;
                 else __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail, at, 0, 0);  // overflow
                 pos++;
@@ -555,10 +561,10 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                 const uint32_t base = (tg + k) * A.stride;
                 for (uint32_t i = s0 + 32 * R + qq; i < ec; i += kPbLanes) {
                     const uint32_t rr = __builtin_amdgcn_raw_buffer_load_b32(rrec, (base + i) * 4, 0, 0);
-                    const uint32_t o = SP == 1 ? (rr & kPSliceMask) : ((rr & kPSliceMask) | ((rr >> 10) & kPSliceBits));
+                    const uint32_t o = SP == 1 ? (rr & kPSliceMask) : ((rr & kPSliceMask) | ((rr >> A.tile_log) & kPSliceBits));
                     if (!((img[o >> 3] >> (o & 7)) & 1))
                         __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail,
-                                                             tbase + ((rr >> kPSliceLog) & (kPaBlock - 1)), 0, 0);
+                                                             tbase + ((rr >> kPSliceLog) & tmask), 0, 0);
                 }
             }
 #pragma unroll
@@ -585,9 +591,10 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
     const uint32_t T = kPcBlock, tid = threadIdx.x;
     uint32_t gt0, gt1;
     part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
-    const uint64_t end = uint64_t(gt1) * kPaBlock < A.n ? uint64_t(gt1) * kPaBlock : A.n;
+    const uint64_t tile = uint64_t(1) << A.tile_log;
+    const uint64_t end = uint64_t(gt1) * tile < A.n ? uint64_t(gt1) * tile : A.n;
     const uint64_t stride = uint64_t(gridDim.x / kPGroups) * T * U;
-    for (uint64_t base = uint64_t(gt0) * kPaBlock + uint64_t(blockIdx.x / kPGroups) * T * U; base < end;
+    for (uint64_t base = uint64_t(gt0) * tile + uint64_t(blockIdx.x / kPGroups) * T * U; base < end;
          base += stride) {
         bool valid[U];
         uint32_t *w[U];
@@ -1071,6 +1078,9 @@ static uint32_t part_km(uint32_t ksum) {
     return 0;
 }
 
+// records per tile, rounded so tiles start on 128-B lines
+static uint32_t part_stride(uint32_t ksum, uint32_t tile_log) { return ((ksum << tile_log) + 31) & ~31u; }
+
 static bool part_plan(const ChainDev &ch, PartArgs *A) {
     if (ch.nlinks < 1 || ch.nlinks > kPMaxLinks) return false;
     uint32_t slices = 0, ksum = 0;
@@ -1093,7 +1103,8 @@ static bool part_plan(const ChainDev &ch, PartArgs *A) {
     A->nlinks = uint32_t(ch.nlinks);
     A->nslices = slices;
     A->ksum = ksum;
-    A->stride = (kPaBlock * ksum + 31) & ~31u;  // tiles start on 128-B lines
+    A->tile_log = 10;
+    A->stride = part_stride(ksum, 10);
     return true;
 }
 
@@ -1122,11 +1133,14 @@ static hipError_t hll_scratch(HllArgs *H, uint32_t m, Scratch *scr) {
 
 static hipError_t part_scratch(PartArgs *A, uint64_t n, uint32_t sub, Scratch *scr) {
     const uint32_t m = n < sub ? uint32_t(n) : sub;
+    // sized for either tile size (1024 or 2048 swipes; the launcher picks)
     const uint32_t ntiles_max = (m + kPaBlock - 1) / kPaBlock;
+    const uint64_t rec_words = std::max<uint64_t>(uint64_t(ntiles_max) * part_stride(A->ksum, 10),
+                                                  uint64_t((m + 2047) / 2048) * part_stride(A->ksum, 11));
     const uint32_t fstride = (m + 255) & ~255u;
     A->off_stride = (ntiles_max + 15) & ~15u;
     hipError_t e = hipSuccess;
-    A->rec = (uint32_t *)scratch_get(scr, 28, size_t(ntiles_max) * A->stride * 4, &e);
+    A->rec = (uint32_t *)scratch_get(scr, 28, size_t(rec_words) * 4, &e);
     if (e == hipSuccess) A->off = (uint32_t *)scratch_get(scr, 29, size_t(A->off_stride) * (A->nslices + 1) * 4, &e);
     if (e == hipSuccess) A->fail = (uint8_t *)scratch_get(scr, 30, size_t(fstride) * A->nlinks, &e);
     if (e == hipSuccess) A->hllw = (uint32_t *)scratch_get(scr, 31, size_t(m) * 4, &e);
@@ -1178,8 +1192,8 @@ hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratc
 // equal the serial order: units touch disjoint answers and PFADD is a max.
 hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t nb, uint8_t *regs,
                               uint32_t nslots, Scratch *scr, unsigned int *err, int cus, uint32_t sub_opt,
-                              int hll_mode, int pb_pairs, hipStream_t st, hipStream_t side, hipEvent_t *ev,
-                              PassHook hook, void *hook_user) {
+                              int hll_mode, int pb_pairs, int tile_opt, hipStream_t st, hipStream_t side,
+                              hipEvent_t *ev, PassHook hook, void *hook_user) {
     PartArgs A{};
     if (!part_plan(ch, &A)) return hipErrorInvalidValue;
     const uint32_t sub = part_sub(sub_opt);
@@ -1201,6 +1215,13 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
     A.nslots = nslots;
     A.err = err;
     const uint32_t km = part_km(A.ksum);
+    // tiles of 1024 swipes; tile_opt 11: 2048 for a one-link k = 11 chain
+    // (k_part_a2<11, 1024>, one block per CU): pass B's runs twice as long
+    // (0.287 -> 0.26 ms at C3) but pass A slower (0.276 -> 0.315 ms), no net gain
+    const bool one11 = A.nlinks == 1 && A.ksum == 11;
+    A.tile_log = (one11 && tile_opt == 11) ? 11 : 10;
+    A.stride = part_stride(A.ksum, A.tile_log);
+    const uint32_t tile = 1u << A.tile_log;
 #define SKE_CK(x)                        \
     do {                                 \
         hipError_t e_ = (x);             \
@@ -1247,7 +1268,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             A.hllw = set ? hllw1 : hllw0;
             A.fixed_w = B.fixed_w;
             A.n = ms;
-            A.ntiles = (ms + kPaBlock - 1) / kPaBlock;
+            A.ntiles = (ms + tile - 1) / tile;
             A.bytes = B.offs ? B.bytes : B.bytes + s0 * B.fixed_w;
             A.offs = B.offs ? B.offs + s0 : nullptr;
             A.slot = B.slot + s0;
@@ -1257,7 +1278,10 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             const unsigned per_cu = km <= 11 ? 2 : 1;
             const unsigned ga = unsigned(cus) * per_cu / kPGroups * kPGroups;  // blocks past a group's tiles exit
             if (hook) hook(hook_user, 0, 0, st);
-            if (A.nlinks == 1 && A.ksum == 11)  // RESERVE 0.001 (C3/C5): one link, k = 11
+            if (one11 && A.tile_log == 11)  // RESERVE 0.001 (C3/C5): one link, k = 11
+                hipLaunchKernelGGL((k_part_a2<11, 1024>), dim3(unsigned(cus) / kPGroups * kPGroups), dim3(1024),
+                                   0, st, A);
+            else if (one11)
                 hipLaunchKernelGGL((k_part_a2<11>), dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(kA2Threads),
                                    0, st, A);
             else if (km <= 11)
@@ -1277,7 +1301,9 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             const bool pairs = A.nlinks == 1 && pb_pairs;
             const unsigned gb = unsigned(cus) * (pairs ? 1 : 2) / kPGroups * kPGroups;
             if (hook) hook(hook_user, 1, 0, st);
-            if (pairs)
+            if (pairs && A.tile_log == 11)  // runs of ~148 records
+                hipLaunchKernelGGL((k_part_b<2, 6>), dim3(gb), dim3(kPbBlock), 0, st, A);
+            else if (pairs)
                 hipLaunchKernelGGL(k_part_b<2>, dim3(gb), dim3(kPbBlock), 0, st, A);
             else
                 hipLaunchKernelGGL(k_part_b<1>, dim3(gb), dim3(kPbBlock), 0, st, A);

@@ -180,8 +180,8 @@ def test_hll_reserve_refused_while_graph_alive(engine):
     engine.hll_reserve(cap + 100)  # no graph holds the slab any more
 
 
-@pytest.mark.parametrize("hll_mode", [1, 0])
-def test_partitioned_hot_register_and_many_keys(engine, orc, hll_mode):
+@pytest.mark.parametrize("hll_mode,pa_tile", [(1, 10), (0, 10), (0, 11)])
+def test_partitioned_hot_register_and_many_keys(engine, orc, hll_mode, pa_tile):
     """Adversarial PFADD shapes for the line-owned apply: 2M swipes where half
     repeat ONE id into ONE key (one register line takes a million updates) and
     the rest spread over 40k keys (many lines per sub-bucket); registers ==
@@ -189,6 +189,7 @@ def test_partitioned_hot_register_and_many_keys(engine, orc, hll_mode):
     from rtsas_amd.engine import DeviceBatch, DeviceBuffer
     w, p = _c3_small(engine)
     engine.set_option("hll_mode", hll_mode)
+    engine.set_option("pa_tile", pa_tile)   # 11: 2048-swipe tiles (k_part_a2<11, 1024>, pass B R = 6)
     engine.hll_reserve(40_001)
     b = engine.swipe_batch(p, 0, 2_000_000)
     buf, offs, slot = b.to_host()
