@@ -83,6 +83,11 @@ def parse():
     ap.add_argument("--pa-tile", type=int, default=-1,
                     help="partitioned K1 tile: 10 = 1024 swipes, 11 = 2048 (one-link k = 11 "
                          "chains; -1: library default)")
+    ap.add_argument("--pa-precheck", type=int, default=-1,
+                    help="partitioned K1: 1 = pass A pre-checks the HLL registers (pass C only "
+                         "raises), 0 = pass C loads them (-1: library default)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="library option (ske_set_option), e.g. part_overlap=2; repeatable")
     ap.add_argument("--pb-pairs", type=int, default=-1,
                     help="partitioned K1 pass B: 1 = slice pairs (128 KiB images), 0 = single "
                          "slices (-1: library default)")
@@ -342,6 +347,11 @@ def main():
         engine.set_option("pb_pairs", args.pb_pairs)
     if args.pa_tile >= 0:
         engine.set_option("pa_tile", args.pa_tile)
+    if args.pa_precheck >= 0:
+        engine.set_option("pa_precheck", args.pa_precheck)
+    for kv in args.opt:
+        name, _, val = kv.partition("=")
+        engine.set_option(name, int(val))
 
     # Bloom preload (replicated on every rank), this rank's HLL key shard, and
     # 64 spare slots for the verification batch

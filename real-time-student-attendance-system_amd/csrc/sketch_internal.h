@@ -151,7 +151,7 @@ struct PartBatch {
 // side == nullptr: every pass on st; else pass C on `side` (ev: 4 events)
 hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t nb, uint8_t *regs,
                               uint32_t nslots, Scratch *scr, unsigned int *err, int cus, uint32_t sub,
-                              int hll_mode, int pb_pairs, int tile_opt, hipStream_t st, hipStream_t side,
+                              int hll_mode, int pb_pairs, int tile_opt, int pre_opt, int ovl, int a_grid, hipStream_t st, hipStream_t side,
                               hipEvent_t *ev,
                               PassHook hook = nullptr, void *hook_user = nullptr);
 

@@ -47,6 +47,7 @@ constexpr uint32_t kPSliceBytes = kPSliceBits / 8;  // 64 KiB
 constexpr uint32_t kPSub = 1u << 24;                // swipes per sub-batch (passes A-B-C)
 constexpr uint32_t kPbGroup = 8;                    // tiles a pass-B wave reads at once
 constexpr uint32_t kPbLanes = 64 / kPbGroup;        // lanes per tile run
+constexpr uint32_t kPcErr = 0xffffffffu;            // pre: an HLL word whose slot is outside the slab
 
 struct PartLink {
     const uint8_t *bf;
@@ -69,8 +70,10 @@ struct PartArgs {
     uint32_t *rec;         // [ntiles][stride] probe records
     uint32_t *off;         // [nslices + 1][off_stride] run boundaries (slice-major)
     uint8_t *fail;         // [nlinks][fail_stride]
-    uint32_t *hllw;        // [n] register | rank << 16
+    uint32_t *hllw;        // [n] register | rank << 16 (pre: rank 0 = no raise, kPcErr = slot out of range)
+    uint32_t *oldw;        // [n] pre: the register's aligned word as pass A read it (pass C's CAS expectation)
     uint32_t fixed_w, n, stride, ntiles, nslices, nlinks, ksum, nslots, fail_stride, off_stride;
+    uint32_t pre;          // pass A pre-checks the register (k_part_a2, CAS pass C only)
     uint32_t tile_log;     // swipes per tile = 1 << tile_log (10, or 11 for k_part_a2<11, 1024>)
     PartLink link[kPMaxLinks];
 };
@@ -296,24 +299,25 @@ __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part
     const uint32_t S = A.nslices;
     for (uint32_t g = tid; g <= kPMaxSlices; g += kA2Threads) scnt2[0][g] = scnt2[1][g] = 0;
     __syncthreads();
-    auto offsets = [&](uint32_t t, uint32_t u, uint32_t &b, uint32_t &e) {
+    auto offsets = [&](uint32_t t, uint32_t u, uint32_t &b, uint32_t &e, uint32_t &sl) {
         const uint32_t i = t * kTile + u * kA2Threads + tid;
         const uint32_t ic = i < A.n ? i : A.n - 1;
         b = A.offs ? A.offs[ic] : ic * A.fixed_w;
         e = A.offs ? A.offs[ic + 1] : b + A.fixed_w;
+        sl = A.pre ? A.slot[ic] : 0;
     };
     uint32_t gt0, gt1;
     part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
     const uint32_t tstep = gridDim.x / kPGroups;
     const __amdgpu_buffer_rsrc_t rbytes = part_rsrc(A.bytes, 0xfffffff0u);
     const PartLink &L = A.link[0];
-    uint32_t par = 0, nb_[kA2U], ne_[kA2U];
+    uint32_t par = 0, nb_[kA2U], ne_[kA2U], sl_[kA2U];
     PartId it[kA2U];
     {
         const uint32_t t = gt0 + blockIdx.x / kPGroups;
 #pragma unroll
         for (uint32_t u = 0; u < kA2U; u++) {
-            offsets(t < gt1 ? t : gt0, u, nb_[u], ne_[u]);
+            offsets(t < gt1 ? t : gt0, u, nb_[u], ne_[u], sl_[u]);
             part_id_load(rbytes, nb_[u], ne_[u], it[u]);
         }
     }
@@ -321,9 +325,16 @@ __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part
         uint32_t *scnt = scnt2[par];
         uint32_t rv[kA2U][KM], rp[kA2U][KM];
         bool act[kA2U];
+        // pre: this tile's register words, loaded after hashing and examined
+        // after the scan (their latency hidden by the probes and the sort)
+        uint32_t hv[kA2U], wv[kA2U];
         const uint32_t tn = t + tstep < gt1 ? t + tstep : t;
+        uint32_t slc[kA2U];
 #pragma unroll
-        for (uint32_t u = 0; u < kA2U; u++) offsets(tn, u, nb_[u], ne_[u]);
+        for (uint32_t u = 0; u < kA2U; u++) {
+            slc[u] = sl_[u];
+            offsets(tn, u, nb_[u], ne_[u], sl_[u]);
+        }
 #pragma unroll
         for (uint32_t u = 0; u < kA2U; u++) {
             const uint32_t lu = u * kA2Threads + tid;
@@ -331,10 +342,18 @@ __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part
             act[u] = i < A.n;
             uint64_t ha, hb, hh;
             part_hash3(A.bytes, it[u], ha, hb, hh);
+            hv[u] = kPcErr;
+            wv[u] = 0;
             if (act[u]) {
                 uint32_t idx, rank;
                 hll_patlen(hh, idx, rank);
-                A.hllw[i] = idx | (rank << 16);
+                if (!A.pre) {
+                    A.hllw[i] = idx | (rank << 16);
+                } else if (slc[u] < A.nslots) {
+                    hv[u] = idx | (rank << 16);
+                    wv[u] = *reinterpret_cast<const uint32_t *>(A.regs + (uint64_t(slc[u]) << kHllP) +
+                                                                (idx & ~3u));
+                }
                 A.fail[i] = 0;
             }
             // bit 19 + tile_log of a record: its slice's parity (pass B's pairs)
@@ -378,6 +397,21 @@ __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part
             run += v[j];
         }
         __syncthreads();
+        if (A.pre) {
+            // rank 0: the register already holds at least this rank (registers
+            // only grow, so pass C may skip it); else pass C's CAS starts from
+            // the word read here
+#pragma unroll
+            for (uint32_t u = 0; u < kA2U; u++) {
+                const uint32_t i = t * kTile + u * kA2Threads + tid;
+                if (act[u]) {
+                    uint32_t h = hv[u];
+                    if (h != kPcErr && ((wv[u] >> ((h & 3u) * 8)) & 0xffu) >= (h >> 16)) h &= 0xffffu;
+                    A.hllw[i] = h;
+                    A.oldw[i] = wv[u];
+                }
+            }
+        }
         for (uint32_t g = tid; g <= S; g += kA2Threads) A.off[size_t(g) * A.off_stride + t] = scnt[g];
 #pragma unroll
         for (uint32_t u = 0; u < kA2U; u++)
@@ -606,9 +640,22 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
             w[u] = nullptr;
             rank[u] = 0;
             sh[u] = 0;
+            cur[u] = 0;
             if (i < end) {
                 for (uint32_t l = 0; l < A.nlinks; l++) valid[u] |= A.fail[size_t(l) * A.fail_stride + i] == 0;
-                if (valid[u]) {
+                if (valid[u] && A.pre) {
+                    // pass A read the register: only raises remain, from its word
+                    const uint32_t hv = A.hllw[i];
+                    if (hv == kPcErr) {
+                        atomicOr(A.err, 1u);
+                    } else if (hv >> 16) {
+                        const uint32_t s = A.slot[i];
+                        w[u] = reinterpret_cast<uint32_t *>(A.regs + (uint64_t(s) << kHllP) + (hv & 0xfffcu));
+                        sh[u] = (hv & 3) * 8;
+                        rank[u] = hv >> 16;
+                        cur[u] = A.oldw[i];
+                    }
+                } else if (valid[u]) {
                     const uint32_t s = A.slot[i];
                     if (s >= A.nslots) {
                         atomicOr(A.err, 1u);
@@ -622,8 +669,10 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
                 }
             }
         }
+        if (!A.pre) {
 #pragma unroll
-        for (int u = 0; u < U; u++) cur[u] = w[u] ? *w[u] : 0xffffffffu;
+            for (int u = 0; u < U; u++) cur[u] = w[u] ? *w[u] : 0xffffffffu;
+        }
 #pragma unroll
         for (int u = 0; u < U; u++)
             if (w[u]) part_reg_max(w[u], sh[u], rank[u], cur[u]);
@@ -1144,6 +1193,7 @@ static hipError_t part_scratch(PartArgs *A, uint64_t n, uint32_t sub, Scratch *s
     if (e == hipSuccess) A->off = (uint32_t *)scratch_get(scr, 29, size_t(A->off_stride) * (A->nslices + 1) * 4, &e);
     if (e == hipSuccess) A->fail = (uint8_t *)scratch_get(scr, 30, size_t(fstride) * A->nlinks, &e);
     if (e == hipSuccess) A->hllw = (uint32_t *)scratch_get(scr, 31, size_t(m) * 4, &e);
+    if (e == hipSuccess) A->oldw = (uint32_t *)scratch_get(scr, 42, size_t(m) * 4, &e);
     A->fail_stride = fstride;
     if (e == hipSuccess) {
         HllArgs H{};
@@ -1160,14 +1210,15 @@ static uint32_t part_sub(uint32_t sub_opt) {
 
 
 
-// The fail bytes and HLL words pass C reads: two sets, so that with pass C on
-// a side stream the next unit's pass A (which writes them) does not wait for
-// it (set 1: slots 38, 39)
+// The fail bytes, HLL words and register words pass C reads: two sets, so
+// that with pass C on a side stream the next unit's pass A (which writes them)
+// does not wait for it (set 1: slots 38, 39, 43; set 0 holds its register words in slot 42)
 static hipError_t part_scratch_c(PartArgs *A, uint32_t m, int set, Scratch *scr) {
     if (set == 0) return hipSuccess;  // part_scratch's slots 30, 31
     hipError_t e = hipSuccess;
     A->fail = (uint8_t *)scratch_get(scr, 38, size_t(A->fail_stride) * A->nlinks, &e);
     if (e == hipSuccess) A->hllw = (uint32_t *)scratch_get(scr, 39, size_t(m) * 4, &e);
+    if (e == hipSuccess) A->oldw = (uint32_t *)scratch_get(scr, 43, size_t(m) * 4, &e);
     return e;
 }
 
@@ -1185,14 +1236,16 @@ hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratc
 // Units = (batch, sub-batch of at most `sub` swipes), in order.  Without a
 // side stream every pass runs on st.  With one (`side`, events ev[0..3]):
 // passes A and B of unit u on st, its pass C on `side` once pass A of unit
-// u + 1 is done (event ev[(u + 1) & 1]); unit u's pass A first waits for pass
-// C of unit u - 2 (event ev[2 + (u & 1)]), the last reader of the scratch set
-// it writes; st joins `side` at the end.  So pass C of one unit (memory-side
-// register atomics) runs beside pass B of the next (slice probes).  Results
-// equal the serial order: units touch disjoint answers and PFADD is a max.
+// u + 1 is done (ovl 1, event ev[(u + 1) & 1]: pass C of one unit, memory-side
+// register atomics, beside pass B of the next, slice probes) or once its own
+// pass B is done (ovl 2, event ev[u & 1]: beside pass A of the next, hashing
+// and LDS sorting); unit u's pass A first waits for pass C of unit u - 2
+// (event ev[2 + (u & 1)]), the last reader of the scratch set it writes; st
+// joins `side` at the end.  Results equal the serial order: units touch
+// disjoint answers and PFADD is a max.
 hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t nb, uint8_t *regs,
                               uint32_t nslots, Scratch *scr, unsigned int *err, int cus, uint32_t sub_opt,
-                              int hll_mode, int pb_pairs, int tile_opt, hipStream_t st, hipStream_t side,
+                              int hll_mode, int pb_pairs, int tile_opt, int pre_opt, int ovl, int a_grid, hipStream_t st, hipStream_t side,
                               hipEvent_t *ev, PassHook hook, void *hook_user) {
     PartArgs A{};
     if (!part_plan(ch, &A)) return hipErrorInvalidValue;
@@ -1204,13 +1257,11 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
     if (e != hipSuccess) return e;
     // (set 1 too, even when not pipelined: see part_reserve)
     uint8_t *fail0 = A.fail;
-    uint32_t *hllw0 = A.hllw;
-    uint8_t *fail1 = nullptr;
-    uint32_t *hllw1 = nullptr;
+    uint32_t *hllw0 = A.hllw, *oldw0 = A.oldw;
     e = part_scratch_c(&A, uint32_t(nmax < sub ? nmax : sub), 1, scr);
     if (e != hipSuccess) return e;
-    fail1 = A.fail;
-    hllw1 = A.hllw;
+    uint8_t *fail1 = A.fail;
+    uint32_t *hllw1 = A.hllw, *oldw1 = A.oldw;
     A.regs = regs;
     A.nslots = nslots;
     A.err = err;
@@ -1221,6 +1272,10 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
     const bool one11 = A.nlinks == 1 && A.ksum == 11;
     A.tile_log = (one11 && tile_opt == 11) ? 11 : 10;
     A.stride = part_stride(A.ksum, A.tile_log);
+    // the register pre-check moves pass C's random register loads into pass A
+    // (VALU / LDS bound, its memory path has room), so pass C touches only the
+    // registers that rise (k_part_a2 of 1024-swipe tiles, CAS PFADD)
+    A.pre = (pre_opt && hll_mode == 0 && one11 && A.tile_log == 10) ? 1u : 0u;
     const uint32_t tile = 1u << A.tile_log;
 #define SKE_CK(x)                        \
     do {                                 \
@@ -1266,6 +1321,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             const int set = side ? int(u & 1) : 0;
             A.fail = set ? fail1 : fail0;
             A.hllw = set ? hllw1 : hllw0;
+            A.oldw = set ? oldw1 : oldw0;
             A.fixed_w = B.fixed_w;
             A.n = ms;
             A.ntiles = (ms + tile - 1) / tile;
@@ -1275,21 +1331,21 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             A.out = B.out ? B.out + s0 : nullptr;
             // pass C of unit u - 2 was the last reader of this scratch set
             if (side && u >= 2) SKE_CK(hipStreamWaitEvent(st, ev[2 + set], 0));
-            const unsigned per_cu = km <= 11 ? 2 : 1;
+            const unsigned per_cu = km <= 11 ? (a_grid ? unsigned(a_grid) : 2u) : 1;
             const unsigned ga = unsigned(cus) * per_cu / kPGroups * kPGroups;  // blocks past a group's tiles exit
             if (hook) hook(hook_user, 0, 0, st);
             if (one11 && A.tile_log == 11)  // RESERVE 0.001 (C3/C5): one link, k = 11
                 hipLaunchKernelGGL((k_part_a2<11, 1024>), dim3(unsigned(cus) / kPGroups * kPGroups), dim3(1024),
                                    0, st, A);
             else if (one11)
-                hipLaunchKernelGGL((k_part_a2<11>), dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(kA2Threads),
-                                   0, st, A);
+                hipLaunchKernelGGL((k_part_a2<11>), dim3(unsigned(cus) * per_cu / kPGroups * kPGroups),
+                                   dim3(kA2Threads), 0, st, A);
             else if (km <= 11)
                 hipLaunchKernelGGL(k_part_a<11>, dim3(ga), dim3(kPaBlock), 0, st, A);
             else
                 hipLaunchKernelGGL(k_part_a<22>, dim3(ga), dim3(kPaBlock), 0, st, A);
             if (hook) hook(hook_user, 0, 1, st);
-            if (side && have_prev) {  // C(u - 1) behind A(u) (and so behind B(u - 1))
+            if (side && ovl == 1 && have_prev) {  // C(u - 1) behind A(u) (and so behind B(u - 1))
                 SKE_CK(hipEventRecord(ev[set], st));
                 SKE_CK(hipStreamWaitEvent(side, ev[set], 0));
                 SKE_CK(launch_c(prev, prev_ms, side));
@@ -1308,7 +1364,13 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             else
                 hipLaunchKernelGGL(k_part_b<1>, dim3(gb), dim3(kPbBlock), 0, st, A);
             if (hook) hook(hook_user, 1, 1, st);
-            if (side) {
+            if (side && ovl == 2) {  // C(u) behind B(u), beside A(u + 1)
+                SKE_CK(hipEventRecord(ev[set], st));
+                SKE_CK(hipStreamWaitEvent(side, ev[set], 0));
+                SKE_CK(launch_c(A, ms, side));
+                SKE_CK(hipEventRecord(ev[2 + set], side));
+                have_prev = true;
+            } else if (side) {
                 prev = A;
                 prev_ms = ms;
                 have_prev = true;
@@ -1318,7 +1380,9 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             SKE_CK(hipGetLastError());
         }
     }
-    if (side && have_prev) {  // the last unit's pass C behind its pass B, then join
+    if (side && ovl == 2 && have_prev) {  // join the last unit's pass C
+        SKE_CK(hipStreamWaitEvent(st, ev[2 + int((u - 1) & 1)], 0));
+    } else if (side && have_prev) {  // the last unit's pass C behind its pass B, then join
         const int set = int((u - 1) & 1);
         SKE_CK(hipEventRecord(ev[set], st));
         SKE_CK(hipStreamWaitEvent(side, ev[set], 0));

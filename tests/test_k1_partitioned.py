@@ -180,16 +180,18 @@ def test_hll_reserve_refused_while_graph_alive(engine):
     engine.hll_reserve(cap + 100)  # no graph holds the slab any more
 
 
-@pytest.mark.parametrize("hll_mode,pa_tile", [(1, 10), (0, 10), (0, 11)])
-def test_partitioned_hot_register_and_many_keys(engine, orc, hll_mode, pa_tile):
+@pytest.mark.parametrize("hll_mode,pa_tile,pre", [(1, 10, 0), (0, 10, 0), (0, 11, 0), (0, 10, 1)])
+def test_partitioned_hot_register_and_many_keys(engine, orc, hll_mode, pa_tile, pre):
     """Adversarial PFADD shapes for the line-owned apply: 2M swipes where half
     repeat ONE id into ONE key (one register line takes a million updates) and
     the rest spread over 40k keys (many lines per sub-bucket); registers ==
-    the oracle."""
+    the oracle.  pre = 1: pass A pre-checks the registers and pass C only
+    raises (option pa_precheck)."""
     from rtsas_amd.engine import DeviceBatch, DeviceBuffer
     w, p = _c3_small(engine)
     engine.set_option("hll_mode", hll_mode)
     engine.set_option("pa_tile", pa_tile)   # 11: 2048-swipe tiles (k_part_a2<11, 1024>, pass B R = 6)
+    engine.set_option("pa_precheck", pre)
     engine.hll_reserve(40_001)
     b = engine.swipe_batch(p, 0, 2_000_000)
     buf, offs, slot = b.to_host()
@@ -213,10 +215,12 @@ def test_partitioned_hot_register_and_many_keys(engine, orc, hll_mode, pa_tile):
     assert np.array_equal(engine.registers_all(40_001), regs)
 
 
-@pytest.mark.parametrize("mode", ["direct", "graph"])
-def test_many_pipelined_small_units(engine, orc, mode):
+@pytest.mark.parametrize("mode,ovl,pre", [("direct", 1, 0), ("graph", 1, 0), ("direct", 2, 0), ("graph", 2, 1),
+                                          ("direct", 2, 1)])
+def test_many_pipelined_small_units(engine, orc, mode, ovl, pre):
     """ske_swipes_many_async through the partitioned K1 with pass C of every
-    unit on a side stream beside the next unit's pass B (option part_overlap):
+    unit on a side stream beside the next unit's pass B (option part_overlap
+    1) or its pass A (2), with or without the pass-A register pre-check:
     sub-batches of
     64k swipes make ~25 units over 7 ragged batches (incl. 1 swipe and a
     partial tile), so the two scratch sets alternate many times; answers and
@@ -225,7 +229,8 @@ def test_many_pipelined_small_units(engine, orc, mode):
     from rtsas_amd.engine import DeviceBuffer
     w, p = _c3_small(engine)
     engine.set_option("part_sub", 65536)
-    engine.set_option("part_overlap", 1)
+    engine.set_option("part_overlap", ovl)
+    engine.set_option("pa_precheck", pre)
     sizes = [300_000, 1, 70_001, 300_000, 250_000, 2048, 400_000]
     bs, start = [], 0
     for n in sizes:
