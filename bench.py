@@ -508,6 +508,16 @@ def main():
             "achieved_Gsectors_per_s": sectors, "peak_Gsectors_per_s": RANDOM_SECTOR_GPS,
             "frac": sectors / RANDOM_SECTOR_GPS}
         if pmc and "TCC_EA0_ATOMIC_sum" in pmc.get("mean", {}):
+            # every register touch is one random 64-B request: the valid swipes'
+            # pre-check loads plus the raising CASes (memory-side atomics, PMC)
+            req = (nvalid + pmc["mean"]["TCC_EA0_ATOMIC_sum"]) / (kern_ms * 1e-3) / 1e9
+            roofline["random_sector_bound"].update({
+                "what": "random 64-B requests into the 1.6 GB register slab per second: one "
+                        "pre-check load per valid swipe plus one memory-side CAS per raise "
+                        "(TCC_EA0_ATOMIC_sum, PMC per dispatch), against the measured random 4-B "
+                        "read rate over a 1.6 GB table (tools/randbench.hip)",
+                "achieved_Gsectors_per_s": req, "frac": req / RANDOM_SECTOR_GPS,
+                "loads_only_frac": sectors / RANDOM_SECTOR_GPS})
             cas = pmc["mean"]["TCC_EA0_ATOMIC_sum"] / (kern_ms * 1e-3) / 1e9
             roofline["binding"] = {
                 "counter": "TCC_EA0_ATOMIC_sum",

@@ -108,7 +108,7 @@ struct ske_ctx {
     // capture); ske_pass_times() sums them per pass
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
-    struct Mark { int pass; hipEvent_t a, b; };
+    struct Mark { int pass; hipEvent_t a, b; bool own_a; };
     std::vector<Mark> marks;
     double pass_ms[kPassKinds] = {};
     uint64_t pass_n[kPassKinds] = {};
@@ -208,14 +208,16 @@ struct PassMark {
     hipEvent_t a = nullptr, b = nullptr;
     hipStream_t st = nullptr;  // the stream the kernel runs on
 };
-PassMark mark_begin(ske_ctx *c, int pass, hipStream_t st) {
+// `start`: an end event just recorded on st with nothing enqueued since (the
+// previous kernel's), reused as this kernel's start: one marker packet fewer
+PassMark mark_begin(ske_ctx *c, int pass, hipStream_t st, hipEvent_t start = nullptr) {
     PassMark m;
     if (!c->timing || c->capturing) return m;
-    m.a = ev_get(c);
+    m.a = start ? start : ev_get(c);
     m.b = ev_get(c);
     m.st = st;
-    if (!m.a || !m.b || hipEventRecord(m.a, st) != hipSuccess) return PassMark();
-    c->marks.push_back({pass, m.a, m.b});
+    if (!m.a || !m.b || (!start && hipEventRecord(m.a, st) != hipSuccess)) return PassMark();
+    c->marks.push_back({pass, m.a, m.b, start == nullptr});
     return m;
 }
 PassMark mark_begin(ske_ctx *c, int pass) { return mark_begin(c, pass, c->st); }
@@ -475,15 +477,25 @@ int launch_part(ske_ctx *c, const ChainDev &ch, const PartBatch *bt, uint32_t nb
     unsigned long long cid = 0;
     int rc = scratch_user_begin(c, &cid);
     if (rc) return rc;
-    // one event pair per kernel and unit, bracketed on the kernel's stream
-    PassMark pm[3];
+    // one event pair per kernel and unit, bracketed on the kernel's stream;
+    // back-to-back kernels on one stream share the event between them
+    struct Hook {
+        PassMark pm[3];
+        PassMark last;  // the mark whose end event was recorded last, if nothing came after it
+    } hs;
     auto hook = [](void *u, int pass, int end, hipStream_t st) {
         ske_ctx *cc = static_cast<ske_ctx *>(u);
-        PassMark *marks = reinterpret_cast<PassMark *>(cc->hook_arg);
-        if (end) mark_end(cc, marks[pass]);
-        else marks[pass] = mark_begin(cc, 1 + pass, st);
+        Hook *h = reinterpret_cast<Hook *>(cc->hook_arg);
+        if (end) {
+            mark_end(cc, h->pm[pass]);
+            h->last = h->pm[pass];
+        } else {
+            const bool share = h->last.b && h->last.st == st;
+            h->pm[pass] = mark_begin(cc, 1 + pass, st, share ? h->last.b : nullptr);
+            h->last = PassMark();
+        }
     };
-    c->hook_arg = pm;
+    c->hook_arg = &hs;
     e = launch_swipes_part(ch, bt, nb, c->regs, c->nslots, c->scratch, c->err, c->cus, c->part_sub, c->hll_mode,
                            c->pb_pairs, c->pa_tile, c->pa_pre, pipelined ? c->part_overlap : 0, c->pa_grid, c->st, side, c->part_ev, c->timing && !c->capturing ? +hook : nullptr, c);
     if (e != hipSuccess) {
@@ -659,7 +671,7 @@ int ske_pass_times(ske_ctx *c, double *ms, uint64_t *count, int reset) {
             HIPCHK(c, hipEventElapsedTime(&t, m.a, m.b));
             c->pass_ms[m.pass] += t;
             c->pass_n[m.pass]++;
-            c->ev_pool.push_back(m.a);
+            if (m.own_a) c->ev_pool.push_back(m.a);
             c->ev_pool.push_back(m.b);
         }
         c->marks.clear();
@@ -1243,6 +1255,17 @@ int ske_swipes_many_async(ske_ctx *c, uint32_t fid, const ske_swipe_batch *b, ui
                               b[j].n, b[j].out_valid, &A);
         if (ok) return swipes_many_persistent(c, A, b, nb);
     }
+    // the partitioned K1: one call over every batch (pass C beside the next
+    // A / B when pipelined), before any branch streams are made (it uses
+    // none; creating them lazily here cost ms of host time per new count)
+    const int var = (nb && !c->ablate) ? k1_variant(c, ch) : 0;
+    if (var == 3) {
+        std::vector<PartBatch> pb(nb);
+        for (uint32_t j = 0; j < nb; j++)
+            pb[j] = PartBatch{b[j].bytes, b[j].width ? nullptr : b[j].offs, b[j].width, b[j].slot, b[j].n,
+                              b[j].out_valid};
+        return launch_part(c, ch, pb.data(), nb, c->part_overlap != 0 && nb > 1);
+    }
     uint32_t br = branches ? branches : SKE_MANY_DEFAULT_BRANCHES;
     if (nb && br > nb) br = nb;
     if (br > 1) {  // with nb == 0: only prepares the side streams (e.g. before capture)
@@ -1258,14 +1281,6 @@ int ske_swipes_many_async(ske_ctx *c, uint32_t fid, const ske_swipe_batch *b, ui
     // different sizes never reallocate it between recorded launches
     uint64_t nmax = 0;
     for (uint32_t j = 0; j < nb; j++) nmax = b[j].n > nmax ? b[j].n : nmax;
-    const int var = c->ablate ? 0 : k1_variant(c, ch);
-    if (var == 3) {  // one pipelined call over every batch (pass C beside the next A / B)
-        std::vector<PartBatch> pb(nb);
-        for (uint32_t j = 0; j < nb; j++)
-            pb[j] = PartBatch{b[j].bytes, b[j].width ? nullptr : b[j].offs, b[j].width, b[j].slot, b[j].n,
-                              b[j].out_valid};
-        return launch_part(c, ch, pb.data(), nb, c->part_overlap != 0 && nb > 1);
-    }
     if (var == 2 && nmax) {
         hipError_t e = hipSuccess;
         (void)scratch_get(c->scratch, 16, xr_scratch_bytes(nmax, ch.nlinks), &e);

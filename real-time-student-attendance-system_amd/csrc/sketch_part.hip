@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const Par
 // width.  C3: 0.315 -> 0.273 ms per 16M swipes (A/B on one box); 256 threads x
 // 4 swipes (208 VGPRs, 8 waves per CU) was slower again, 0.323 ms.
 constexpr uint32_t kA2Threads = 512;
-template <int KM, uint32_t kA2Threads = kA2Threads, uint32_t kA2U = 2>
+template <int KM, uint32_t kA2Threads = kA2Threads, uint32_t kA2U = 2, bool kPre = false>
 __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part_a2(const PartArgs A) {
     constexpr uint32_t kTile = kA2Threads * kA2U;  // swipes per tile (1 << A.tile_log)
     constexpr uint32_t kTileLog = kTile == 2048 ? 11 : 10;
@@ -297,14 +297,16 @@ __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part
     __shared__ uint32_t swsum[kA2Threads / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t S = A.nslices;
-    for (uint32_t g = tid; g <= kPMaxSlices; g += kA2Threads) scnt2[0][g] = scnt2[1][g] = 0;
+    // a slice counter starts at g << 16, so an LDS atomic's return value is
+    // already the record's (slice, rank) pair
+    for (uint32_t g = tid; g <= kPMaxSlices; g += kA2Threads) scnt2[0][g] = scnt2[1][g] = g << 16;
     __syncthreads();
     auto offsets = [&](uint32_t t, uint32_t u, uint32_t &b, uint32_t &e, uint32_t &sl) {
         const uint32_t i = t * kTile + u * kA2Threads + tid;
         const uint32_t ic = i < A.n ? i : A.n - 1;
         b = A.offs ? A.offs[ic] : ic * A.fixed_w;
         e = A.offs ? A.offs[ic + 1] : b + A.fixed_w;
-        sl = A.pre ? A.slot[ic] : 0;
+        sl = kPre ? A.slot[ic] : 0;
     };
     uint32_t gt0, gt1;
     part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
@@ -347,7 +349,7 @@ __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part
             if (act[u]) {
                 uint32_t idx, rank;
                 hll_patlen(hh, idx, rank);
-                if (!A.pre) {
+                if (!kPre) {
                     A.hllw[i] = idx | (rank << 16);
                 } else if (slc[u] < A.nslots) {
                     hv[u] = idx | (rank << 16);
@@ -365,20 +367,24 @@ __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part
                 const uint32_t x = wk.x;
                 const uint32_t g = x >> kPSliceLog;
                 rv[u][q] = (x & kPSliceMask) | ((g & 1u) << (kPSliceLog + kTileLog)) | rbase;
-                rp[u][q] = 0xffffffffu;
-                if (act[u]) rp[u][q] = (g << 16) | atomicAdd(&scnt[g], 1u);
+                // no branch: a lane past the batch counts into scnt[S], which
+                // the exclusive scan leaves out (it becomes the tile's total),
+                // so its records land past the tile's end, never copied out;
+                // the swipe's 11 returning atomics are in flight together
+                rp[u][q] = atomicAdd(&scnt[act[u] ? g : S], 1u);
                 if (q + 1 < KM) wk.step(L.d);
             }
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this swipe's 11 atomics, once
         }
         __syncthreads();
 #pragma unroll
         for (uint32_t u = 0; u < kA2U; u++) part_id_load(rbytes, nb_[u], ne_[u], it[u]);  // the next tile's ids
-        // exclusive scan of scnt[0..S] (scnt[S] == 0 becomes the tile's total)
+        // exclusive scan of the counts in scnt[0..S] (scnt[S] becomes the tile's total)
         constexpr int kPer = (kPMaxSlices + 1) / kA2Threads;
         uint32_t v[kPer], s = 0;
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
-            v[j] = scnt[tid * kPer + j];
+            v[j] = scnt[tid * kPer + j] - ((tid * kPer + j) << 16);
             s += v[j];
         }
         uint32_t incl = s;
@@ -397,7 +403,7 @@ __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part
             run += v[j];
         }
         __syncthreads();
-        if (A.pre) {
+        if (kPre) {
             // rank 0: the register already holds at least this rank (registers
             // only grow, so pass C may skip it); else pass C's CAS starts from
             // the word read here
@@ -417,8 +423,8 @@ __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part
         for (uint32_t u = 0; u < kA2U; u++)
 #pragma unroll
             for (int q = 0; q < KM; q++)
-                if (rp[u][q] != 0xffffffffu) srec[scnt[rp[u][q] >> 16] + (rp[u][q] & 0xffffu)] = rv[u][q];
-        for (uint32_t g = tid; g <= S; g += kA2Threads) scnt2[par ^ 1][g] = 0;
+                srec[scnt[rp[u][q] >> 16] + (rp[u][q] & 0xffffu)] = rv[u][q];
+        for (uint32_t g = tid; g <= S; g += kA2Threads) scnt2[par ^ 1][g] = g << 16;
         __syncthreads();
         const uint32_t total = scnt[S];
         uint4 *dst = reinterpret_cast<uint4 *>(A.rec + size_t(t) * A.stride);
@@ -575,11 +581,20 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
             const uint32_t nq = __shfl(incl, 63, 64);
             uint32_t pos = incl - cnt;
             while (fm) {
+                // record ctz(fm) by a select tree on its index bits (no compare chain)
                 const uint32_t j = __builtin_ctz(fm);
                 fm &= fm - 1;
-                uint32_t rr = rec[0];
+                constexpr uint32_t kNR = 4 * R, kL = kNR <= 8 ? 3 : (kNR <= 16 ? 4 : 5);
+                uint32_t tt[1u << kL];
 #pragma unroll
-                for (uint32_t jj = 1; jj < 4 * R; jj++) rr = j == jj ? rec[jj] : rr;
+                for (uint32_t i = 0; i < (1u << kL); i++) tt[i] = rec[i < kNR ? i : 0];
+#pragma unroll
+                for (uint32_t l = 0; l < kL; l++) {
+                    const bool bit = (j >> l) & 1u;
+#pragma unroll
+                    for (uint32_t i = 0; i < ((1u << kL) >> (l + 1)); i++) tt[i] = bit ? tt[2 * i + 1] : tt[2 * i];
+                }
+                const uint32_t rr = tt[0];
                 const uint32_t at = tbase + ((rr >> kPSliceLog) & tmask);
                 if (pos < kPbQueue) q[pos] = at;
                 else __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail, at, 0, 0);  // overflow
@@ -1337,6 +1352,9 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             if (one11 && A.tile_log == 11)  // RESERVE 0.001 (C3/C5): one link, k = 11
                 hipLaunchKernelGGL((k_part_a2<11, 1024>), dim3(unsigned(cus) / kPGroups * kPGroups), dim3(1024),
                                    0, st, A);
+            else if (one11 && A.pre)
+                hipLaunchKernelGGL((k_part_a2<11, kA2Threads, 2, true>),
+                                   dim3(unsigned(cus) * per_cu / kPGroups * kPGroups), dim3(kA2Threads), 0, st, A);
             else if (one11)
                 hipLaunchKernelGGL((k_part_a2<11>), dim3(unsigned(cus) * per_cu / kPGroups * kPGroups),
                                    dim3(kA2Threads), 0, st, A);
