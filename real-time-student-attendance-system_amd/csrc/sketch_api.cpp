@@ -97,7 +97,8 @@ struct ske_ctx {
     // a launch on another stream first waits for the previous one
     hipEvent_t xr_done = nullptr;
     hipStream_t xr_stream = nullptr;
-    unsigned long long xr_cap = 0;  // capture id xr_done was recorded in (0: none)
+    unsigned long long xr_cap = 0;  // capture id of xr_stream's last scratch use (0: none)
+    bool xr_pending = false;        // that use is not yet covered by xr_done (recorded lazily)
     // executable graphs alive (recorded, not yet freed): they hold pointers to
     // the scratch and the register slab, so neither may be reallocated
     void *hook_arg = nullptr;  // launch_swipes_part's pass hook state
@@ -344,22 +345,60 @@ int k1_variant(const ske_ctx *c, const ChainDev &ch) {
 // event recorded outside a capture cannot be waited on inside it, nor the
 // reverse (the caller synchronises before recording a graph, as
 // engine.capture does; ske_graph_launch records the event after a replay).
-int scratch_user_begin(ske_ctx *c, unsigned long long *cid_out) {
-    if (!c->xr_done) HIPCHK(c, hipEventCreateWithFlags(&c->xr_done, hipEventDisableTiming));
+//
+// xr_done is recorded lazily: only when a use on another stream needs it (or
+// ske_set_stream leaves the stream), not after every call -- a marker packet
+// per call costs ~6 us of GPU time between back-to-back steps.  Recording it
+// later on xr_stream still covers the last use (it covers everything enqueued
+// there so far).  A stream whose capture state changed since that use needs
+// no wait: recording a graph starts from a synchronised stream.
+static unsigned long long capture_id(hipStream_t st, hipError_t *e) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     unsigned long long cid = 0;
-    HIPCHK(c, hipStreamGetCaptureInfo(c->st, &cs, &cid));
-    if (cs != hipStreamCaptureStatusActive) cid = 0;
-    if (c->xr_stream && c->xr_stream != c->st && c->xr_cap == cid)
-        HIPCHK(c, hipStreamWaitEvent(c->st, c->xr_done, 0));
+    *e = hipStreamGetCaptureInfo(st, &cs, &cid);
+    return cs == hipStreamCaptureStatusActive ? cid : 0;
+}
+
+// cover xr_stream's last scratch use by xr_done (false: no wait is needed)
+static int xr_flush(ske_ctx *c, bool *covered) {
+    *covered = false;
+    if (!c->xr_stream) return SKE_OK;
+    if (!c->xr_pending) {
+        *covered = true;
+        return SKE_OK;
+    }
+    hipError_t e = hipSuccess;
+    const unsigned long long now = capture_id(c->xr_stream, &e);
+    HIPCHK(c, e);
+    c->xr_pending = false;
+    if (now != c->xr_cap) {
+        c->xr_stream = nullptr;
+        return SKE_OK;
+    }
+    HIPCHK(c, hipEventRecord(c->xr_done, c->xr_stream));
+    *covered = true;
+    return SKE_OK;
+}
+
+int scratch_user_begin(ske_ctx *c, unsigned long long *cid_out) {
+    if (!c->xr_done) HIPCHK(c, hipEventCreateWithFlags(&c->xr_done, hipEventDisableTiming));
+    hipError_t e = hipSuccess;
+    const unsigned long long cid = capture_id(c->st, &e);
+    HIPCHK(c, e);
+    if (c->xr_stream && c->xr_stream != c->st && c->xr_cap == cid) {
+        bool covered = false;
+        const int rc = xr_flush(c, &covered);
+        if (rc) return rc;
+        if (covered) HIPCHK(c, hipStreamWaitEvent(c->st, c->xr_done, 0));
+    }
     *cid_out = cid;
     return SKE_OK;
 }
 
 int scratch_user_end(ske_ctx *c, unsigned long long cid) {
-    HIPCHK(c, hipEventRecord(c->xr_done, c->st));
     c->xr_stream = c->st;
     c->xr_cap = cid;
+    c->xr_pending = true;
     return SKE_OK;
 }
 
@@ -647,7 +686,15 @@ int ske_close(ske_ctx *c) {
 
 int ske_set_stream(ske_ctx *c, void *stream) {
     if (!c) return SKE_EINVAL;
-    c->st = stream ? (hipStream_t)stream : c->own;
+    hipStream_t next = stream ? (hipStream_t)stream : c->own;
+    // leaving the stream of the last scratch use: cover it now, while the
+    // stream is known to be alive
+    if (next != c->st && c->xr_pending && c->xr_stream == c->st) {
+        bool covered = false;
+        const int rc = xr_flush(c, &covered);
+        if (rc) return rc;
+    }
+    c->st = next;
     return SKE_OK;
 }
 
@@ -1800,6 +1847,13 @@ int ske_capture_end(ske_ctx *c, void **graph_out) {
 
 int ske_graph_launch(ske_ctx *c, void *graph) {
     if (!c || !graph) return SKE_EINVAL;
+    // a direct scratch use on another stream before the replay
+    if (c->xr_done && c->xr_stream && c->xr_stream != c->st && c->xr_cap == 0) {
+        bool covered = false;
+        const int rc = xr_flush(c, &covered);
+        if (rc) return rc;
+        if (covered) HIPCHK(c, hipStreamWaitEvent(c->st, c->xr_done, 0));
+    }
     HIPCHK(c, hipGraphLaunch(hipGraphExec_t(graph), c->st));
     // a replay may hold scratch users (the partitioned / XCD-partitioned K1):
     // a later direct launch on another stream waits for it.  Two replays of
@@ -1809,6 +1863,7 @@ int ske_graph_launch(ske_ctx *c, void *graph) {
         HIPCHK(c, hipEventRecord(c->xr_done, c->st));
         c->xr_stream = c->st;
         c->xr_cap = 0;
+        c->xr_pending = false;
     }
     return SKE_OK;
 }
