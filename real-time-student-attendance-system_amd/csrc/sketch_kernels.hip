@@ -349,6 +349,20 @@ __device__ __forceinline__ uint4 max_u8x16(uint4 a, uint4 b) {
 
 // Max over the 16-B chunk `chunk` of the keys srcs[s0..s1) (slots index the
 // slab; srcs == nullptr: keys s0..s1), four loads in flight per step.
+#ifndef SKE_K2_NT
+#define SKE_K2_NT 0
+#endif
+// one 16-B chunk of a key's registers (rollups stream the slab once: nt)
+__device__ __forceinline__ uint4 ld_regs16(const uint8_t *p) {
+    typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+    if constexpr (SKE_K2_NT != 0) {
+        const v4 x = __builtin_nontemporal_load(reinterpret_cast<const v4 *>(p));
+        return make_uint4(x[0], x[1], x[2], x[3]);
+    } else {
+        return *reinterpret_cast<const uint4 *>(p);
+    }
+}
+
 __device__ __forceinline__ uint4 max_keys(const uint8_t *__restrict__ regs, const uint32_t *srcs,
                                           uint32_t s0, uint32_t s1, uint32_t chunk, uint4 v) {
     uint32_t s = s0;
@@ -357,13 +371,13 @@ __device__ __forceinline__ uint4 max_keys(const uint8_t *__restrict__ regs, cons
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const uint32_t key = srcs ? srcs[s + q] : s + q;
-            r[q] = reinterpret_cast<const uint4 *>(regs + size_t(key) * kHllRegs)[chunk];
+            r[q] = ld_regs16(regs + size_t(key) * kHllRegs + size_t(chunk) * 16);
         }
         v = max_u8x16(max_u8x16(v, r[0]), max_u8x16(max_u8x16(r[1], r[2]), r[3]));
     }
     for (; s < s1; s++) {
         const uint32_t key = srcs ? srcs[s] : s;
-        v = max_u8x16(v, reinterpret_cast<const uint4 *>(regs + size_t(key) * kHllRegs)[chunk]);
+        v = max_u8x16(v, ld_regs16(regs + size_t(key) * kHllRegs + size_t(chunk) * 16));
     }
     return v;
 }
@@ -455,9 +469,9 @@ __global__ void __launch_bounds__(64 * kK2Waves)
     uint32_t g = blockIdx.x * kK2Waves + wave;
     uint4 v[16];
     if (g < nkeys) {
-        const uint4 *src = reinterpret_cast<const uint4 *>(regs + size_t(slots ? slots[g] : g) * kHllRegs);
+        const uint8_t *src = regs + size_t(slots ? slots[g] : g) * kHllRegs;
 #pragma unroll
-        for (int q = 0; q < 16; q++) v[q] = src[q * 64 + lane];  // coalesced 1 KiB per step
+        for (int q = 0; q < 16; q++) v[q] = ld_regs16(src + (q * 64 + lane) * 16);  // coalesced 1 KiB per step
     }
     wave_sync();
     uint32_t e = 0;  // histograms waiting for their estimate
@@ -465,10 +479,9 @@ __global__ void __launch_bounds__(64 * kK2Waves)
         const uint32_t gn = g + stride;
         uint4 nv[16];
         if (gn < nkeys) {  // the next key's registers fly while this one is binned
-            const uint4 *src =
-                reinterpret_cast<const uint4 *>(regs + size_t(slots ? slots[gn] : gn) * kHllRegs);
+            const uint8_t *src = regs + size_t(slots ? slots[gn] : gn) * kHllRegs;
 #pragma unroll
-            for (int q = 0; q < 16; q++) nv[q] = src[q * 64 + lane];
+            for (int q = 0; q < 16; q++) nv[q] = ld_regs16(src + (q * 64 + lane) * 16);
         }
 #pragma unroll
         for (int q = 0; q < 16; q++) {

@@ -104,6 +104,28 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t part_rsrc(const void *p, uint3
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, int(nbytes), 0x00020000);
 }
 
+// Streams read or written once take the non-temporal policy (`nt`): pass B's
+// probe records always; SKE_NT bits select the rest -- 1 pass B's run
+// boundaries, 2 pass A's ids and offsets, 4 pass A's record copy-out, 8 pass
+// A's HLL words and fail bytes, 16 pass C's streams (fail bytes, slots, HLL
+// words, answers), 32 pass C's register pre-check loads.  Measured at C3 (A/B,
+// two alternations): records nt: pass B 0.276 -> 0.260 ms; + bits 1|2|4:
+// 0.25 ms; bits 8 and 16 neutral to slightly slower; bit 32 makes pass C
+// 0.39 -> 0.59 ms (the raising CAS no longer finds its line near).  Default 7.
+#ifndef SKE_NT
+#define SKE_NT 7
+#endif
+typedef uint32_t part_u32x4 __attribute__((ext_vector_type(4)));
+template <int BIT, class T> __device__ __forceinline__ T nt_ld(const T *p) {
+    if constexpr ((SKE_NT & BIT) != 0) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <int BIT, class T> __device__ __forceinline__ void nt_st(T *p, T v) {
+    if constexpr ((SKE_NT & BIT) != 0) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+template <int BIT> __device__ __forceinline__ constexpr int nt_aux() { return (SKE_NT & BIT) ? 2 : 0; }
+
 struct PartId {
     uint32_t b, len;
     uint64_t w0, w1;
@@ -117,8 +139,8 @@ __device__ __forceinline__ void part_id_load(const __amdgpu_buffer_rsrc_t &rb, u
     const bool sh = d.len && d.len <= 8;
     const uint32_t o0 = sh ? (b & ~7u) : 0xfffffff8u;
     const uint32_t o1 = (sh && s8 + d.len > 8) ? o0 + 8 : o0;
-    d.w0 = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rb, o0, 0, 0));
-    d.w1 = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rb, o1, 0, 0));
+    d.w0 = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rb, o0, 0, nt_aux<2>()));
+    d.w1 = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rb, o1, 0, nt_aux<2>()));
 }
 
 __device__ __forceinline__ void part_hash3(const uint8_t *bytes, const PartId &d, uint64_t &ha, uint64_t &hb,
@@ -304,8 +326,8 @@ __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part
     auto offsets = [&](uint32_t t, uint32_t u, uint32_t &b, uint32_t &e, uint32_t &sl) {
         const uint32_t i = t * kTile + u * kA2Threads + tid;
         const uint32_t ic = i < A.n ? i : A.n - 1;
-        b = A.offs ? A.offs[ic] : ic * A.fixed_w;
-        e = A.offs ? A.offs[ic + 1] : b + A.fixed_w;
+        b = A.offs ? nt_ld<2>(A.offs + ic) : ic * A.fixed_w;
+        e = A.offs ? nt_ld<2>(A.offs + ic + 1) : b + A.fixed_w;
         sl = kPre ? A.slot[ic] : 0;
     };
     uint32_t gt0, gt1;
@@ -350,13 +372,13 @@ __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part
                 uint32_t idx, rank;
                 hll_patlen(hh, idx, rank);
                 if (!kPre) {
-                    A.hllw[i] = idx | (rank << 16);
+                    nt_st<8>(A.hllw + i, idx | (rank << 16));
                 } else if (slc[u] < A.nslots) {
                     hv[u] = idx | (rank << 16);
                     wv[u] = *reinterpret_cast<const uint32_t *>(A.regs + (uint64_t(slc[u]) << kHllP) +
                                                                 (idx & ~3u));
                 }
-                A.fail[i] = 0;
+                nt_st<8>(A.fail + i, uint8_t(0));
             }
             // bit 19 + tile_log of a record: its slice's parity (pass B's pairs)
             const uint32_t rbase = (lu << kPSliceLog) | 0x80000000u;
@@ -427,9 +449,9 @@ __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part
         for (uint32_t g = tid; g <= S; g += kA2Threads) scnt2[par ^ 1][g] = g << 16;
         __syncthreads();
         const uint32_t total = scnt[S];
-        uint4 *dst = reinterpret_cast<uint4 *>(A.rec + size_t(t) * A.stride);
-        const uint4 *src = reinterpret_cast<const uint4 *>(srec);
-        for (uint32_t j = tid; j * 4 < total; j += kA2Threads) dst[j] = src[j];
+        part_u32x4 *dst = reinterpret_cast<part_u32x4 *>(A.rec + size_t(t) * A.stride);
+        const part_u32x4 *src = reinterpret_cast<const part_u32x4 *>(srec);
+        for (uint32_t j = tid; j * 4 < total; j += kA2Threads) nt_st<4>(dst + j, src[j]);
     }
 }
 
@@ -505,8 +527,8 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
         auto load_be8 = [&](uint32_t tg0, uint32_t &B, uint32_t &E) {
             const uint32_t t = tg0 + (lane / kPbGroup) * kStep + lane % kPbGroup;
             const bool in = t < tb;
-            B = __builtin_amdgcn_raw_buffer_load_b32(roff, in ? (orow + t) * 4 : kOOR, 0, 0);
-            E = __builtin_amdgcn_raw_buffer_load_b32(roff, in ? (erow + t) * 4 : kOOR, 0, 0);
+            B = __builtin_amdgcn_raw_buffer_load_b32(roff, in ? (orow + t) * 4 : kOOR, 0, nt_aux<1>());
+            E = __builtin_amdgcn_raw_buffer_load_b32(roff, in ? (erow + t) * 4 : kOOR, 0, nt_aux<1>());
         };
         // 16-byte pieces qq, qq + 8, ... of the run from the 128-B line holding
         // its start: every piece is one whole line (one request, not two)
@@ -516,7 +538,7 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
             for (uint32_t c = 0; c < R; c++) {
                 const uint32_t i = s0 + c * 32 + qq * 4;
                 r[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     rrec, i < e ? (base + i) * 4 : kOOR, 0, 0));
+                                                     rrec, i < e ? (base + i) * 4 : kOOR, 0, 2));
             }
         };
         uint32_t tg = ta + wave * kPbGroup;
@@ -657,7 +679,7 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
             sh[u] = 0;
             cur[u] = 0;
             if (i < end) {
-                for (uint32_t l = 0; l < A.nlinks; l++) valid[u] |= A.fail[size_t(l) * A.fail_stride + i] == 0;
+                for (uint32_t l = 0; l < A.nlinks; l++) valid[u] |= nt_ld<16>(A.fail + size_t(l) * A.fail_stride + i) == 0;
                 if (valid[u] && A.pre) {
                     // pass A read the register: only raises remain, from its word
                     const uint32_t hv = A.hllw[i];
@@ -671,11 +693,11 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
                         cur[u] = A.oldw[i];
                     }
                 } else if (valid[u]) {
-                    const uint32_t s = A.slot[i];
+                    const uint32_t s = nt_ld<16>(A.slot + i);
                     if (s >= A.nslots) {
                         atomicOr(A.err, 1u);
                     } else {
-                        const uint32_t hv = A.hllw[i];
+                        const uint32_t hv = nt_ld<16>(A.hllw + i);
                         const uint32_t ridx = hv & 0xffffu;
                         w[u] = reinterpret_cast<uint32_t *>(A.regs + (uint64_t(s) << kHllP) + (ridx & ~3u));
                         sh[u] = (ridx & 3) * 8;
@@ -686,7 +708,7 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
         }
         if (!A.pre) {
 #pragma unroll
-            for (int u = 0; u < U; u++) cur[u] = w[u] ? *w[u] : 0xffffffffu;
+            for (int u = 0; u < U; u++) cur[u] = w[u] ? nt_ld<32>(w[u]) : 0xffffffffu;
         }
 #pragma unroll
         for (int u = 0; u < U; u++)
@@ -695,7 +717,7 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const uint64_t i = base + uint64_t(u) * T + tid;
-                if (i < end) A.out[i] = valid[u];
+                if (i < end) nt_st<16>(A.out + i, uint8_t(valid[u]));
             }
         }
     }
