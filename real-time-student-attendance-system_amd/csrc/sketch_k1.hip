@@ -28,6 +28,14 @@
 
 namespace ske {
 
+// cache policy of the swipe streams (read or written once): SKE_K1_NT bits --
+// 1 offsets and slots, 2 id words, 4 answers -- take `nt`.  Off: at C2 the
+// persistent kernel was 1-4 % slower with bits 3 or 7 (A/B, two alternations)
+#ifndef SKE_K1_NT
+#define SKE_K1_NT 0
+#endif
+template <int BIT> __device__ __forceinline__ constexpr int k1_aux() { return (SKE_K1_NT & BIT) ? 2 : 0; }
+
 constexpr uint32_t kK1Block = 1024;     // threads per block, one block per CU
 constexpr uint32_t kK1Waves = kK1Block / 64;
 constexpr int kK1MaxPieces = 10;        // 1 KiB LDS pieces per wave (152 KiB / 16 waves)
@@ -193,13 +201,13 @@ __device__ __forceinline__ void k1_issue_a(const K1View &V, uint32_t base, uint3
         in.idx[u] = i;
         const uint32_t ic = in.act[u] ? i : V.n - 1;  // clamped: every load stays in bounds
         if (V.offs_p) {
-            in.b[u] = __builtin_amdgcn_raw_buffer_load_b32(V.offs, ic * 4, 0, 0);
-            in.e[u] = __builtin_amdgcn_raw_buffer_load_b32(V.offs, ic * 4 + 4, 0, 0);
+            in.b[u] = __builtin_amdgcn_raw_buffer_load_b32(V.offs, ic * 4, 0, k1_aux<1>());
+            in.e[u] = __builtin_amdgcn_raw_buffer_load_b32(V.offs, ic * 4 + 4, 0, k1_aux<1>());
         } else {
             in.b[u] = ic * V.fixed_w;
             in.e[u] = in.b[u] + V.fixed_w;
         }
-        in.sl[u] = kHll ? __builtin_amdgcn_raw_buffer_load_b32(V.slot, ic * 4, 0, 0) : 0u;
+        in.sl[u] = kHll ? __builtin_amdgcn_raw_buffer_load_b32(V.slot, ic * 4, 0, k1_aux<1>()) : 0u;
     }
 }
 
@@ -212,8 +220,8 @@ __device__ __forceinline__ void k1_issue_b(const K1View &R, K1In<U> &in) {
         const uint32_t len = in.e[u] - in.b[u], s8 = in.b[u] & 7;
         const uint32_t o0 = len ? (in.b[u] & ~7u) : 0xfffffff8u;
         const uint32_t o1 = (s8 + len > 8 && len <= 8) ? o0 + 8 : o0;
-        in.w0[u] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(R.bytes, o0, 0, 0));
-        in.w1[u] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(R.bytes, o1, 0, 0));
+        in.w0[u] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(R.bytes, o0, 0, k1_aux<2>()));
+        in.w1[u] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(R.bytes, o1, 0, k1_aux<2>()));
     }
 }
 
@@ -360,7 +368,7 @@ __device__ __forceinline__ void k1_commit(const K1Args &A, const K1View &V, cons
 #pragma unroll
         for (int u = 0; u < U; u++)  // lanes past the chunk store out of range (dropped)
             __builtin_amdgcn_raw_buffer_store_b8(uint8_t(valid[u]), r_out, h.act[u] ? h.idx[u] : 0xffffffffu,
-                                                 0, 0);
+                                                 0, k1_aux<4>());
     }
 }
 

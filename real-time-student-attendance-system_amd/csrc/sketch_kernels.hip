@@ -349,10 +349,13 @@ __device__ __forceinline__ uint4 max_u8x16(uint4 a, uint4 b) {
 
 // Max over the 16-B chunk `chunk` of the keys srcs[s0..s1) (slots index the
 // slab; srcs == nullptr: keys s0..s1), four loads in flight per step.
+// One 16-B chunk of a key's registers.  The rollups (K2, K3) stream the slab
+// once, with the non-temporal policy: C5 per-lecture unions 4.94 -> 4.67 ms
+// (6.05 -> 6.40 TB/s), PFCOUNT-each 5.24 -> 5.20 ms, PFMERGE unchanged
+// (tools/bench_rollup.py A/B, two alternations).
 #ifndef SKE_K2_NT
-#define SKE_K2_NT 0
+#define SKE_K2_NT 1
 #endif
-// one 16-B chunk of a key's registers (rollups stream the slab once: nt)
 __device__ __forceinline__ uint4 ld_regs16(const uint8_t *p) {
     typedef uint32_t v4 __attribute__((ext_vector_type(4)));
     if constexpr (SKE_K2_NT != 0) {

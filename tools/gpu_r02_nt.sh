@@ -15,3 +15,12 @@ for r in 1 2; do
     echo "$(basename $lib) $(tail -1 gpurun_out/nt_roll.json | cut -c1-600)"
   done
 done
+# the LDS K1 (C2) with nt swipe streams
+for r in 1 2; do
+  for lib in real-time-student-attendance-system_amd/csrc/libsketch.so tools/ab/libsketch_k1nt3.so tools/ab/libsketch_k1nt7.so; do
+    SKE_LIB=$lib timeout -k 10 200 python bench.py --config c2 --steps 20 --warmup 5 --no-cpu --no-check > gpurun_out/nt_c2.json 2> gpurun_out/nt_c2.err || { tail -5 gpurun_out/nt_c2.err; exit 1; }
+    python -c "
+import json,sys; d=json.loads(open('gpurun_out/nt_c2.json').read().strip().splitlines()[-1])
+print(sys.argv[1], 'c2 %.4e/s ms/step %.5f kernel %.5f' % (d['value'], d['ms_per_step'], d['roofline']['kernel_ms']))" $(basename $lib)
+  done
+done
