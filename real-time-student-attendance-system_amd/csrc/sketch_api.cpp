@@ -164,9 +164,7 @@ int stage_items(ske_ctx *c, const uint8_t *bytes, const uint32_t *offs, uint64_t
         out->offs = offs;
         return SKE_OK;
     }
-    if (!offs || (!bytes && offs[n] != offs[0])) return SKE_EINVAL;
-    for (uint64_t i = 0; i < n; i++)
-        if (offs[i + 1] < offs[i]) return SKE_EINVAL;
+    if (!offs || (!bytes && offs[n] != offs[0]) || offs[n] < offs[0]) return SKE_EINVAL;
     const uint64_t b0 = offs[0], total = uint64_t(offs[n]) - b0;
     int rc = SKE_OK;
     uint8_t *db = (uint8_t *)stage_buf(c, slot_bytes, total + 16, &rc);
@@ -174,6 +172,14 @@ int stage_items(ske_ctx *c, const uint8_t *bytes, const uint32_t *offs, uint64_t
     if (rc) return rc;
     if (total) HIPCHK(c, hipMemcpyAsync(db, bytes + b0, total, hipMemcpyHostToDevice, c->st));
     HIPCHK(c, hipMemcpyAsync(dof, offs, (n + 1) * 4, hipMemcpyHostToDevice, c->st));
+    // the offsets are checked while the copies run (no kernel reads them
+    // before this returns); a branch-free pass the compiler vectorises
+    uint32_t bad = 0;
+    for (uint64_t i = 0; i < n; i++) bad |= uint32_t(offs[i + 1] < offs[i]);
+    if (bad) {
+        HIPCHK(c, hipStreamSynchronize(c->st));  // the copies still read the caller's buffers
+        return SKE_EINVAL;
+    }
     out->bytes = db - b0;
     out->offs = dof;
     return SKE_OK;

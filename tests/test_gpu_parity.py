@@ -632,3 +632,38 @@ def test_pfcount_each_many_keys_vs_oracle(client, orc):
     out = np.zeros(cap, np.uint64)
     client.ctx.call("ske_hll_pfcount_each", None, cap, out.ctypes.data_as(C.c_void_p), 0)
     assert np.array_equal(out[slots], want)
+
+
+def test_host_staged_swipes_reject_decreasing_offsets(engine, pkg, orc):
+    """ske_swipes with host buffers (SKE_MEM_HOST) checks the offsets while the
+    copies run: decreasing offsets return SKE_EINVAL before any kernel reads
+    them (registers untouched); a valid call right after answers == the oracle."""
+    from rtsas_amd._lib import SKE_EINVAL, SKE_MEM_HOST
+    rng = np.random.default_rng(11)
+    engine.reserve(0, 0.01, 10_000)
+    members = [b"%d" % v for v in rng.choice(np.arange(10**6, 10**7), 5000, replace=False)]
+    buf = np.frombuffer(b"".join(members), np.uint8).copy()
+    offs = np.concatenate([[0], np.cumsum([len(m) for m in members])]).astype(np.uint32)
+    engine.ctx.call("ske_bf_madd", 0, C.c_void_p(buf.ctypes.data), C.c_void_p(offs.ctypes.data),
+                    len(members), None, SKE_MEM_HOST)
+    engine.hll_reserve(8)
+    n = 4000
+    items = members[:2000] + [b"%d" % v for v in rng.integers(10**7, 10**8, 2000)]
+    ib = np.frombuffer(b"".join(items), np.uint8).copy()
+    io = np.concatenate([[0], np.cumsum([len(x) for x in items])]).astype(np.uint32)
+    slot = rng.integers(0, 8, n).astype(np.uint32)
+    out = np.zeros(n, np.uint8)
+    bad = io.copy()
+    bad[1000], bad[1001] = bad[1001], bad[1000]
+    ptr = lambda a: C.c_void_p(a.ctypes.data)
+    with pytest.raises(pkg.SketchLibError) as ei:
+        engine.ctx.call("ske_swipes", 0, ptr(slot), ptr(ib), ptr(bad), n, ptr(out), SKE_MEM_HOST)
+    assert ei.value.code == SKE_EINVAL
+    assert not engine.registers_all(8).any()
+    engine.ctx.call("ske_swipes", 0, ptr(slot), ptr(ib), ptr(io), n, ptr(out), SKE_MEM_HOST)
+    chain = orc.Chain(10_000, 0.01)
+    chain.madd_packed(buf, offs)
+    regs = np.zeros((8, 16384), np.uint8)
+    want, _, _ = orc.process_swipes(chain, regs, slot, ib, io)
+    assert np.array_equal(out, want)
+    assert np.array_equal(engine.registers_all(8), regs)
