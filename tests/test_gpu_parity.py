@@ -569,12 +569,17 @@ def test_pfmerge_many_sources_two_level(client):
     assert [int(out[s]) for s in slots] == client.pfcount_each([f"day{i}" for i in range(0, 3000, 250)]).tolist()
 
 
-def test_property_swipes_vs_oracle(pkg, orc):
+@pytest.mark.parametrize("variant", [-1, 3])
+def test_property_swipes_vs_oracle(pkg, orc, variant):
     """Hypothesis: fused swipes on random byte ids (0..64 B), random key skews
     and batch sizes from 0 to a few thousand == the oracle's sequential
-    BF.EXISTS + PFADD, answers and registers."""
+    BF.EXISTS + PFADD, answers and registers; through the variant the library
+    picks (the LDS K1 for this filter) and through the partitioned K1 forced
+    (variant 3: ragged tiles, empty and long ids through its generic hash)."""
     from hypothesis import HealthCheck, given, settings, strategies as st
     client = pkg.SketchClient(decode_responses=True)
+    if variant >= 0:
+        client.ctx.call("ske_set_option", b"variant", variant)
     members = [bytes([i % 256, i // 256, 7]) * (1 + i % 5) for i in range(3000)]
     client.execute_command("BF.RESERVE", "bf", 0.01, 5000)
     client.execute_command("BF.MADD", "bf", *members)
