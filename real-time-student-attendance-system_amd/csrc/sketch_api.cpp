@@ -72,6 +72,7 @@ struct ske_ctx {
     // staging buffers (grow on demand)
     void *stg[8] = {};
     size_t stg_cap[8] = {};
+    HostStager *hs = nullptr;  // pinned double buffer + copy threads for pageable inputs (lazy)
     unsigned int *err = nullptr;
     unsigned long long *stats = nullptr;
     int pb = 2;           // K1 tile: swipes per thread in flight (1, 2, 4, 8)
@@ -170,14 +171,15 @@ int stage_items(ske_ctx *c, const uint8_t *bytes, const uint32_t *offs, uint64_t
     uint8_t *db = (uint8_t *)stage_buf(c, slot_bytes, total + 16, &rc);
     uint32_t *dof = (uint32_t *)stage_buf(c, slot_offs, (n + 1) * 4, &rc);
     if (rc) return rc;
-    if (total) HIPCHK(c, hipMemcpyAsync(db, bytes + b0, total, hipMemcpyHostToDevice, c->st));
-    HIPCHK(c, hipMemcpyAsync(dof, offs, (n + 1) * 4, hipMemcpyHostToDevice, c->st));
-    // the offsets are checked while the copies run (no kernel reads them
-    // before this returns); a branch-free pass the compiler vectorises
-    uint32_t bad = 0;
-    for (uint64_t i = 0; i < n; i++) bad |= uint32_t(offs[i + 1] < offs[i]);
-    if (bad) {
-        HIPCHK(c, hipStreamSynchronize(c->st));  // the copies still read the caller's buffers
+    if (!c->hs) c->hs = stager_new();
+    // the offsets are checked (never decreasing) as they are copied; no
+    // kernel reads them before this returns
+    // (bytes first: a direct offsets copy is checked while both DMAs run)
+    bool ok = true;
+    if (total) HIPCHK(c, stage_h2d(c->hs, db, bytes + b0, total, c->st, false, nullptr));
+    HIPCHK(c, stage_h2d(c->hs, dof, offs, (n + 1) * 4, c->st, true, &ok));
+    if (!ok) {
+        HIPCHK(c, hipStreamSynchronize(c->st));  // the copies may still read the caller's buffers
         return SKE_EINVAL;
     }
     out->bytes = db - b0;
@@ -193,7 +195,8 @@ int stage_u32(ske_ctx *c, const uint32_t *p, uint64_t n, int mem, int slot, cons
     int rc = SKE_OK;
     uint32_t *d = (uint32_t *)stage_buf(c, slot, n * 4, &rc);
     if (rc) return rc;
-    HIPCHK(c, hipMemcpyAsync(d, p, n * 4, hipMemcpyHostToDevice, c->st));
+    if (!c->hs) c->hs = stager_new();
+    HIPCHK(c, stage_h2d(c->hs, d, p, n * 4, c->st, false, nullptr));
     *out = d;
     return SKE_OK;
 }
@@ -666,6 +669,7 @@ int ske_close(ske_ctx *c) {
     if (c->sig) (void)hipFree(c->sig);
     for (int i = 0; i < 8; i++)
         if (c->stg[i]) (void)hipFree(c->stg[i]);
+    stager_delete(c->hs);
     if (c->err) (void)hipFree(c->err);
     if (c->zero16) (void)hipFree(c->zero16);
     if (c->xr_done) (void)hipEventDestroy(c->xr_done);

@@ -192,4 +192,11 @@ hipError_t launch_bf_resolve(const LinkDev &L, uint64_t n, const uint64_t *ha, c
 hipError_t launch_bf_fill_rest(uint64_t n, uint8_t *state, int8_t *res, int8_t code, int cus,
                                hipStream_t st);
 
+// host -> device staging of pageable caller buffers (sketch_host.cpp)
+struct HostStager;
+HostStager *stager_new();
+void stager_delete(HostStager *s);
+hipError_t stage_h2d(HostStager *s, void *dst, const void *src, size_t bytes, hipStream_t st, bool mono,
+                     bool *ok);
+
 }  // namespace ske
