@@ -127,14 +127,16 @@ void stager_delete(HostStager *s) {
     delete s;
 }
 
-static bool is_pinned(const void *p) {
+// memory HIP knows (pinned host, device, managed): copied by the DMA engine
+// as it is; false for pageable memory
+static bool hip_known(const void *p) {
     hipPointerAttribute_t a{};
     const hipError_t e = hipPointerGetAttributes(&a, p);
     if (e != hipSuccess) {
         (void)hipGetLastError();  // pageable memory: not an error of ours
         return false;
     }
-    return a.type == hipMemoryTypeHost;
+    return a.type == hipMemoryTypeHost || a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
 static bool u32_monotone(const uint32_t *u, size_t n) {
@@ -154,10 +156,15 @@ hipError_t stage_h2d(HostStager *s, void *dst, const void *src, size_t bytes, hi
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     hipError_t e = hipStreamIsCapturing(st, &cs);
     if (e != hipSuccess) return e;
-    if (bytes < kDirectMax || cs != hipStreamCaptureStatusNone || is_pinned(src)) {
+    if (bytes < kDirectMax || cs != hipStreamCaptureStatusNone || hip_known(src)) {
         e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
         if (e != hipSuccess || !mono || !ok) return e;
-        // checked while the DMA runs: by the pool when large
+        // checked while the DMA runs: by the pool when large (device memory
+        // is not readable here: a device offsets array stays unchecked, as on
+        // the SKE_MEM_DEVICE path)
+        hipPointerAttribute_t pa{};
+        if (hipPointerGetAttributes(&pa, src) == hipSuccess && pa.type == hipMemoryTypeDevice) return e;
+        (void)hipGetLastError();
         if (bytes < kDirectMax) {
             *ok = u32_monotone(static_cast<const uint32_t *>(src), bytes / 4);
         } else {
