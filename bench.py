@@ -293,8 +293,9 @@ def pass_bytes(n, nvalid, probes, width, fixed, geometry, lds_k1=False, slab_byt
         "k_part_a": n * (width + s_off) + rec + 4 * (nslices + 1) * ntiles + 4 * n + n * len(geometry),
         # probe records + their run boundaries in, the filter staged once
         "k_part_b": rec + 8 * nslices * ntiles + filter_bytes,
-        # fail byte, HLL word, slot in, answer out; one sector per valid swipe's register
-        "k_part_c": n * (len(geometry) + 4 + 4 + 1) + 64 * nvalid,
+        # fail byte, HLL word, slot in, answer out; per valid swipe its register's
+        # sector read + written (SURVEY §8d's 128·v, as the one-kernel K1 above)
+        "k_part_c": n * (len(geometry) + 4 + 4 + 1) + 128 * nvalid,
     }
 
 

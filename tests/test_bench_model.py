@@ -24,7 +24,7 @@ def test_partitioned_pass_bytes_c3():
     rec = 4 * k * n
     assert alg["k_part_a"] == n * (8 + 4) + rec + 4 * (nslices + 1) * ntiles + 4 * n + n
     assert alg["k_part_b"] == rec + 8 * nslices * ntiles + bits // 8
-    assert alg["k_part_c"] == n * (1 + 4 + 4 + 1) + 64 * nvalid
+    assert alg["k_part_c"] == n * (1 + 4 + 4 + 1) + 128 * nvalid   # 128 B per valid swipe
     assert alg["k1_stage"] == 0
 
 
