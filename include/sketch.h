@@ -14,9 +14,11 @@
  *   - return 0 (SKE_OK) or a negative SKE_E* code; no exception crosses the ABI;
  *     ske_strerror() maps a code to the Redis / RedisBloom error text.
  *   - the caller owns every input / output buffer.  `mem` says where the
- *     buffers live: SKE_MEM_HOST (pageable host memory, staged through the
- *     context's device buffers) or SKE_MEM_DEVICE (HIP device pointers, e.g.
- *     torch-ROCm data_ptr(), used in place on the context stream).
+ *     buffers live: SKE_MEM_HOST (host memory, staged through the context's
+ *     device buffers; pageable inputs above 8 MB go through two pinned 32 MB
+ *     buffers filled by up to 8 host threads the context starts on first use)
+ *     or SKE_MEM_DEVICE (HIP device pointers, e.g. torch-ROCm data_ptr(), used
+ *     in place on the context stream).
  *   - packed items: `bytes` + `offs[n+1]` (u32 byte offsets, offs[0] may be
  *     non-zero).  Device byte buffers must stay readable up to the next 8-byte
  *     boundary after bytes+offs[n] (any hipMalloc / torch allocation is).
