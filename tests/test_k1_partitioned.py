@@ -261,3 +261,39 @@ def test_many_pipelined_small_units(engine, orc, mode, ovl, pre):
         v, _, _ = orc.process_swipes(chain, regs, slot.astype(np.uint32), buf, offs)
         assert np.array_equal(o.to_host(np.uint8, b.n), v)
     assert np.array_equal(engine.registers_all(w.n_keys), regs)
+
+
+def test_host_staged_large_batch_equals_device_resident(engine, orc):
+    """A 3M-swipe batch handed over in pageable host memory (SKE_MEM_HOST) is
+    staged through the library's pinned double buffer by its copy threads
+    (inputs above 8 MB, several 32 MB chunks); answers and registers equal the
+    same batch run device-resident.  Offsets that decrease inside a later
+    chunk are refused (SKE_EINVAL) with the registers untouched."""
+    import ctypes as C
+    from rtsas_amd._lib import SKE_EINVAL, SKE_MEM_HOST
+    from rtsas_amd.engine import DeviceBuffer
+    from rtsas_amd import SketchLibError
+    w, p = _c3_small(engine)
+    n = 3_000_000
+    b = engine.swipe_batch(p, 0, n)
+    buf, offs, slot = b.to_host()
+    buf = np.concatenate([buf, np.zeros(16, np.uint8)])
+    assert buf.nbytes > (8 << 20) and offs.nbytes > (8 << 20)
+    ptr = lambda a: C.c_void_p(a.ctypes.data)
+    bad = offs.copy()
+    k = 2_500_000                      # inside the second 32 MB chunk of the bytes, late in the offsets
+    bad[k], bad[k + 1] = bad[k + 1], bad[k]
+    out = np.zeros(n, np.uint8)
+    with pytest.raises(SketchLibError) as ei:
+        engine.ctx.call("ske_swipes", 0, ptr(slot), ptr(buf), ptr(bad), n, ptr(out), SKE_MEM_HOST)
+    assert ei.value.code == SKE_EINVAL
+    assert not engine.registers_all(w.n_keys).any()
+    engine.ctx.call("ske_swipes", 0, ptr(slot), ptr(buf), ptr(offs), n, ptr(out), SKE_MEM_HOST)
+    host_regs = engine.registers_all(w.n_keys).copy()
+    engine.hll_reserve(2 * w.n_keys)
+    b.slot.from_host(slot + w.n_keys)
+    dout = DeviceBuffer(engine.ctx, n)
+    engine.swipes(0, b, dout)
+    assert np.array_equal(out, dout.to_host(np.uint8, n))
+    assert np.array_equal(engine.registers_all(2 * w.n_keys)[w.n_keys:], host_regs)
+    assert out.sum() > 0.8 * n
