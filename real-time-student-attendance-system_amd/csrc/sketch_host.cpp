@@ -30,16 +30,14 @@ namespace {
 class CopyPool {
   public:
     explicit CopyPool(int n) {
-        for (int i = 0; i < n; i++) th_.emplace_back([this, i] { work(i); });
-    }
-    ~CopyPool() {
-        {
-            std::lock_guard<std::mutex> g(m_);
-            quit_ = true;
+        try {
+            for (int i = 0; i < n; i++) th_.emplace_back([this, i] { work(i); });
+        } catch (...) {  // the threads already started are stopped before rethrowing
+            stop();
+            throw;
         }
-        cv_.notify_all();
-        for (auto &t : th_) t.join();
     }
+    ~CopyPool() { stop(); }
     // copy n bytes (dst nullptr: none); with `mono`, also check the u32
     // array never decreases (returns false if it does)
     bool copy(void *dst, const void *src, size_t n, bool mono) {
@@ -57,6 +55,15 @@ class CopyPool {
     }
 
   private:
+    void stop() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+        th_.clear();
+    }
     void work(int i) {
         uint64_t seen = 0;
         for (;;) {
@@ -108,6 +115,7 @@ constexpr int kThreads = 8;
 
 struct HostStager {
     CopyPool *pool = nullptr;
+    bool no_pool = false;  // the threads could not be started: plain hipMemcpyAsync
     void *pin[2] = {nullptr, nullptr};
     hipEvent_t ev[2] = {nullptr, nullptr};
     bool busy[2] = {false, false};
@@ -125,6 +133,18 @@ void stager_delete(HostStager *s) {
     }
     delete s->pool;
     delete s;
+}
+
+// the copy threads, started on first use (nullptr if they cannot be)
+static CopyPool *get_pool(HostStager *s) {
+    if (!s->pool && !s->no_pool) {
+        try {
+            s->pool = new CopyPool(kThreads);
+        } catch (...) {
+            s->no_pool = true;
+        }
+    }
+    return s->pool;
 }
 
 // memory HIP knows (pinned host, device, managed): copied by the DMA engine
@@ -165,15 +185,17 @@ hipError_t stage_h2d(HostStager *s, void *dst, const void *src, size_t bytes, hi
         hipPointerAttribute_t pa{};
         if (hipPointerGetAttributes(&pa, src) == hipSuccess && pa.type == hipMemoryTypeDevice) return e;
         (void)hipGetLastError();
-        if (bytes < kDirectMax) {
-            *ok = u32_monotone(static_cast<const uint32_t *>(src), bytes / 4);
-        } else {
-            if (!s->pool) s->pool = new CopyPool(kThreads);
-            *ok = s->pool->copy(nullptr, src, bytes, true);
-        }
+        CopyPool *pool = bytes < kDirectMax ? nullptr : get_pool(s);
+        *ok = pool ? pool->copy(nullptr, src, bytes, true)
+                   : u32_monotone(static_cast<const uint32_t *>(src), bytes / 4);
         return e;
     }
-    if (!s->pool) s->pool = new CopyPool(kThreads);
+    CopyPool *pool = get_pool(s);
+    if (!pool) {  // no threads: the runtime's own pageable path
+        e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess && mono && ok) *ok = u32_monotone(static_cast<const uint32_t *>(src), bytes / 4);
+        return e;
+    }
     for (int k = 0; k < 2; k++) {
         if (!s->pin[k] && (e = hipHostMalloc(&s->pin[k], kChunk, hipHostMallocDefault)) != hipSuccess) return e;
         if (!s->ev[k] && (e = hipEventCreateWithFlags(&s->ev[k], hipEventDisableTiming)) != hipSuccess) return e;
@@ -188,7 +210,7 @@ hipError_t stage_h2d(HostStager *s, void *dst, const void *src, size_t bytes, hi
         s->next ^= 1;
         if (s->busy[k] && (e = hipEventSynchronize(s->ev[k])) != hipSuccess) return e;
         s->busy[k] = false;
-        good &= s->pool->copy(s->pin[k], src8 + off, len, mono);
+        good &= pool->copy(s->pin[k], src8 + off, len, mono);
         if (mono && off) {  // the chunk boundary (chunks hold whole u32 elements)
             good &= *reinterpret_cast<const uint32_t *>(src8 + off) >= prev_last;
         }
