@@ -5,27 +5,37 @@ Default workload: C3 (configs[2], the configuration BASELINE.md quotes the
 1/2/4/8-GPU curve on), this rank's shard of it: the replicated 10M-student
 Bloom filter (RESERVE 0.001 / 1e7: 19.8 MB, k = 11) preloaded by BF.MADD, a
 Zipf(1.1)-over-lectures x uniform-over-days stream of 8-digit ids with 10 %
-invalid swipes, and this rank's HLL keys (100k at N = 1, 12.5k per rank at
-N = 8; synthetic.shard).  One step = one K1 call over one resident batch of
-16M swipes (answers written, PFADD of the valid ones): the partitioned K1,
-three kernels (sketch_part.hip: hash + probe records, LDS-slice probes,
-answers + register max).  `--config c2` runs C2 (1M swipes, the LDS K1).
+invalid swipes, and the HLL keys this rank owns (distributed.KeyMap:
+MurmurHash64A(key name) mod world over the 100k README-form key names; all
+of them at N = 1, ~12.5k per rank at N = 8).  One step = one K1 call over
+one resident batch of 16M swipes (answers written, PFADD of the valid ones):
+the partitioned K1, three kernels (sketch_part.hip: hash + probe records,
+LDS-slice probes, answers + register max).  `--config c2` runs C2 (1M
+swipes, the LDS K1).
 
 Inputs are generated on the GPU and resident in HBM before timing; every
 step consumes a distinct batch of the stream.  Timing: W untimed warm-up
 steps, then K steps bracketed by barrier + synchronize; value = swipes of all
-ranks / the slowest rank's wall time.  With the library's pass timing on,
-every K1 kernel of the timed steps is bracketed by a HIP event pair on the
-stream it runs on (ske_pass_times): the roofline is priced on the kernel that
-takes the most time, from those live durations.
+ranks / the slowest rank's wall time.  The timed region carries no
+instrumentation.  Per-kernel times for the roofline come from a separate
+REPLAY of the same steps: the register slab is zeroed, the W warm-up steps
+are re-run, and the K steps are replayed with a HIP event pair around every
+K1 kernel on the stream it runs on (ske_pass_times) -- the same batches from
+the same register state, so the same work.
+
+`secondary` (N = 1, default workload): C2 (configs[1], the configuration
+sized for one MI355X) measured in the same process on its own context.
 
 N>1: one process per GPU (torch.distributed.run), RCCL ("nccl") process
 group; every rank runs its own stream over its own key shard with the Bloom
 replicated (no data-path collective; weak scaling).  After timing, every rank
-checks a verification batch against the CPU oracle and the cross-shard
-queries (all_reduce MAX union, reduce_scatter MAX rollup) against the same
-collectives over the oracle's registers; the line carries the outcome under
-"check".
+checks a verification stream through the SHIPPED classes: the stream names
+64 keys of a second universe (distributed.KeyMap), each rank runs K1 on the
+swipes of the keys it owns (or, with --exchange 1, routes its slice through
+distributed.SwipeExchange), and distributed.ShardedSketch answers union
+PFCOUNT, PFCOUNT of every key and a rollup by key name over RCCL; answers,
+registers and every query are compared with the CPU oracle over the whole
+stream ("check").
 
 Prints ONE JSON line on rank 0.
 """
@@ -54,14 +64,19 @@ RANDOM_CAS_GPS = 21.1
 MALL_BYTES = 256 << 20  # Infinity Cache: a slab this small stays on chip
 METRIC = "swipes/sec (fused BF.EXISTS+PFADD) at 1/2/4/8 GPUs; % of HBM peak"
 PASS_NAMES = ["k1", "k_part_a", "k_part_b", "k_part_c"]
+PMC_ROUNDS = ["r03", "r02"]  # newest committed PMC summaries first
+VERIFY_KEYS = 64
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3")
+    ap.add_argument("--secondary", default="auto",
+                    help="config measured after the headline in the same process (N = 1 only); "
+                         "auto = c2 when the headline is c3, none = skip")
     ap.add_argument("--batch", type=int, default=0, help="swipes per step (default: config)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -104,14 +119,15 @@ def parse():
     ap.add_argument("--graph", type=int, default=-1,
                     help="1 = record the K timed steps into a HIP graph and replay it (default for "
                          "the LDS K1); 0 = launch them from the host (default otherwise)")
-    ap.add_argument("--pass-timing", type=int, default=1,
-                    help="1 = HIP events around every K1 kernel of the timed steps (host launches)")
+    ap.add_argument("--pass-replay", type=int, default=1,
+                    help="1 = per-kernel times from an instrumented replay of the same steps "
+                         "after the timed region (the timed region itself is never instrumented)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N>1 (nccl = RCCL over xGMI; gloo only to rehearse "
                          "several ranks on a one-GPU box)")
     ap.add_argument("--layout", default="offsets", choices=["offsets", "fixed"],
                     help="id batch layout: bytes + u32 offsets, or fixed-width ids")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def cpu_threads():
@@ -146,7 +162,7 @@ def oracle_chain(engine, orc, w, p):
     return chain
 
 
-def cpu_baseline(orc, chain, w, b0, seconds):
+def cpu_baseline(orc, chain, w, b0, seconds, key_name):
     """The processor loop attendance_processor.py:100-137 (BF.EXISTS, then
     PFADD when valid) on the host, over a bounded sample of the first batch:
       - the C oracle on all host threads (orc_process_swipes_mt; the value),
@@ -155,7 +171,6 @@ def cpu_baseline(orc, chain, w, b0, seconds):
         BF.EXISTS, PFADD per message) over the oracle, one core (§8d item 1)."""
     import numpy as np
     from datetime import datetime
-    from rtsas_amd import synthetic
     buf, offs, slot = b0.to_host()
     n = min(len(offs) - 1, 1 << 20)
     offs = np.ascontiguousarray(offs[:n + 1])
@@ -179,7 +194,7 @@ def cpu_baseline(orc, chain, w, b0, seconds):
     msgs = []
     for i in range(m):
         sid = bytes(buf[offs[i]:offs[i + 1]]).decode()
-        _, _, lecture, day = synthetic.key_name(w, int(slot[i])).split(":")
+        _, _, lecture, day = key_name(int(slot[i])).split(":")
         msgs.append('{"student_id": %s, "timestamp": "%sT09:00:00", "lecture_id": "%s", '
                     '"is_valid": true, "event_type": "entry"}' % (sid, day, lecture))
     hlls = {}
@@ -203,70 +218,79 @@ def cpu_baseline(orc, chain, w, b0, seconds):
                                            "(attendance_processor.py:100-137 without transport)"}}
 
 
-def verify(engine, orc, chain, w, rank, world, dist, dev):
-    """A verification batch through K1 into 64 spare slots of this rank,
-    compared with the oracle (answers + registers), then the cross-shard
-    queries: union PFCOUNT of the 64 keys of every rank (all_reduce MAX) and
-    the 64 per-key unions across ranks (reduce_scatter MAX), each against the
-    same collective over the oracle's registers."""
+def verify(engine, orc, chain, w, km, rank, world, dist, dev, exchange):
+    """The shipped multi-GPU classes on a verification stream, against the
+    CPU oracle over the WHOLE stream (no collective on the expected side).
+
+    The stream (identical on every rank: same seed, generated on the device)
+    names VERIFY_KEYS keys of a second universe, `vk`, bound above this rank's
+    workload keys (KeyMap base = the workload map's slots_end).  Pre-routed
+    input: each rank runs K1 on the swipes of the keys it owns (ingest
+    routing by owner()); --exchange: each rank hands its slice of the stream
+    to distributed.SwipeExchange.  Then distributed.ShardedSketch, over a
+    client that KeyMap.bind named, answers union PFCOUNT, PFCOUNT of every key
+    and a rollup (RCCL at N > 1)."""
     import numpy as np
     import torch
+    import rtsas_amd
     from rtsas_amd import synthetic
-    from rtsas_amd.engine import DeviceBuffer
-    nk, base = 64, w.n_keys
-    wv = synthetic.Workload(**{**w.__dict__, "n_keys": nk, "zipf_lectures": 0, "zipf_days": 0})
-    pv = engine.gen_params(wv, seed=w.seed + 7919 * (rank + 1), slot_base=base)
+    from rtsas_amd.distributed import KeyMap, ShardedSketch, SwipeExchange, engine_k1
+    from rtsas_amd.engine import DeviceBatch, DeviceBuffer
+    names = [f"hll:unique:VERIFY{j:03d}:2025-10-03" for j in range(VERIFY_KEYS)]
+    vk = KeyMap(names, world, base=[km.slots_end(r) for r in range(world)])
+    engine.hll_reserve(vk.slots_end(rank))
+    client = rtsas_amd.SketchClient(context=engine.ctx)
+    vk.bind(client, rank)
+    wv = synthetic.Workload(**{**w.__dict__, "n_keys": VERIFY_KEYS, "zipf_lectures": 0, "zipf_days": 0})
+    pv = engine.gen_params(wv, seed=w.seed + 7919, slot_base=0)
     n = 1 << 19
     b = engine.swipe_batch(pv, 0, n)
-    out = DeviceBuffer(engine.ctx, n)
-    engine.swipes(0, b, out)
-    buf, offs, slot = b.to_host()
-    regs = np.zeros((nk, 16384), np.uint8)
-    want, _, _ = orc.process_swipes(chain, regs, (slot - base).astype(np.uint32), buf, offs)
-    ok_local = bool(np.array_equal(out.to_host(np.uint8, n), want)) and \
-        bool(np.array_equal(engine.registers_all(base + nk)[base:], regs))
-    b.free()
-    out.free()
-    slots = np.arange(base, base + nk, dtype=np.uint32)
-    # union of the 64 keys of every rank: device merge -> all_reduce MAX -> K2
-    t = torch.zeros((1, 16384), dtype=torch.uint8, device=dev)
-    go = np.array([0, nk], np.uint32)
-    torch.cuda.synchronize()
-    engine.ctx.call("ske_hll_merge_groups_dev", slots.ctypes.data_as(C.c_void_p),
-                    go.ctypes.data_as(C.c_void_p), 1, C.c_void_p(t.data_ptr()))
-    o = torch.from_numpy(regs.max(axis=0, keepdims=True)).to(dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(o, op=dist.ReduceOp.MAX)
-    torch.cuda.synchronize()
-    union = np.zeros(1, np.uint64)
-    engine.ctx.call("ske_hll_count_raw_dev", C.c_void_p(t.data_ptr()), 1,
-                    union.ctypes.data_as(C.c_void_p))
-    ok_union = bool(torch.equal(t, o)) and int(union[0]) == orc.hll_count_regs(o.cpu().numpy()[0])
-    # per-key unions across ranks: reduce_scatter MAX, each rank owns 64/world keys
-    per = -(-nk // world)
-    tk = torch.zeros((per * world, 16384), dtype=torch.uint8, device=dev)
-    gk = np.arange(nk + 1, dtype=np.uint32)
-    engine.ctx.call("ske_hll_merge_groups_dev", slots.ctypes.data_as(C.c_void_p),
-                    gk.ctypes.data_as(C.c_void_p), nk, C.c_void_p(tk.data_ptr()))
-    tk_o = torch.zeros_like(tk)
-    tk_o[:nk] = torch.from_numpy(regs).to(dev)
-    mine = torch.empty((per, 16384), dtype=torch.uint8, device=dev)
-    mine_o = torch.empty_like(mine)
-    if world > 1:
-        dist.reduce_scatter_tensor(mine, tk, op=dist.ReduceOp.MAX)
-        dist.reduce_scatter_tensor(mine_o, tk_o, op=dist.ReduceOp.MAX)
+    buf, offs, gkey = b.to_host()
+    width = int(offs[1] - offs[0])
+    regs_o = np.zeros((VERIFY_KEYS, 16384), np.uint8)
+    want, _, _ = orc.process_swipes(chain, regs_o, gkey.astype(np.uint32), buf, offs)
+    want = want.astype(np.uint8)
+    if exchange:
+        lo, hi = rank * n // world, (rank + 1) * n // world
+        ids = torch.as_tensor(buf[:n * width].reshape(n, width)[lo:hi].copy(), device=dev)
+        ex = SwipeExchange(rank, world, engine_k1(engine), vk, engine=engine)
+        got = ex.swipes(ids, torch.as_tensor(gkey[lo:hi].astype(np.int64), device=dev))
+        torch.cuda.synchronize()
+        ok_answers = bool(np.array_equal(got.cpu().numpy(), want[lo:hi]))
     else:
-        mine.copy_(tk)
-        mine_o.copy_(tk_o)
-    torch.cuda.synchronize()
-    ok_rollup = bool(torch.equal(mine, mine_o))
-    ok = torch.tensor([int(ok_local and ok_union and ok_rollup)], device=dev)
+        sel = np.nonzero(vk.owner[gkey] == rank)[0]
+        sb = np.ascontiguousarray(buf[:n * width].reshape(n, width)[sel]).reshape(-1)
+        so = np.arange(0, width * sel.size + 1, width, dtype=np.uint32)
+        mb = DeviceBatch.from_host(engine.ctx, sb, so, vk.local[gkey[sel]])
+        out = DeviceBuffer(engine.ctx, max(1, sel.size))
+        if sel.size:
+            engine.swipes(0, mb, out)
+        ok_answers = bool(np.array_equal(out.to_host(np.uint8, sel.size), want[sel]))
+        mb.free()
+        out.free()
+    b.free()
+    engine.sync()
+    mine = vk.keys_of(rank)
+    have = engine.registers_all(vk.slots_end(rank))
+    ok_regs = bool(np.array_equal(have[vk.local[mine]], regs_o[mine]))
+    sk = ShardedSketch(client, rank, world)
+    groups = [names[i::8] for i in range(8)] + [names, []]
+    union = sk.pfcount_union(names)
+    each = sk.pfcount_each(names)
+    roll = sk.rollup(groups)
+    ok_union = union == orc.hll_count_regs(regs_o.max(axis=0))
+    ok_each = each.tolist() == [orc.hll_count_regs(r) for r in regs_o]
+    ok_roll = roll.tolist() == [orc.hll_count_regs(regs_o[[names.index(k) for k in g]].max(axis=0))
+                                if g else 0 for g in groups]
+    ok = torch.tensor([int(ok_answers and ok_regs and ok_union and ok_each and ok_roll)],
+                      device=dev if dist.is_initialized() and dist.get_backend() == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-    return {"ok": bool(ok.item()), "swipes_per_rank": n, "keys_per_rank": nk,
-            "local_answers_and_registers": ok_local, "union_all_reduce_max": ok_union,
-            "rollup_reduce_scatter_max": ok_rollup, "union_pfcount": int(union[0]),
+    return {"ok": bool(ok.item()), "stream_swipes": n, "keys": VERIFY_KEYS, "keys_owned": int(mine.size),
+            "input": "SwipeExchange slice" if exchange else "owner-routed",
+            "answers": ok_answers, "owned_registers": ok_regs,
+            "sharded_pfcount_union": bool(ok_union), "sharded_pfcount_each": bool(ok_each),
+            "sharded_rollup": bool(ok_roll), "union_pfcount": int(union),
             "backend": dist.get_backend() if world > 1 else "none"}
 
 
@@ -299,6 +323,327 @@ def pass_bytes(n, nvalid, probes, width, fixed, geometry, lds_k1=False, slab_byt
     }
 
 
+def load_pmc(config, kernel):
+    """The newest committed rocprofv3 PMC summary of this workload's kernel."""
+    for r in PMC_ROUNDS:
+        path = os.path.join(ROOT, "profiles", f"{r}_pmc_{config}_{kernel}.json")
+        if os.path.exists(path):
+            with open(path) as f:
+                return json.load(f), os.path.relpath(path, ROOT)
+    return None, None
+
+
+class Run:
+    """One workload on one context: setup, timed steps, instrumented replay."""
+
+    def __init__(self, args, cfg, world, rank, local, dev, dist):
+        import torch
+        from rtsas_amd import synthetic
+        from rtsas_amd.distributed import KeyMap
+        from rtsas_amd.engine import DeviceBuffer, SketchEngine
+        self.args, self.cfg, self.world, self.rank, self.dist, self.dev = args, cfg, world, rank, dist, dev
+        self.torch = torch
+        w_all = synthetic.WORKLOADS[cfg]
+        self.w_all = w_all
+        # the job's key universe and its one ownership rule (distributed.KeyMap)
+        self.names = synthetic.key_names(w_all)
+        self.km = KeyMap(self.names, world)
+        mine = self.km.keys_of(rank)
+        probs = synthetic.key_probs(w_all)
+        if args.exchange:
+            # unpartitioned input: the stream spans every key (global indices);
+            # this rank's slab holds the keys it owns
+            w_gen = synthetic.Workload(**{**w_all.__dict__})
+            cdf = None
+        else:
+            # routed at ingest: this rank's stream is the global stream's
+            # share of the keys it owns, over their local slots
+            # (a uniform workload stays uniform over the owned keys: no table)
+            w_gen = synthetic.Workload(**{**w_all.__dict__, "n_keys": int(mine.size),
+                                          "zipf_lectures": 0, "zipf_days": 0})
+            cdf = synthetic.cdf_from_probs(probs[mine]) if probs is not None else None
+        self.w = w = synthetic.Workload(**{**w_all.__dict__, "n_keys": int(mine.size)})
+        self.n = n = args.batch or w.step_swipes
+        self.engine = engine = SketchEngine(local)
+        self.stream = stream = torch.cuda.Stream()  # shared by libsketch and torch
+        torch.cuda.set_stream(stream)
+        engine.set_stream(stream.cuda_stream)
+        for name, val in (("tile", args.tile), ("ablate", args.ablate), ("part_sub", args.part_sub)):
+            if val:
+                engine.set_option(name, val)
+        for name, val in (("variant", args.variant), ("hll_mode", args.hll_mode), ("pb_pairs", args.pb_pairs),
+                          ("pa_tile", args.pa_tile), ("pa_precheck", args.pa_precheck)):
+            if val >= 0:
+                engine.set_option(name, val)
+        for kv in args.opt:
+            name, _, val = kv.partition("=")
+            engine.set_option(name, int(val))
+        # Bloom preload (replicated on every rank) and this rank's HLL keys
+        engine.reserve(0, w.bf_error, w.bf_capacity)
+        self.p = p = engine.gen_params(w_gen, cdf=cdf)
+        t0 = time.perf_counter()
+        engine.preload(0, p, w.n_members)
+        self.preload_s = time.perf_counter() - t0
+        self.nslots = self.km.slots_end(rank)
+        engine.hll_reserve(self.nslots + VERIFY_KEYS)
+        self.variant = variant = engine.variant(0)
+        self.lds_k1 = lds_k1 = variant == 1
+        self.persistent = bool(args.persistent if args.persistent >= 0 else lds_k1) and not args.exchange
+        if lds_k1:
+            engine.set_option("k1_persistent", 1 if self.persistent else 0)
+        streams_n = 1 if self.persistent else (args.streams or (16 if lds_k1 else 1))
+        self.use_graph = 0 if self.persistent else (args.graph if args.graph >= 0 else (1 if lds_k1 else 0))
+        k1_grid = args.k1_grid
+        if k1_grid < 0:
+            cus = torch.cuda.get_device_properties(local).multi_processor_count
+            k1_grid = cus // 2 if (lds_k1 and streams_n > 1) else 0
+        if k1_grid:
+            engine.set_option("k1_grid", k1_grid)
+        self.nb = nb = max(1, min(args.max_batches, args.steps + args.warmup))
+        self.batches = [engine.swipe_batch(p, (rank * nb + j) * n, n) for j in range(nb)]
+        self.out = DeviceBuffer(engine.ctx, n)  # BF.EXISTS answers (the reference stores is_valid)
+        self.probes, self.nvalid = engine.swipes_stats(0, self.batches[0])
+        self.width = synthetic.id_width(w)
+        self.fixed = args.layout == "fixed"
+        self.streams = [stream] + [torch.cuda.Stream() for _ in range(max(0, streams_n - 1))]
+        self.ex, self.xviews = None, []
+        if args.exchange:
+            from rtsas_amd.distributed import SwipeExchange, engine_k1
+
+            def tview(ptr, shape, typestr):  # zero-copy torch view of a library buffer
+                class _V:
+                    __cuda_array_interface__ = {"shape": shape, "typestr": typestr, "data": (ptr, False),
+                                                "version": 3, "strides": None}
+                return torch.as_tensor(_V(), device=dev)
+            self.ex = SwipeExchange(rank, world, engine_k1(engine), self.km, engine=engine)
+            self.xviews = [(tview(b.bytes.ptr, (n, self.width), "|u1"), tview(b.slot.ptr, (n,), "<i4"))
+                           for b in self.batches]
+
+    # ---- steps
+    def step(self, j):
+        e = self.engine
+        if self.ex is not None:
+            self.ex.swipes(*self.xviews[j % self.nb])
+            return
+        if len(self.streams) > 1:
+            e.set_stream(self.streams[j % len(self.streams)].cuda_stream)
+        if self.fixed:
+            e.swipes_fixed_async(0, self.batches[j % self.nb], self.out)
+        else:
+            e.swipes_async(0, self.batches[j % self.nb], self.out)
+
+    def warm(self):
+        a, e = self.args, self.engine
+        if self.persistent:  # the same call shape as the timed region (loads the kernel)
+            e.swipes_many_async(0, [self.batches[j % self.nb] for j in range(max(1, a.warmup))],
+                                [self.out] * max(1, a.warmup), fixed=self.fixed)
+        else:
+            for j in range(a.warmup):
+                self.step(j)
+        e.set_stream(self.stream.cuda_stream)
+        self.torch.cuda.synchronize()
+        e.check_errors()
+
+    def enqueue_steps(self, graph):
+        a, e, torch = self.args, self.engine, self.torch
+        if graph is not None:
+            graph.launch()
+        elif self.persistent:
+            e.swipes_many_async(0, [self.batches[(a.warmup + j) % self.nb] for j in range(a.steps)],
+                                [self.out] * a.steps, fixed=self.fixed)
+        else:
+            for s_ in self.streams[1:]:
+                s_.wait_stream(self.stream)
+            for j in range(a.steps):
+                self.step(a.warmup + j)
+            e.set_stream(self.stream.cuda_stream)
+            for s_ in self.streams[1:]:
+                self.stream.wait_stream(s_)
+
+    def capture(self):
+        a, e = self.args, self.engine
+        if not self.use_graph:
+            return None
+        if len(self.streams) == 1:
+            return e.capture(lambda: [self.step(a.warmup + j) for j in range(a.steps)])
+        e.swipes_many_async(0, [], branches=len(self.streams))  # side streams, before capture
+        self.torch.cuda.synchronize()
+        return e.capture(lambda: e.swipes_many_async(
+            0, [self.batches[(a.warmup + j) % self.nb] for j in range(a.steps)],
+            [self.out] * a.steps, branches=len(self.streams), fixed=self.fixed))
+
+    def timed(self, barrier=True):
+        """Warm-up, then the K timed steps (no instrumentation)."""
+        a, torch, dist = self.args, self.torch, self.dist
+        self.warm()
+        graph = self.capture()
+        self.engine.set_option("pass_timing", 0)
+        if barrier and self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(self.stream)
+        self.enqueue_steps(graph)
+        e1.record(self.stream)
+        host_enqueue = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        if barrier and self.world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        self.engine.check_errors()  # an out-of-range slot in any timed step raises here
+        self.graph = graph
+        return elapsed, e0.elapsed_time(e1) / a.steps, host_enqueue
+
+    def replay_instrumented(self):
+        """The same warm-up + steps from a zeroed slab, every K1 kernel of the
+        K steps bracketed by HIP events on its own stream: per-kernel times
+        of the same work the timed region did.  A graph replays instead as a
+        whole (its launch time / steps)."""
+        a, e, torch = self.args, self.engine, self.torch
+        if self.graph is not None:
+            return None
+        self.zero_slab()
+        self.warm()
+        e.set_option("pass_timing", 1)
+        e.pass_times(reset=True)
+        self.enqueue_steps(None)
+        torch.cuda.synchronize()
+        e.set_option("pass_timing", 0)
+        e.check_errors()
+        return e.pass_times(reset=True)
+
+    def zero_slab(self):
+        p, nb = C.c_void_p(), C.c_uint64()
+        self.engine.ctx.call("ske_hll_slab", C.byref(p), C.byref(nb))
+        nbytes = self.nslots * 16384
+        assert nbytes <= nb.value
+
+        class _V:
+            __cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (p.value, False),
+                                        "version": 3, "strides": None}
+        self.torch.cuda.synchronize()
+        self.torch.as_tensor(_V(), device=self.dev).zero_()
+        self.torch.cuda.synchronize()
+
+    def roofline(self, pt, step_ms):
+        """§3's roofline on the kernel that takes the most time."""
+        a, n = self.args, self.n
+        cus = self.torch.cuda.get_device_properties(self.dev).multi_processor_count
+        alg = pass_bytes(n, self.nvalid, self.probes, self.width, self.fixed, chain_geometry(self.engine),
+                         lds_k1=self.lds_k1, slab_bytes=(self.nslots + VERIFY_KEYS) * 16384, cus=cus)
+        passes = {}
+        for i, (ms, cnt) in enumerate(pt or []):
+            if cnt:
+                mean = ms / cnt
+                name = PASS_NAMES[i]
+                # a persistent launch covers several steps and stages the filter once
+                ab = (alg[name] * (a.steps / cnt if (self.persistent and name == "k1") else 1)
+                      + (alg["k1_stage"] if name == "k1" else 0))
+                passes[name] = {"ms": mean, "launches": cnt, "alg_bytes": ab,
+                                "GBps": ab / (mean * 1e-3) / 1e9}
+        if passes:
+            dom = max(passes, key=lambda k: passes[k]["ms"])
+            kern_ms, dom_bytes = passes[dom]["ms"], passes[dom]["alg_bytes"]
+        else:  # graph replay: the launch time is the timed region's events / steps
+            dom, kern_ms, dom_bytes = "k1", step_ms, alg["k1"] + alg["k1_stage"]
+        achieved = dom_bytes / (kern_ms * 1e-3) / 1e9
+        # HBM-side bytes per launch of that kernel from the committed rocprofv3
+        # PMC passes of this workload (FETCH_SIZE + WRITE_SIZE, separate passes,
+        # FETCH corrected for 16-B-per-lane streams where the summary says so)
+        pmc, pmc_src = load_pmc(self.cfg, dom)
+        traffic = None
+        if pmc is not None:
+            traffic = pmc.get("hbm_bytes_corrected", pmc.get("hbm_bytes_per_dispatch"))
+            if traffic is not None and self.persistent and dom == "k1":
+                traffic *= a.steps / passes["k1"]["launches"] / pmc.get("steps_per_dispatch", a.steps)
+        r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": pmc_src,
+             "kernel": dom, "kernel_ms": kern_ms, "alg_bytes_per_launch": dom_bytes,
+             "kernel_times": "instrumented replay of the timed steps" if passes else "timed region events",
+             "device_ms_per_step": step_ms, "probes_per_swipe": self.probes / n,
+             "valid_frac": self.nvalid / n, "passes": passes}
+        if dom == "k_part_c":
+            sectors = self.nvalid / (kern_ms * 1e-3) / 1e9
+            r["random_sector_bound"] = {
+                "what": "one 64-B HBM sector per valid swipe's register, against the measured random "
+                        "4-B read rate over a 1.6 GB table (tools/randbench.hip)",
+                "achieved_Gsectors_per_s": sectors, "peak_Gsectors_per_s": RANDOM_SECTOR_GPS,
+                "frac": sectors / RANDOM_SECTOR_GPS}
+            if pmc and "TCC_EA0_ATOMIC_sum" in pmc.get("mean", {}):
+                req = (self.nvalid + pmc["mean"]["TCC_EA0_ATOMIC_sum"]) / (kern_ms * 1e-3) / 1e9
+                r["random_sector_bound"].update({
+                    "what": "random 64-B requests into the 1.6 GB register slab per second: one "
+                            "pre-check load per valid swipe plus one memory-side CAS per raise "
+                            "(TCC_EA0_ATOMIC_sum, PMC per dispatch), against the measured random 4-B "
+                            "read rate over a 1.6 GB table (tools/randbench.hip)",
+                    "achieved_Gsectors_per_s": req, "frac": req / RANDOM_SECTOR_GPS,
+                    "loads_only_frac": sectors / RANDOM_SECTOR_GPS})
+                cas = pmc["mean"]["TCC_EA0_ATOMIC_sum"] / (kern_ms * 1e-3) / 1e9
+                r["binding"] = {
+                    "counter": "TCC_EA0_ATOMIC_sum",
+                    "what": "register CASes (memory-side device atomics, PMC per dispatch) / this run's "
+                            "kernel time, against the measured rate of the same load + raising CAS "
+                            "over a 1.6 GB table (tools/casbench.hip, profiles/r02_casbench.json)",
+                    "atomics_per_dispatch": pmc["mean"]["TCC_EA0_ATOMIC_sum"],
+                    "achieved_G_per_s": cas, "peak_G_per_s": RANDOM_CAS_GPS, "frac": cas / RANDOM_CAS_GPS}
+        if dom == "k1" and pmc and "SQ_INSTS_VALU" in pmc.get("mean", {}):
+            m = pmc["mean"]
+            r["binding"] = {
+                "counter": "SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_VALU",
+                "what": "the LDS K1 is issue/latency bound, not HBM bound: per wave, the share of its "
+                        "cycles waiting in s_waitcnt and issuing VALU (PMC of this workload's dispatch)",
+                "wait_frac": m["SQ_WAIT_INST_ANY"] / m["SQ_WAVE_CYCLES"],
+                "valu_frac": m["SQ_ACTIVE_INST_VALU"] / m["SQ_WAVE_CYCLES"],
+                "valu_wave_insts_per_64_swipes":
+                    m["SQ_INSTS_VALU"] / max(1.0, pmc.get("swipes_per_dispatch", 0) / 64),
+                "lds_bank_conflict_rate": pmc.get("lds_bank_conflict_rate")}
+        return r
+
+    def config(self):
+        a, w = self.args, self.w
+        return {"workload": w.name, "swipes_per_step": self.n, "students": w.n_members,
+                "hll_keys_total": self.w_all.n_keys, "hll_keys_this_gpu": w.n_keys,
+                "key_ownership": "MurmurHash64A(key name, 0) mod world (distributed.KeyMap)",
+                "invalid_frac": w.invalid_frac,
+                "bloom": {"error": w.bf_error, "capacity": w.bf_capacity},
+                "id_bytes": self.width, "parallelism": f"dp{self.world} (key-sharded, Bloom replicated)",
+                "k1_variant": {0: "global-bloom", 1: "lds-bloom", 2: "xcd-regions",
+                               3: "partitioned"}[self.variant],
+                "layout": a.layout, "streams": len(self.streams),
+                "input": ("unpartitioned: alltoallv to the key owners per step"
+                          if a.exchange else "routed to the key owners at ingest"),
+                "launch": ("hip-graph" if self.graph is not None else
+                           ("persistent (one K1 launch per 48 steps)" if self.lds_k1 else
+                            "one many-batch call (pass C of a step beside passes A/B of the next)")
+                           if self.persistent else "host"),
+                "answers": "written (1 B per swipe)"}
+
+    def free(self):
+        if getattr(self, "graph", None) is not None:
+            self.graph.free()
+        for b in self.batches:
+            b.free()
+        self.out.free()
+
+
+def secondary(args, cfg, local, dev, dist):
+    """A second configuration on its own context in the same process (N = 1)."""
+    sargs = parse(["--config", cfg, "--steps", str(args.steps), "--warmup", str(args.warmup)])
+    r = Run(sargs, cfg, 1, 0, local, dev, dist)
+    elapsed, step_ms, _ = r.timed(barrier=False)
+    pt = r.replay_instrumented() if args.pass_replay else None
+    roof = r.roofline(pt, step_ms)
+    keep = {k: roof[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_source",
+                                 "kernel", "kernel_ms", "kernel_times", "binding") if k in roof}
+    out = {"metric": METRIC, "value": r.n * sargs.steps / elapsed, "unit": "swipes/s",
+           "steps": sargs.steps, "warmup": sargs.warmup, "ms_per_step": elapsed * 1e3 / sargs.steps,
+           "device_ms_per_step": step_ms, "config": r.config(), "roofline": keep}
+    r.free()
+    return out
+
+
 def main():
     args = parse()
     import numpy as np  # noqa: F401
@@ -308,7 +653,6 @@ def main():
     import __graft_entry__ as ge
     ge.load_package()
     from rtsas_amd import synthetic
-    from rtsas_amd.engine import DeviceBuffer, SketchEngine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -324,220 +668,22 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    w_all = synthetic.WORKLOADS[args.config]
-    w = synthetic.shard(w_all, world)
-    w_gen = w
-    if args.exchange:
-        # unpartitioned input: the stream spans every key; this rank's slab
-        # holds the keys it owns (slot s -> rank s % world, local slot s // world)
-        w_gen = synthetic.Workload(**{**w_all.__dict__, "step_swipes": w.step_swipes})
-        w = synthetic.Workload(**{**w.__dict__, "n_keys": -(-w_all.n_keys // world)})
-    n = args.batch or w.step_swipes
-    engine = SketchEngine(local)
-    stream = torch.cuda.Stream()  # a dedicated stream shared by libsketch and torch
-    torch.cuda.set_stream(stream)
-    engine.set_stream(stream.cuda_stream)
-    for name, val in (("tile", args.tile), ("ablate", args.ablate), ("part_sub", args.part_sub)):
-        if val:
-            engine.set_option(name, val)
-    if args.variant >= 0:
-        engine.set_option("variant", args.variant)
-    if args.hll_mode >= 0:
-        engine.set_option("hll_mode", args.hll_mode)
-    if args.pb_pairs >= 0:
-        engine.set_option("pb_pairs", args.pb_pairs)
-    if args.pa_tile >= 0:
-        engine.set_option("pa_tile", args.pa_tile)
-    if args.pa_precheck >= 0:
-        engine.set_option("pa_precheck", args.pa_precheck)
-    for kv in args.opt:
-        name, _, val = kv.partition("=")
-        engine.set_option(name, int(val))
-
-    # Bloom preload (replicated on every rank), this rank's HLL key shard, and
-    # 64 spare slots for the verification batch
-    engine.reserve(0, w.bf_error, w.bf_capacity)
-    p = engine.gen_params(w_gen)
-    t0 = time.perf_counter()
-    engine.preload(0, p, w.n_members)
-    preload_s = time.perf_counter() - t0
-    engine.hll_reserve(w.n_keys + 64)
-    variant = engine.variant(0)
-    lds_k1 = variant == 1
-    persistent = bool(args.persistent if args.persistent >= 0 else lds_k1) and not args.exchange
-    if lds_k1:
-        engine.set_option("k1_persistent", 1 if persistent else 0)
-    streams_n = 1 if persistent else (args.streams or (16 if lds_k1 else 1))
-    use_graph = 0 if persistent else (args.graph if args.graph >= 0 else (1 if lds_k1 else 0))
-    if args.k1_grid < 0:
-        cus = torch.cuda.get_device_properties(local).multi_processor_count
-        args.k1_grid = cus // 2 if (lds_k1 and streams_n > 1) else 0
-    if args.k1_grid:
-        engine.set_option("k1_grid", args.k1_grid)
-
-    nb = max(1, min(args.max_batches, args.steps + args.warmup))
-    batches = [engine.swipe_batch(p, (rank * nb + j) * n, n) for j in range(nb)]
-    out = DeviceBuffer(engine.ctx, n)  # BF.EXISTS answers (the reference stores is_valid)
-    probes, nvalid = engine.swipes_stats(0, batches[0])
-    width = synthetic.id_width(w)
-    fixed = args.layout == "fixed"
-    streams = [stream] + [torch.cuda.Stream() for _ in range(max(0, streams_n - 1))]
-
-    ex, xviews = None, []
-    if args.exchange:
-        from rtsas_amd.distributed import SwipeExchange, engine_k1
-
-        def tview(ptr, shape, typestr):  # zero-copy torch view of a library buffer
-            class _V:
-                __cuda_array_interface__ = {"shape": shape, "typestr": typestr, "data": (ptr, False),
-                                            "version": 3, "strides": None}
-            return torch.as_tensor(_V(), device=dev)
-        ex = SwipeExchange(rank, world, engine_k1(engine), engine=engine)
-        xviews = [(tview(b.bytes.ptr, (n, width), "|u1"), tview(b.slot.ptr, (n,), "<i4")) for b in batches]
-
-    def step(j):
-        if ex is not None:
-            ex.swipes(*xviews[j % nb])
-            return
-        if len(streams) > 1:
-            engine.set_stream(streams[j % len(streams)].cuda_stream)
-        if fixed:
-            engine.swipes_fixed_async(0, batches[j % nb], out)
-        else:
-            engine.swipes_async(0, batches[j % nb], out)
-
-    if persistent:  # the same call shape as the timed region (loads the kernel)
-        engine.swipes_many_async(0, [batches[j % nb] for j in range(max(1, args.warmup))],
-                                 [out] * max(1, args.warmup), fixed=fixed)
-    else:
-        for j in range(args.warmup):
-            step(j)
-    engine.set_stream(stream.cuda_stream)
-    torch.cuda.synchronize()
-    engine.check_errors()
-    graph = None
-    if use_graph and len(streams) == 1:
-        graph = engine.capture(lambda: [step(args.warmup + j) for j in range(args.steps)])
-    elif use_graph:
-        engine.swipes_many_async(0, [], branches=len(streams))  # side streams, before capture
-        torch.cuda.synchronize()
-        graph = engine.capture(lambda: engine.swipes_many_async(
-            0, [batches[(args.warmup + j) % nb] for j in range(args.steps)],
-            [out] * args.steps, branches=len(streams), fixed=fixed))
-    timing = bool(args.pass_timing) and graph is None
-    engine.set_option("pass_timing", 1 if timing else 0)
-    engine.pass_times(reset=True)
+    run = Run(args, args.config, world, rank, local, dev, dist)
+    elapsed, step_ms, host_enqueue = run.timed()
     if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record(stream)
-    if graph is not None:
-        graph.launch()
-    elif persistent:
-        engine.swipes_many_async(0, [batches[(args.warmup + j) % nb] for j in range(args.steps)],
-                                 [out] * args.steps, fixed=fixed)
-    else:
-        for s_ in streams[1:]:
-            s_.wait_stream(stream)
-        for j in range(args.steps):
-            step(args.warmup + j)
-        engine.set_stream(stream.cuda_stream)
-        for s_ in streams[1:]:
-            stream.wait_stream(s_)
-    e1.record(stream)
-    host_enqueue = time.perf_counter() - t0
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    engine.set_option("pass_timing", 0)
-    engine.check_errors()  # an out-of-range slot in any timed step raises here
-    step_ms = e0.elapsed_time(e1) / args.steps
-    pt = engine.pass_times(reset=True)
-    if world > 1:
-        t = torch.tensor([elapsed, step_ms] + [ms for ms, _ in pt], dtype=torch.float64,
+        t = torch.tensor([elapsed, step_ms], dtype=torch.float64,
                          device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, step_ms = float(t[0]), float(t[1])
-        pt = [(float(t[2 + i]), c) for i, (_, c) in enumerate(pt)]
+    pt = run.replay_instrumented() if args.pass_replay else None
+    if world > 1 and pt is not None:
+        t = torch.tensor([ms for ms, _ in pt], dtype=torch.float64,
+                         device=dev if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        pt = [(float(t[i]), c) for i, (_, c) in enumerate(pt)]
 
     ms_per_step = elapsed * 1e3 / args.steps
-    value = world * n * args.steps / elapsed
-    cus = torch.cuda.get_device_properties(local).multi_processor_count
-    alg = pass_bytes(n, nvalid, probes, width, fixed, chain_geometry(engine), lds_k1=lds_k1,
-                     slab_bytes=(w.n_keys + 64) * 16384, cus=cus)
-    passes = {}
-    for i, (ms, cnt) in enumerate(pt):
-        if cnt:
-            mean = ms / cnt
-            name = PASS_NAMES[i]
-            # a persistent launch covers several steps and stages the filter once
-            ab = (alg[name] * (args.steps / cnt if (persistent and name == "k1") else 1)
-                  + (alg["k1_stage"] if name == "k1" else 0))
-            passes[name] = {"ms": mean, "launches": cnt, "alg_bytes": ab,
-                            "GBps": ab / (mean * 1e-3) / 1e9}
-    if passes:
-        dom = max(passes, key=lambda k: passes[k]["ms"])
-        kern_ms, dom_bytes = passes[dom]["ms"], passes[dom]["alg_bytes"]
-    else:  # graph replay: the launch time is the replay's events / steps
-        dom, kern_ms, dom_bytes = "k1", step_ms, alg["k1"] + alg["k1_stage"]
-    achieved = dom_bytes / (kern_ms * 1e-3) / 1e9
-    # HBM-side bytes per launch of that kernel from the committed rocprofv3 PMC
-    # passes of this workload (FETCH_SIZE + WRITE_SIZE, separate passes), or null
-    traffic, traffic_src, pmc = None, None, None
-    pmc_path = os.path.join(ROOT, "profiles", f"r02_pmc_{args.config}_{dom}.json")
-    if os.path.exists(pmc_path):
-        with open(pmc_path) as f:
-            pmc = json.load(f)
-        traffic = pmc.get("hbm_bytes_per_dispatch")
-        if traffic is not None and persistent and dom == "k1":
-            traffic *= args.steps / passes["k1"]["launches"] / pmc.get("steps_per_dispatch", args.steps)
-        traffic_src = os.path.relpath(pmc_path, ROOT)
-    roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": dom, "kernel_ms": kern_ms, "alg_bytes_per_launch": dom_bytes,
-                "device_ms_per_step": step_ms, "probes_per_swipe": probes / n,
-                "valid_frac": nvalid / n, "passes": passes}
-    if dom == "k_part_c":
-        sectors = nvalid / (kern_ms * 1e-3) / 1e9
-        roofline["random_sector_bound"] = {
-            "what": "one 64-B HBM sector per valid swipe's register, against the measured random "
-                    "4-B read rate over a 1.6 GB table (tools/randbench.hip)",
-            "achieved_Gsectors_per_s": sectors, "peak_Gsectors_per_s": RANDOM_SECTOR_GPS,
-            "frac": sectors / RANDOM_SECTOR_GPS}
-        if pmc and "TCC_EA0_ATOMIC_sum" in pmc.get("mean", {}):
-            # every register touch is one random 64-B request: the valid swipes'
-            # pre-check loads plus the raising CASes (memory-side atomics, PMC)
-            req = (nvalid + pmc["mean"]["TCC_EA0_ATOMIC_sum"]) / (kern_ms * 1e-3) / 1e9
-            roofline["random_sector_bound"].update({
-                "what": "random 64-B requests into the 1.6 GB register slab per second: one "
-                        "pre-check load per valid swipe plus one memory-side CAS per raise "
-                        "(TCC_EA0_ATOMIC_sum, PMC per dispatch), against the measured random 4-B "
-                        "read rate over a 1.6 GB table (tools/randbench.hip)",
-                "achieved_Gsectors_per_s": req, "frac": req / RANDOM_SECTOR_GPS,
-                "loads_only_frac": sectors / RANDOM_SECTOR_GPS})
-            cas = pmc["mean"]["TCC_EA0_ATOMIC_sum"] / (kern_ms * 1e-3) / 1e9
-            roofline["binding"] = {
-                "counter": "TCC_EA0_ATOMIC_sum",
-                "what": "register CASes (memory-side device atomics, PMC per dispatch) / this run's "
-                        "kernel time, against the measured rate of the same load + raising CAS "
-                        "over a 1.6 GB table (tools/casbench.hip, profiles/r02_casbench.json)",
-                "atomics_per_dispatch": pmc["mean"]["TCC_EA0_ATOMIC_sum"],
-                "achieved_G_per_s": cas, "peak_G_per_s": RANDOM_CAS_GPS, "frac": cas / RANDOM_CAS_GPS}
-    if dom == "k1" and pmc and "SQ_INSTS_VALU" in pmc.get("mean", {}):
-        m = pmc["mean"]
-        roofline["binding"] = {
-            "counter": "SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_VALU",
-            "what": "the LDS K1 is issue/latency bound, not HBM bound: per wave, the share of its "
-                    "cycles waiting in s_waitcnt and issuing VALU (PMC of this workload's dispatch)",
-            "wait_frac": m["SQ_WAIT_INST_ANY"] / m["SQ_WAVE_CYCLES"],
-            "valu_frac": m["SQ_ACTIVE_INST_VALU"] / m["SQ_WAVE_CYCLES"],
-            "valu_wave_insts_per_64_swipes":
-                m["SQ_INSTS_VALU"] / max(1.0, pmc.get("swipes_per_dispatch", 0) / 64),
-            "lds_bank_conflict_rate": pmc.get("lds_bank_conflict_rate")}
+    value = world * run.n * args.steps / elapsed
     line = {
         "metric": METRIC,
         "value": value,
@@ -550,41 +696,30 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u64",
-        "data": "synthetic (device counter-based generator, seed %d)" % w.seed,
-        "config": {"workload": w.name, "swipes_per_step": n, "students": w.n_members,
-                   "hll_keys_total": w_all.n_keys, "hll_keys_per_gpu": w.n_keys,
-                   "invalid_frac": w.invalid_frac,
-                   "bloom": {"error": w.bf_error, "capacity": w.bf_capacity},
-                   "id_bytes": width, "parallelism": f"dp{world} (key-sharded, Bloom replicated)",
-                   "k1_variant": {0: "global-bloom", 1: "lds-bloom", 2: "xcd-regions",
-                                  3: "partitioned"}[variant],
-                   "layout": args.layout, "streams": len(streams),
-                   "input": ("unpartitioned: alltoallv to the key owners per step"
-                             if args.exchange else "routed to the key owners at ingest"),
-                   "launch": ("hip-graph" if graph is not None else
-                              ("persistent (one K1 launch per 48 steps)" if lds_k1 else
-                               "one many-batch call (pass C of a step beside passes A/B of the next)")
-                              if persistent else "host"),
-                   "answers": "written (1 B per swipe)"},
-        "roofline": roofline,
-        "preload_s": preload_s,
+        "data": "synthetic (device counter-based generator, seed %d)" % run.w.seed,
+        "config": run.config(),
+        "roofline": run.roofline(pt, step_ms),
+        "preload_s": run.preload_s,
         "host_enqueue_us_per_step": host_enqueue * 1e6 / args.steps,
     }
     want_cpu = rank == 0 and world == 1 and not args.no_cpu and args.cpu_seconds > 0
     if not args.no_check or want_cpu:
         orc = ge.load_oracle()
-        chain = oracle_chain(engine, orc, w, p)
+        chain = oracle_chain(run.engine, orc, run.w, run.p)
         if not args.no_check:
-            line["check"] = verify(engine, orc, chain, w, rank, world, dist, dev)
+            line["check"] = verify(run.engine, orc, chain, run.w, run.km, rank, world, dist, dev,
+                                   bool(args.exchange))
         if want_cpu:
-            line["cpu_baseline"] = cpu_baseline(orc, chain, w, batches[0], args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(orc, chain, run.w, run.batches[0], args.cpu_seconds,
+                                                lambda s: run.names[int(run.km.keys_of(0)[s])])
+    run.free()
+    sec = args.secondary
+    if sec == "auto":
+        sec = "c2" if args.config == "c3" else "none"
+    if world == 1 and sec != "none" and sec != args.config:
+        line["secondary"] = secondary(args, sec, local, dev, dist)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if graph is not None:
-        graph.free()
-    for b in batches:
-        b.free()
-    out.free()
     if world > 1:
         dist.destroy_process_group()
 

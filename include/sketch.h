@@ -105,9 +105,14 @@ int ske_close(ske_ctx *ctx);
 const char *ske_strerror(int code);
 const char *ske_last_hip_error(ske_ctx *ctx);
 int ske_set_stream(ske_ctx *ctx, void *hip_stream); /* NULL = the context's own stream */
+int ske_get_stream(ske_ctx *ctx, void **hip_stream); /* the stream calls enqueue on now */
 /* Wait for the context stream.  Also reports (and clears) the sticky device
  * error word that enqueue-only calls leave set: SKE_ERANGE when a valid swipe
- * named an HLL slot outside the slab since the last check. */
+ * named an HLL slot outside the slab since the last check.  The word is read
+ * and cleared by device-side atomic exchanges (no flag set concurrently on
+ * another stream is lost).  A synchronous K1 / PFADD / ingest call reports
+ * only its OWN out-of-range slots; what earlier enqueue-only calls left is
+ * kept for the next ske_sync / ske_check_errors. */
 int ske_sync(ske_ctx *ctx);
 int ske_check_errors(ske_ctx *ctx);  /* the same check: sync + report + clear */
 int ske_device_alloc(ske_ctx *ctx, uint64_t bytes, void **out); /* device scratch for callers */
@@ -205,13 +210,17 @@ int ske_swipes_fixed_async(ske_ctx *ctx, uint32_t fid, const uint32_t *slot,
  * alltoallv per batch; distributed.SwipeExchange; no reference counterpart --
  * the reference's Shared subscription hands any event to any consumer,
  * attendance_processor.py:30-34).  Device pointers.  Swipe i (fixed-width id,
- * GLOBAL key slot s) goes to rank s % world as local slot s / world:
- * send_ids / send_slots are filled owner by owner (the alltoallv input),
- * pos[i] = the swipe's position there, counts[o] (host) = swipes for owner o
- * (the split sizes; the call synchronizes the context stream for them).
- * world <= 64, n < 2^32. */
-int ske_route_swipes(ske_ctx *ctx, const uint8_t *ids, uint32_t width, const uint32_t *slot, uint64_t n,
-                     uint32_t world, uint8_t *send_ids, uint32_t *send_slots, uint32_t *pos, uint64_t *counts);
+ * GLOBAL key index g into the job's key universe) goes to rank key_owner[g]
+ * as local slot key_local[g] -- the key map every multi-GPU path shares
+ * (distributed.KeyMap: owner = MurmurHash64A(key name, 0) mod world).  An
+ * index g >= nkeys goes to rank 0 with local slot 0xffffffff (K1 answers it
+ * and reports SKE_ERANGE for its PFADD).  send_ids / send_slots are filled
+ * owner by owner (the alltoallv input), pos[i] = the swipe's position there,
+ * counts[o] (host) = swipes for owner o (the split sizes; the call
+ * synchronizes the context stream for them).  world <= 64, n < 2^32. */
+int ske_route_swipes(ske_ctx *ctx, const uint8_t *ids, uint32_t width, const uint32_t *gkey, uint64_t n,
+                     uint32_t world, const uint32_t *key_owner, const uint32_t *key_local, uint32_t nkeys,
+                     uint8_t *send_ids, uint32_t *send_slots, uint32_t *pos, uint64_t *counts);
 /* out[i] = answers[pos[i]]: the owners' BF.EXISTS answers, received back in
  * send order, into input order (enqueue only). */
 int ske_route_return_async(ske_ctx *ctx, const uint8_t *answers, const uint32_t *pos, uint64_t n,
@@ -244,7 +253,11 @@ int ske_swipes_many_async(ske_ctx *ctx, uint32_t fid, const ske_swipe_batch *bat
  * and valid count, to price the algorithmic bytes of the roofline. */
 int ske_swipes_stats(ske_ctx *ctx, uint32_t fid, const uint8_t *bytes, const uint32_t *offs,
                      uint64_t n, uint64_t *probes, uint64_t *nvalid);
-/* which K1 variant the current chain selects: 1 = LDS-staged Bloom, 0 = global */
+/* which K1 variant the current chain and options select:
+ *   0 = generic LDS / global-memory K1 (sketch_kernels.hip),
+ *   1 = short-id LDS K1, the chain staged in LDS (sketch_k1.hip; C1/C2/C4),
+ *   2 = XCD-partitioned K1 (sketch_xr.hip),
+ *   3 = partitioned K1, passes A/B/C over LDS slices (sketch_part.hip; C3/C5) */
 int ske_swipes_variant(ske_ctx *ctx, uint32_t fid);
 int ske_set_option(ske_ctx *ctx, const char *name, int64_t value);
 /* Kernel timing for the benchmark's roofline: with option "pass_timing" = 1

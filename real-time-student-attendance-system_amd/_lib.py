@@ -80,6 +80,7 @@ SIGNATURES = {
     "ske_strerror": (C.c_char_p, [C.c_int]),
     "ske_last_hip_error": (C.c_char_p, [_CTX]),
     "ske_set_stream": (C.c_int, [_CTX, _vp]),
+    "ske_get_stream": (C.c_int, [_CTX, C.POINTER(_vp)]),
     "ske_sync": (C.c_int, [_CTX]),
     "ske_check_errors": (C.c_int, [_CTX]),
     "ske_device_alloc": (C.c_int, [_CTX, C.c_uint64, C.POINTER(C.c_void_p)]),
@@ -119,8 +120,8 @@ SIGNATURES = {
     "ske_swipes_fixed_async": (C.c_int, [_CTX, C.c_uint32, _u32p, _u8p, C.c_uint32, C.c_uint64,
                                          _u8p]),
     "ske_swipes_many_async": (C.c_int, [_CTX, C.c_uint32, _vp, C.c_uint32, C.c_uint32]),
-    "ske_route_swipes": (C.c_int, [_CTX, _u8p, C.c_uint32, _u32p, C.c_uint64, C.c_uint32, _u8p, _u32p,
-                                   _u32p, _u64p]),
+    "ske_route_swipes": (C.c_int, [_CTX, _u8p, C.c_uint32, _u32p, C.c_uint64, C.c_uint32, _u32p, _u32p,
+                                   C.c_uint32, _u8p, _u32p, _u32p, _u64p]),
     "ske_route_return_async": (C.c_int, [_CTX, _u8p, _u32p, C.c_uint64, _u8p]),
     "ske_swipes_stats": (C.c_int, [_CTX, C.c_uint32, _u8p, _u32p, C.c_uint64,
                                    C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),

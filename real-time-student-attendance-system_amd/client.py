@@ -68,6 +68,7 @@ class KeySpace:
         self._free_fids = list(range(_lib.SKE_MAX_FILTERS - 1, -1, -1))
         self._free_slots: list[int] = []
         self._next_slot = 0
+        self._slot_key: dict[int, bytes] = {}
         self.slots_released = 0  # bumps whenever an HLL slot is freed (ingest key table)
 
     def type_of(self, key: bytes) -> str | None:
@@ -101,7 +102,33 @@ class KeySpace:
                 self.ctx.call("ske_hll_reserve", s + 1)
         self.kind[key] = "hll"
         self.slot[key] = s
+        self._slot_key[s] = key
         return s
+
+    def bind(self, key: bytes, slot: int) -> None:
+        """Name an HLL key at a given slab slot without touching its registers:
+        a multi-GPU job's key map (distributed.KeyMap.bind) fixes the local
+        slot of every key its rank owns, and K1 writes those slots directly."""
+        slot = int(slot)
+        if self.kind.get(key, "hll") != "hll":
+            raise ResponseError(WRONGTYPE)
+        have = self.slot.get(key)
+        if have is not None:
+            if have != slot:
+                raise ResponseError(f"ERR key already bound to slot {have}")
+            return
+        if slot in self._slot_key:
+            raise ResponseError(f"ERR slot {slot} already holds another key")
+        if slot >= self.ctx.lib.ske_hll_capacity(self.ctx.ptr):
+            self.ctx.call("ske_hll_reserve", slot + 1)
+        if slot >= self._next_slot:
+            self._free_slots.extend(range(slot - 1, self._next_slot - 1, -1))
+            self._next_slot = slot + 1
+        else:
+            self._free_slots.remove(slot)
+        self.kind[key] = "hll"
+        self.slot[key] = slot
+        self._slot_key[slot] = key
 
     def drop(self, key: bytes) -> bool:
         k = self.kind.pop(key, None)
@@ -111,6 +138,7 @@ class KeySpace:
             self._free_fids.append(f)
         elif k == "hll":
             s = self.slot.pop(key)
+            self._slot_key.pop(s, None)
             self.ctx.call("ske_hll_clear", s)  # a reused slot starts empty
             self._free_slots.append(s)
             self.slots_released += 1
@@ -120,6 +148,7 @@ class KeySpace:
         """Undo new_slot() for a key that no command ended up creating (its
         registers were never written)."""
         s = self.slot.pop(key)
+        self._slot_key.pop(s, None)
         del self.kind[key]
         self._free_slots.append(s)
         self.slots_released += 1

@@ -73,7 +73,8 @@ struct ske_ctx {
     void *stg[8] = {};
     size_t stg_cap[8] = {};
     HostStager *hs = nullptr;  // pinned double buffer + copy threads for pageable inputs (lazy)
-    unsigned int *err = nullptr;
+    unsigned int *err = nullptr;  // [0] sticky slot-error word; see check_call_err
+    bool err_pending = false;     // taken from the device, not yet reported by ske_sync
     unsigned long long *stats = nullptr;
     int pb = 2;           // K1 tile: swipes per thread in flight (1, 2, 4, 8)
     int variant = -1;     // -1 auto, 0 global, 1 LDS
@@ -467,19 +468,60 @@ int ensure_tables(ske_ctx *c) {
     return SKE_OK;
 }
 
-// The device error word is sticky: kernels only ever set it (a valid swipe
-// naming a slot outside the slab).  Enqueue-only calls leave it set; the next
-// synchronous call that checks it -- a synchronous K1 / PFADD, ske_sync,
-// ske_check_errors -- reports it and clears it.
-int check_err_flag(ske_ctx *c, int code_if_set) {
-    unsigned int h = 0;
-    HIPCHK(c, hipMemcpyAsync(&h, c->err, 4, hipMemcpyDeviceToHost, c->st));
+// The device error word err[0] is sticky: kernels only ever set it (a valid
+// swipe naming a slot outside the slab).  It is read and cleared only by
+// device-side exchanges (atomicExch), so a flag set by a kernel on any stream
+// is never lost between a read and a clear:
+//   * a synchronous call (K1, PFADD, ingest) first takes what earlier
+//     enqueue-only calls left into err[kErrPrior] (k_err_begin, OR-ed), and at
+//     its end takes its own flag into the report word (k_err_end); the prior
+//     flag is then held on the host (c->err_pending) for the next ske_sync /
+//     ske_check_errors -- a synchronous call reports only its own slots;
+//   * ske_sync / ske_check_errors report everything not yet reported.
+constexpr int kErrPrior = 16, kErrOut = 32;  // word offsets in c->err (64 words)
+
+__global__ void k_err_begin(unsigned int *err) {
+    const unsigned int v = atomicExch(err, 0u);
+    if (v) atomicOr(err + kErrPrior, v);
+}
+// out[0] = the prior word (then cleared), out[1] = the live word (then cleared)
+__global__ void k_err_end(unsigned int *err) {
+    err[kErrOut] = atomicExch(err + kErrPrior, 0u);
+    err[kErrOut + 1] = atomicExch(err, 0u);
+}
+
+int err_begin(ske_ctx *c) {
+    hipLaunchKernelGGL(k_err_begin, dim3(1), dim3(1), 0, c->st, c->err);
+    HIPCHK(c, hipGetLastError());
+    return SKE_OK;
+}
+
+// the two words after this call's work: {earlier enqueue-only calls, this call}
+int err_end(ske_ctx *c, unsigned int h[2]) {
+    hipLaunchKernelGGL(k_err_end, dim3(1), dim3(1), 0, c->st, c->err);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(h, c->err + kErrOut, 8, hipMemcpyDeviceToHost, c->st));
     HIPCHK(c, hipStreamSynchronize(c->st));
-    if (h) {
-        HIPCHK(c, hipMemsetAsync(c->err, 0, 4, c->st));
-        HIPCHK(c, hipStreamSynchronize(c->st));
-    }
-    return h ? code_if_set : SKE_OK;
+    return SKE_OK;
+}
+
+// end of a synchronous call that did err_begin(): its own slot errors only
+int check_call_err(ske_ctx *c) {
+    unsigned int h[2] = {0, 0};
+    const int rc = err_end(c, h);
+    if (rc) return rc;
+    if (h[0]) c->err_pending = true;
+    return h[1] ? SKE_ERANGE : SKE_OK;
+}
+
+// ske_sync / ske_check_errors: everything not yet reported
+int check_err_flag(ske_ctx *c, int code_if_set) {
+    unsigned int h[2] = {0, 0};
+    const int rc = err_end(c, h);
+    if (rc) return rc;
+    const bool set = h[0] || h[1] || c->err_pending;
+    c->err_pending = false;
+    return set ? code_if_set : SKE_OK;
 }
 
 // The short-id LDS kernel (sketch_k1.hip) when the chain, the batch and the
@@ -644,8 +686,8 @@ int ske_open(int device, ske_ctx **out) {
     c->st = c->own;
     c->filters.resize(SKE_MAX_FILTERS);
     c->scratch = scratch_new();
-    if (hipMalloc(&c->err, 64) != hipSuccess || hipMalloc(&c->stats, 64) != hipSuccess ||
-        hipMemset(c->err, 0, 64) != hipSuccess) {
+    if (hipMalloc(&c->err, 256) != hipSuccess || hipMalloc(&c->stats, 64) != hipSuccess ||
+        hipMemset(c->err, 0, 256) != hipSuccess) {
         ske_close(c);
         return SKE_ENOMEM;
     }
@@ -705,6 +747,12 @@ int ske_set_stream(ske_ctx *c, void *stream) {
         if (rc) return rc;
     }
     c->st = next;
+    return SKE_OK;
+}
+
+int ske_get_stream(ske_ctx *c, void **stream) {
+    if (!c || !stream) return SKE_EINVAL;
+    *stream = c->st == c->own ? nullptr : (void *)c->st;
     return SKE_OK;
 }
 
@@ -1176,6 +1224,7 @@ int ske_hll_pfadd(ske_ctx *c, const uint32_t *slot, const uint8_t *bytes, const 
                   uint64_t n, uint8_t *changed, int mem) {
     if (!c || !slot) return SKE_EINVAL;
     if (n == 0) return SKE_OK;
+    if (const int erc = err_begin(c)) return erc;  // earlier enqueue-only calls' slot errors
     if (n >= 0xffffffffull) return SKE_EINVAL;
     Staged s;
     int rc = stage_items(c, bytes, offs, n, mem, &s);
@@ -1197,7 +1246,7 @@ int ske_hll_pfadd(ske_ctx *c, const uint32_t *slot, const uint8_t *bytes, const 
         HIPCHK(c, launch_pfadd(dslot, s.bytes, s.offs, n, c->regs, c->nslots, c->err, c->cus,
                                c->st));
     }
-    return check_err_flag(c, SKE_ERANGE);
+    return check_call_err(c);
 }
 
 int ske_swipes(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *bytes,
@@ -1206,6 +1255,7 @@ int ske_swipes(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *by
     Filter *F = get_filter(c, fid);
     if (!F) return SKE_EINVAL;
     if (n == 0) return SKE_OK;
+    if (const int erc = err_begin(c)) return erc;  // earlier enqueue-only calls' slot errors
     Staged s;
     int rc = stage_items(c, bytes, offs, n, mem, &s);
     if (rc) return rc;
@@ -1222,7 +1272,7 @@ int ske_swipes(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *by
     if (rc) return rc;
     if (out_valid && mem != SKE_MEM_DEVICE)
         HIPCHK(c, hipMemcpyAsync(out_valid, dout, n, hipMemcpyDeviceToHost, c->st));
-    return check_err_flag(c, SKE_ERANGE);
+    return check_call_err(c);
 }
 
 int ske_swipes_async(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *bytes,
@@ -1360,16 +1410,19 @@ int ske_swipes_many_async(ske_ctx *c, uint32_t fid, const ske_swipe_batch *b, ui
     return rc;
 }
 
-int ske_route_swipes(ske_ctx *c, const uint8_t *ids, uint32_t width, const uint32_t *slot, uint64_t n,
-                     uint32_t world, uint8_t *send_ids, uint32_t *send_slots, uint32_t *pos, uint64_t *counts) {
+int ske_route_swipes(ske_ctx *c, const uint8_t *ids, uint32_t width, const uint32_t *gkey, uint64_t n,
+                     uint32_t world, const uint32_t *key_owner, const uint32_t *key_local, uint32_t nkeys,
+                     uint8_t *send_ids, uint32_t *send_slots, uint32_t *pos, uint64_t *counts) {
     if (!c || !counts || world == 0 || world > 64 || width == 0 || width > 4096 || n >= (uint64_t(1) << 32))
         return SKE_EINVAL;
-    if (n && (!ids || !slot || !send_ids || !send_slots || !pos)) return SKE_EINVAL;
+    if (n && (!ids || !gkey || !send_ids || !send_slots || !pos)) return SKE_EINVAL;
+    if (nkeys && (!key_owner || !key_local)) return SKE_EINVAL;
     hipError_t e = hipSuccess;
     uint32_t *hist = (uint32_t *)scratch_get(c->scratch, 40, route_hist_words(n, world) * 4 + 4, &e);
     uint32_t *tot = e == hipSuccess ? (uint32_t *)scratch_get(c->scratch, 41, size_t(world) * 4, &e) : nullptr;
     if (e != hipSuccess) return scratch_error(c, e);
-    HIPCHK(c, launch_route(ids, width, slot, n, world, send_ids, send_slots, pos, hist, tot, c->st));
+    HIPCHK(c, launch_route(ids, width, gkey, n, world, key_owner, key_local, nkeys, send_ids, send_slots, pos,
+                           hist, tot, c->st));
     uint32_t h[64];
     HIPCHK(c, hipMemcpyAsync(h, tot, size_t(world) * 4, hipMemcpyDeviceToHost, c->st));
     HIPCHK(c, hipStreamSynchronize(c->st));
@@ -1399,6 +1452,7 @@ int ske_swipes_fixed(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8
     Filter *F = get_filter(c, fid);
     if (!F) return SKE_EINVAL;
     if (n == 0) return SKE_OK;
+    if (const int erc = err_begin(c)) return erc;  // earlier enqueue-only calls' slot errors
     int rc = SKE_OK;
     const uint8_t *db = bytes;
     const uint32_t *dslot = slot;
@@ -1419,7 +1473,7 @@ int ske_swipes_fixed(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8
     if (rc) return rc;
     if (out_valid && mem != SKE_MEM_DEVICE)
         HIPCHK(c, hipMemcpyAsync(out_valid, dout, n, hipMemcpyDeviceToHost, c->st));
-    return check_err_flag(c, SKE_ERANGE);
+    return check_call_err(c);
 }
 
 #ifdef SKE_STAMPS
@@ -1775,6 +1829,7 @@ int ske_ingest_swipes(ske_ctx *c, uint32_t fid, const uint8_t *msgs, const ske_i
     if (!F) return SKE_EINVAL;
     if (ntaken) *ntaken = 0;
     if (!n) return SKE_OK;
+    if (const int erc = err_begin(c)) return erc;  // earlier enqueue-only calls' slot errors
     if (n >= (uint64_t(1) << 31)) return SKE_EINVAL;
     hipError_t e = hipSuccess;
     uint32_t *slot = (uint32_t *)scratch_get(c->scratch, 21, n * 4, &e);
@@ -1812,7 +1867,7 @@ int ske_ingest_swipes(ske_ctx *c, uint32_t fid, const uint8_t *msgs, const ske_i
     }
     HIPCHK(c, launch_ingest_unpack(k, slot, flag_incl, kvalid, n, valid_dev, c->cus, c->st));
     if (ntaken) *ntaken = taken;
-    return check_err_flag(c, SKE_ERANGE);
+    return check_call_err(c);
 }
 
 // ------------------------------------------------------------------ graphs

@@ -81,8 +81,8 @@ hipError_t launch_swipes_lds_many(const K1Args &A, const K1Many &M, int tile, in
 
 // sketch_route.hip -- unpartitioned swipes to their key owners (alltoallv halves)
 hipError_t launch_route(const uint8_t *ids, uint32_t width, const uint32_t *slot, uint64_t n, uint32_t world,
-                        uint8_t *sids, uint32_t *sslot, uint32_t *pos, uint32_t *hist, uint32_t *tot,
-                        hipStream_t st);
+                        const uint32_t *kown, const uint32_t *kloc, uint32_t nkeys, uint8_t *sids,
+                        uint32_t *sslot, uint32_t *pos, uint32_t *hist, uint32_t *tot, hipStream_t st);
 uint64_t route_hist_words(uint64_t n, uint32_t world);
 hipError_t launch_route_return(const uint8_t *ans, const uint32_t *pos, uint64_t n, uint8_t *out, int cus,
                                hipStream_t st);

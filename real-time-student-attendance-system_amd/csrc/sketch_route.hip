@@ -2,8 +2,12 @@
 // ("if input is not pre-partitioned, use one alltoallv per
 // batch"), the device half of distributed.SwipeExchange.
 //
-// Key slot s is owned by rank s % world as its local slot s / world.  A batch
-// of fixed-width ids and global slots is counting-sorted by owner into send
+// Global key g (an index into the job's key universe) is owned by rank
+// key_owner[g] as its local slot key_local[g] -- distributed.KeyMap's table,
+// owner = MurmurHash64A(key name, 0) mod world, shared with ingest routing and
+// the cross-shard queries; an index past the table goes to rank 0 with slot
+// kNoSlot (K1 answers it and reports the slot).  A batch of fixed-width ids
+// and global key indices is counting-sorted by owner into send
 // buffers laid out owner by owner (the alltoallv input), remembering every
 // swipe's position; after K1 on the owners and the reverse alltoallv, the
 // answers are gathered back into input order through those positions.
@@ -30,17 +34,30 @@ constexpr uint32_t kRtItems = 16;
 constexpr uint32_t kRtTile = kRtBlock * kRtItems;  // swipes per block
 constexpr uint32_t kRtMaxWorld = 64;
 
+constexpr uint32_t kNoSlot = 0xffffffffu;
+
 struct RouteArgs {
     const uint8_t *ids;    // n x width
-    const uint32_t *slot;  // global key slots
+    const uint32_t *slot;  // global key indices
+    const uint32_t *kown;  // [nkeys] owner rank of each global key
+    const uint32_t *kloc;  // [nkeys] local slot of each global key on its owner
     uint8_t *sids;         // n x width, owner major
     uint32_t *sslot;       // local slots, owner major
     uint32_t *pos;         // input swipe -> position in the send buffers
     uint32_t *hist;        // [world][nblocks] counts, then bases
     uint32_t *tot;         // [world] swipes per owner
     uint64_t n;
-    uint32_t width, world, nblocks;
+    uint32_t width, world, nblocks, nkeys;
 };
+
+// (a table entry naming no rank of this world is treated as a missing key:
+// rank 0, kNoSlot -- never an LDS index past the histogram)
+__device__ __forceinline__ bool route_known(const RouteArgs &R, uint32_t g) {
+    return g < R.nkeys && R.kown[g] < R.world;
+}
+__device__ __forceinline__ uint32_t route_owner(const RouteArgs &R, uint32_t g) {
+    return route_known(R, g) ? R.kown[g] : 0u;
+}
 
 __global__ void __launch_bounds__(kRtBlock) k_route_count(const RouteArgs R) {
     __shared__ uint32_t c[kRtMaxWorld];
@@ -51,7 +68,7 @@ __global__ void __launch_bounds__(kRtBlock) k_route_count(const RouteArgs R) {
 #pragma unroll
     for (uint32_t j = 0; j < kRtItems; j++) {
         const uint64_t i = b0 + j * kRtBlock + tid;
-        if (i < R.n) atomicAdd(&c[R.slot[i] % R.world], 1u);
+        if (i < R.n) atomicAdd(&c[route_owner(R, R.slot[i])], 1u);
     }
     __syncthreads();
     if (tid < R.world) R.hist[size_t(tid) * R.nblocks + blockIdx.x] = c[tid];
@@ -104,11 +121,11 @@ __global__ void __launch_bounds__(kRtBlock) k_route_scatter(const RouteArgs R) {
     for (uint32_t j = 0; j < kRtItems; j++) {
         const uint64_t i = b0 + j * kRtBlock + tid;
         if (i >= R.n) continue;
-        const uint32_t s = R.slot[i];
-        const uint32_t o = s % R.world;
+        const uint32_t g = R.slot[i];
+        const uint32_t o = route_owner(R, g);
         const uint32_t p = base[o] + atomicAdd(&c[o], 1u);
         R.pos[i] = p;
-        R.sslot[p] = s / R.world;
+        R.sslot[p] = route_known(R, g) ? R.kloc[g] : kNoSlot;
         const uint8_t *src = R.ids + i * R.width;
         uint8_t *dst = R.sids + uint64_t(p) * R.width;
         if (R.width == 8) {
@@ -126,11 +143,11 @@ __global__ void __launch_bounds__(256) k_route_return(const uint8_t *ans, const 
 }
 
 hipError_t launch_route(const uint8_t *ids, uint32_t width, const uint32_t *slot, uint64_t n, uint32_t world,
-                        uint8_t *sids, uint32_t *sslot, uint32_t *pos, uint32_t *hist, uint32_t *tot,
-                        hipStream_t st) {
+                        const uint32_t *kown, const uint32_t *kloc, uint32_t nkeys, uint8_t *sids,
+                        uint32_t *sslot, uint32_t *pos, uint32_t *hist, uint32_t *tot, hipStream_t st) {
     if (world == 0 || world > kRtMaxWorld || width == 0 || n >= (uint64_t(1) << 32)) return hipErrorInvalidValue;
-    RouteArgs R{ids, slot, sids, sslot, pos, hist, tot, n, width, world,
-                uint32_t((n + kRtTile - 1) / kRtTile)};
+    RouteArgs R{ids, slot, kown, kloc, sids, sslot, pos, hist, tot, n, width, world,
+                uint32_t((n + kRtTile - 1) / kRtTile), nkeys};
     if (n == 0) return hipMemsetAsync(tot, 0, size_t(world) * 4, st);
     hipLaunchKernelGGL(k_route_count, dim3(R.nblocks), dim3(kRtBlock), 0, st, R);
     hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(1024), 0, st, R);

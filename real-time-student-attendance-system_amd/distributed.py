@@ -2,16 +2,31 @@
 
 The reference scales by running N processor processes on a Pulsar Shared
 subscription (attendance_processor.py:30-34) against ONE Redis that
-serialises every BF / PF op.  Here every GPU holds:
+serialises every BF / PF op, so every process sees every key
+(:127-129 writes it, :152 reads it).  Here every GPU holds:
 
   * a replica of the Bloom chain (read-only on the hot path; preload is
     replayed on every rank -- BF.MADD is deterministic);
-  * the HLL keys it owns: ``owner(key) = MurmurHash64A(key, 0) mod world``.
+  * the HLL keys it owns.
 
-Swipes are routed to their key's owner at ingest (``route``), so the hot path
-has no exchange.  Queries that span shards use one RCCL collective on u8
-register arrays with MAX (HLL merge is an elementwise max, so the result is
-bit-identical to a single-GPU run):
+ONE ownership rule serves every multi-GPU path (``KeyMap``):
+
+  owner(key)      = MurmurHash64A(key name, 0) mod world
+  local slot      = the key's rank among the keys of its owner, in the order
+                    of the job's key universe (every rank derives the same
+                    table from the same names)
+
+  * ingest routing (``route``) sends a swipe to owner(key) -- the hot path
+    then has no exchange;
+  * unpartitioned input (``SwipeExchange``) carries GLOBAL key indices into
+    the universe and maps them through the same table on the device;
+  * cross-shard queries (``ShardedSketch``) name keys, resolved to local
+    slots through the client's key table, which ``KeyMap.bind`` fills with
+    exactly the slots the other two paths write.
+
+Queries that span shards use one RCCL collective on u8 register arrays with
+MAX (HLL merge is an elementwise max, so the result is bit-identical to a
+single-GPU run):
 
   * ``pfcount_union``  -- PFCOUNT k1 k2 ... across shards: local max-merge ->
     all_reduce(MAX) of 16 KiB -> K2 count;
@@ -32,26 +47,74 @@ from typing import Sequence
 import numpy as np
 
 from .encoding import encode
-from .keyhash import murmur64a
+from .keyhash import murmur64a, murmur64a_many
 
 HLL_REGISTERS = 16384
+NO_SLOT = 0xFFFFFFFF  # a global key index outside the universe: K1 reports SKE_ERANGE
 
 
 def owner(key, world: int) -> int:
+    """Owner rank of one key name."""
     return murmur64a(encode(key), 0) % world
 
 
 def route(keys: Sequence, world: int) -> np.ndarray:
-    """Owner rank of every key (ingest routing of swipes)."""
-    cache: dict[bytes, int] = {}
-    out = np.empty(len(keys), np.int32)
-    for i, k in enumerate(keys):
-        b = encode(k)
-        r = cache.get(b)
-        if r is None:
-            r = cache[b] = murmur64a(b, 0) % world
-        out[i] = r
-    return out
+    """Owner rank of every key (ingest routing of swipes): owner() per key."""
+    return (murmur64a_many([encode(k) for k in keys], 0) % np.uint64(world)).astype(np.int32)
+
+
+class KeyMap:
+    """The key namespace of a multi-GPU job.
+
+    ``names[g]`` is global key ``g``; ``owner[g]`` = owner(names[g], world);
+    ``local[g]`` = base(owner) + the position of g among the keys of that
+    owner (increasing g).  ``base`` is an int or one int per rank (slots a
+    rank keeps below the universe, e.g. another universe bound first)."""
+
+    def __init__(self, names: Sequence, world: int, base=0):
+        self.names = [encode(n) for n in names]
+        self.world = int(world)
+        self.owner = route(self.names, world).astype(np.uint32)
+        bases = [int(base)] * self.world if np.isscalar(base) else [int(b) for b in base]
+        assert len(bases) == self.world
+        self.base = bases
+        self.local = np.empty(len(self.names), np.uint32)
+        self._mine = []
+        for r in range(self.world):
+            idx = np.nonzero(self.owner == r)[0]
+            self.local[idx] = bases[r] + np.arange(idx.size, dtype=np.uint32)
+            self._mine.append(idx)
+        self._dev = {}
+
+    def __len__(self):
+        return len(self.names)
+
+    def keys_of(self, rank: int) -> np.ndarray:
+        """Global indices of the keys `rank` owns (increasing = local slot order)."""
+        return self._mine[rank]
+
+    def count(self, rank: int) -> int:
+        return int(self._mine[rank].size)
+
+    def slots_end(self, rank: int) -> int:
+        """One past the last local slot of `rank` in this universe."""
+        return self.base[rank] + self.count(rank)
+
+    def bind(self, client, rank: int) -> None:
+        """Name this rank's keys in the client's key table at their local
+        slots (the slots K1 writes for them), so name-based queries --
+        ShardedSketch, pfcount, hll_registers -- read what the hot path wrote."""
+        for g in self._mine[rank]:
+            client.keys.bind(self.names[g], int(self.local[g]))
+
+    def tables(self, device):
+        """(owner, local) as int32 torch tensors on `device` (cached)."""
+        import torch
+        key = str(device)
+        if key not in self._dev:
+            self._dev[key] = (torch.from_numpy(self.owner.view(np.int32)).to(device),
+                              torch.from_numpy(self.local.view(np.int32)).to(device))
+        return self._dev[key]
 
 
 class LibsketchOps:
@@ -93,6 +156,8 @@ class LibsketchOps:
 
 
 class ShardedSketch:
+    """Name-based queries over keys spread by owner() across the ranks."""
+
     def __init__(self, client, rank: int, world: int, group=None, ops=None):
         import torch.distributed as dist
         self.dist = dist
@@ -101,6 +166,12 @@ class ShardedSketch:
         self.ops = ops if ops is not None else LibsketchOps(client)
         backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
         self.use_reduce_scatter = backend == "nccl"
+
+    def _owned(self, keys: Sequence) -> np.ndarray:
+        keys = list(keys)
+        if not keys:
+            return np.zeros(0, bool)
+        return route(keys, self.world) == self.rank
 
     def owns(self, key) -> bool:
         return owner(key, self.world) == self.rank
@@ -120,17 +191,18 @@ class ShardedSketch:
         return t
 
     def pfcount_union(self, keys: Sequence) -> int:
-        mine = [k for k in keys if self.owns(k)]
-        t = self.ops.merge_groups([mine])
+        keys = list(keys)
+        m = self._owned(keys)
+        t = self.ops.merge_groups([[k for k, o in zip(keys, m) if o]])
         self._all_reduce(t, self._max())
         return int(self.ops.count_raw(t)[0])
 
     def pfcount_each(self, keys: Sequence) -> np.ndarray:
         import torch
         keys = list(keys)
-        idx = [i for i, k in enumerate(keys) if self.owns(k)]
+        idx = np.nonzero(self._owned(keys))[0]
         counts = np.zeros(len(keys), np.int64)
-        if idx:
+        if idx.size:
             counts[idx] = self.ops.count_each([keys[i] for i in idx]).astype(np.int64)
         t = torch.from_numpy(counts)
         if self.use_reduce_scatter:
@@ -143,7 +215,9 @@ class ShardedSketch:
         import torch
         G = len(groups)
         per = -(-G // self.world) if G else 0
-        padded = [[k for k in g if self.owns(k)] for g in groups] + [[]] * (per * self.world - G)
+        flat = [k for g in groups for k in g]
+        m = iter(self._owned(flat).tolist())
+        padded = [[k for k in g if next(m)] for g in groups] + [[]] * (per * self.world - G)
         t = self.ops.merge_groups(padded)
         if self.use_reduce_scatter:
             mine = torch.empty((per, HLL_REGISTERS), dtype=t.dtype, device=t.device)
@@ -164,12 +238,12 @@ class SwipeExchange:
     input is not pre-partitioned, use one alltoallv per batch").
 
     Every rank holds an arbitrary slice of the stream: fixed-width ids and
-    GLOBAL key slots.  Key slot ``s`` is owned by rank ``s % world`` as its
-    local slot ``s // world`` (dense slots spread round-robin, so Zipf-hot
-    low slots land on different ranks).  One call:
+    GLOBAL key indices into ``keymap``'s universe.  Global key ``g`` is owned
+    by ``keymap.owner[g]`` as its local slot ``keymap.local[g]`` -- the rule
+    ``route`` and ``ShardedSketch`` use.  One call:
 
-      1. counting sort of the batch by owner (device: ``argsort`` of
-         ``slot % world``, ``bincount``);
+      1. counting sort of the batch by owner (device: ``ske_route_swipes``
+         through the key map's tables; CPU tensors: ``argsort``);
       2. ``all_to_all_single`` of the per-owner counts, then of the ids and
          of the local slots (RCCL over xGMI; variable splits = alltoallv);
       3. K1 on the received swipes (``k1(ids, local_slots) -> answers``);
@@ -177,15 +251,20 @@ class SwipeExchange:
          un-permuted, so the caller gets BF.EXISTS per swipe in its own order.
 
     The registers end up exactly as if every swipe had been sent to its
-    owner at ingest (PFADD is a per-register max).  With ``gloo`` (CPU tests,
-    or ranks rehearsed on one GPU) the collectives run on host copies.
+    owner at ingest (PFADD is a per-register max).  A global index outside
+    the universe travels to rank 0 with slot ``NO_SLOT``: its answer is
+    still given, its PFADD dropped and reported as SKE_ERANGE by K1.  With
+    ``gloo`` (CPU tests, or ranks rehearsed on one GPU) the collectives run
+    on host copies.
     """
 
-    def __init__(self, rank: int, world: int, k1, group=None, engine=None):
+    def __init__(self, rank: int, world: int, k1, keymap: KeyMap, group=None, engine=None):
         import torch
         import torch.distributed as dist
+        assert keymap.world == world, "the key map was built for another world size"
         self.torch, self.dist = torch, dist
         self.rank, self.world, self.k1, self.group = rank, world, k1, group
+        self.keymap = keymap
         # with an engine, device batches are sorted / returned by the native
         # routing kernels (ske_route_swipes / ske_route_return_async,
         # sketch_route.hip); without one (CPU tensors) by torch ops
@@ -193,8 +272,17 @@ class SwipeExchange:
         backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
         self.device_collectives = backend == "nccl"
 
-    def local_slot(self, slots):
-        return slots // self.world
+    def owner_local(self, gkeys):
+        """(owner, local slot) of global key indices (torch tensors)."""
+        torch = self.torch
+        own, loc = self.keymap.tables(gkeys.device)
+        n = len(self.keymap)
+        g = gkeys.to(torch.int64)
+        inside = (g >= 0) & (g < n)
+        gc = torch.where(inside, g, torch.zeros_like(g))
+        dest = torch.where(inside, own[gc].to(torch.int64), torch.zeros_like(g))
+        local = torch.where(inside, loc[gc], torch.full_like(loc[gc], -1))  # -1 = NO_SLOT as int32
+        return dest, local
 
     def _a2a(self, out, inp, out_splits, in_splits):
         if self.world == 1:  # one rank (no process group): everything is local
@@ -208,14 +296,14 @@ class SwipeExchange:
         out.copy_(o)
         return out
 
-    def swipes(self, ids, slots):
-        """ids: uint8 [n, w] tensor, slots: integer [n] tensor of global key
-        slots (same device).  Returns uint8 [n] answers in the input order."""
+    def swipes(self, ids, gkeys):
+        """ids: uint8 [n, w] tensor, gkeys: integer [n] tensor of global key
+        indices (same device).  Returns uint8 [n] answers in the input order."""
         if self.engine is not None and ids.is_cuda:
-            return self._swipes_native(ids, slots)
+            return self._swipes_native(ids, gkeys)
         torch = self.torch
         n, w = ids.shape
-        dest = (slots % self.world).to(torch.int64)
+        dest, local = self.owner_local(gkeys)
         order = torch.argsort(dest, stable=True)
         send = torch.bincount(dest, minlength=self.world)
         recv = self._a2a(torch.empty_like(send), send, None, None)
@@ -227,7 +315,7 @@ class SwipeExchange:
         r_ids = r_flat[:m * w].view(m, w)
         self._a2a(r_flat[:m * w], ids[order].reshape(-1), [c * w for c in outs], [c * w for c in ins])
         r_slots = torch.empty(m, dtype=torch.int32, device=ids.device)
-        self._a2a(r_slots, self.local_slot(slots[order]).to(torch.int32), outs, ins)
+        self._a2a(r_slots, local[order].to(torch.int32), outs, ins)
         r_ans = self.k1(r_ids, r_slots)
         back = torch.empty(n, dtype=torch.uint8, device=ids.device)
         self._a2a(back, r_ans.to(torch.uint8), ins, outs)
@@ -235,40 +323,46 @@ class SwipeExchange:
         ans[order] = back
         return ans
 
-    def _swipes_native(self, ids, slots):
+    def _swipes_native(self, ids, gkeys):
         torch = self.torch
         n, w = ids.shape
         dev = ids.device
         ids = ids.contiguous()
-        slots32 = slots.to(torch.int32).contiguous()
+        g32 = gkeys.to(torch.int32).contiguous()
+        own, loc = self.keymap.tables(dev)
         sids = torch.empty(n * w, dtype=torch.uint8, device=dev)
         sslot = torch.empty(n, dtype=torch.int32, device=dev)
         pos = torch.empty(n, dtype=torch.int32, device=dev)
         counts = np.zeros(self.world, np.uint64)
         eng = self.engine
-        eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-        eng.ctx.call("ske_route_swipes", C.c_void_p(ids.data_ptr()), w, C.c_void_p(slots32.data_ptr()), n,
-                     self.world, C.c_void_p(sids.data_ptr()), C.c_void_p(sslot.data_ptr()),
-                     C.c_void_p(pos.data_ptr()), counts.ctypes.data_as(C.c_void_p))
-        send = torch.from_numpy(counts.astype(np.int64))
-        if self.device_collectives:
-            send = send.to(dev)
-        recv = self._a2a(torch.empty_like(send), send, None, None)
-        ins = [int(c) for c in counts]
-        outs = recv.cpu().tolist()
-        m = int(sum(outs))
-        r_flat = torch.zeros(m * w + 16, dtype=torch.uint8, device=dev)
-        r_ids = r_flat[:m * w].view(m, w)
-        self._a2a(r_flat[:m * w], sids, [c * w for c in outs], [c * w for c in ins])
-        r_slots = torch.empty(m, dtype=torch.int32, device=dev)
-        self._a2a(r_slots, sslot, outs, ins)
-        r_ans = self.k1(r_ids, r_slots)
-        back = torch.empty(n, dtype=torch.uint8, device=dev)
-        self._a2a(back, r_ans.to(torch.uint8), ins, outs)
-        ans = torch.empty(n, dtype=torch.uint8, device=dev)
-        eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-        eng.ctx.call("ske_route_return_async", C.c_void_p(back.data_ptr()), C.c_void_p(pos.data_ptr()), n,
-                     C.c_void_p(ans.data_ptr()))
+        prev = eng.get_stream()
+        try:
+            eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+            eng.ctx.call("ske_route_swipes", C.c_void_p(ids.data_ptr()), w, C.c_void_p(g32.data_ptr()), n,
+                         self.world, C.c_void_p(own.data_ptr()), C.c_void_p(loc.data_ptr()), len(self.keymap),
+                         C.c_void_p(sids.data_ptr()), C.c_void_p(sslot.data_ptr()),
+                         C.c_void_p(pos.data_ptr()), counts.ctypes.data_as(C.c_void_p))
+            send = torch.from_numpy(counts.astype(np.int64))
+            if self.device_collectives:
+                send = send.to(dev)
+            recv = self._a2a(torch.empty_like(send), send, None, None)
+            ins = [int(c) for c in counts]
+            outs = recv.cpu().tolist()
+            m = int(sum(outs))
+            r_flat = torch.zeros(m * w + 16, dtype=torch.uint8, device=dev)
+            r_ids = r_flat[:m * w].view(m, w)
+            self._a2a(r_flat[:m * w], sids, [c * w for c in outs], [c * w for c in ins])
+            r_slots = torch.empty(m, dtype=torch.int32, device=dev)
+            self._a2a(r_slots, sslot, outs, ins)
+            r_ans = self.k1(r_ids, r_slots)
+            back = torch.empty(n, dtype=torch.uint8, device=dev)
+            self._a2a(back, r_ans.to(torch.uint8), ins, outs)
+            ans = torch.empty(n, dtype=torch.uint8, device=dev)
+            eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+            eng.ctx.call("ske_route_return_async", C.c_void_p(back.data_ptr()), C.c_void_p(pos.data_ptr()), n,
+                         C.c_void_p(ans.data_ptr()))
+        finally:
+            eng.set_stream(prev)
         return ans
 
 
@@ -289,14 +383,18 @@ def engine_k1(engine, fid: int = 0):
     """``SwipeExchange``'s K1 on this rank's GPU: the received fixed-width ids
     and local slots (device tensors; the ids' storage has 16 readable bytes
     past the last id) through ske_swipes_fixed_async on torch's current
-    stream."""
+    stream (the engine's stream is restored afterwards)."""
     import torch
 
     def k1(ids, slots):
         out = torch.empty(ids.shape[0], dtype=torch.uint8, device=ids.device)
         if ids.shape[0]:
-            engine.set_stream(torch.cuda.current_stream(ids.device).cuda_stream)
-            engine.swipes_fixed_async(fid, _FixedBatch(ids, slots.contiguous()), _Ptr(out.data_ptr()))
+            prev = engine.get_stream()
+            try:
+                engine.set_stream(torch.cuda.current_stream(ids.device).cuda_stream)
+                engine.swipes_fixed_async(fid, _FixedBatch(ids, slots.contiguous()), _Ptr(out.data_ptr()))
+            finally:
+                engine.set_stream(prev)
         return out
 
     return k1

@@ -110,8 +110,12 @@ class SketchEngine:
         self.ctx.call("ske_bf_reserve", fid, float(error), int(capacity), int(expansion),
                       1 if nonscaling else 0)
 
-    def gen_params(self, w: synthetic.Workload, seed=None, slot_base=0) -> GenParams:
-        cdf = synthetic.key_cdf(w)
+    def gen_params(self, w: synthetic.Workload, seed=None, slot_base=0,
+                   cdf: np.ndarray | None = None) -> GenParams:
+        """Generator parameters; `cdf` (u32, n_keys entries) overrides the
+        workload's own key distribution (e.g. a rank's share of the keys)."""
+        if cdf is None:
+            cdf = synthetic.key_cdf(w)
         dev = None
         if cdf is not None:
             buf = DeviceBuffer(self.ctx, cdf.nbytes)
@@ -214,6 +218,12 @@ class SketchEngine:
 
     def set_stream(self, stream_ptr: int | None):
         self.ctx.call("ske_set_stream", C.c_void_p(stream_ptr) if stream_ptr else None)
+
+    def get_stream(self) -> int | None:
+        """The stream calls enqueue on now (None: the context's own stream)."""
+        p = C.c_void_p()
+        self.ctx.call("ske_get_stream", C.byref(p))
+        return p.value
 
     def sync(self):
         """Wait for the context stream; raises SKE_ERANGE (SketchLibError)

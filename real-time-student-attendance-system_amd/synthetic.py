@@ -97,17 +97,41 @@ def _coprime_mul(R: int, seed: int) -> int:
     return m % R
 
 
-def key_cdf(w: Workload) -> np.ndarray | None:
-    """u32 CDF (scaled by 2^32) over keys = lecture*days + day."""
+def key_probs(w: Workload) -> np.ndarray | None:
+    """Probability of every key = lecture*days + day (None: uniform)."""
     if not w.zipf_lectures:
         return None
     L, D = w.zipf_lectures, w.zipf_days
     assert L * D == w.n_keys
     p_lect = 1.0 / np.arange(1, L + 1, dtype=np.float64) ** w.zipf_s
     p_lect /= p_lect.sum()
-    p = np.repeat(p_lect / D, D)
-    cdf = np.cumsum(p) * 2.0 ** 32
+    return np.repeat(p_lect / D, D)
+
+
+def cdf_from_probs(p: np.ndarray) -> np.ndarray:
+    """u32 CDF (scaled by 2^32) of a key distribution (renormalised)."""
+    cdf = np.cumsum(p / p.sum()) * 2.0 ** 32
     return np.minimum(np.round(cdf), 2 ** 32 - 1).astype(np.uint32)
+
+
+def key_cdf(w: Workload) -> np.ndarray | None:
+    """u32 CDF (scaled by 2^32) over keys = lecture*days + day."""
+    p = key_probs(w)
+    return None if p is None else cdf_from_probs(p)
+
+
+def key_names(w: Workload) -> list[str]:
+    """key_name() of every key of the workload (the job's key universe)."""
+    import datetime as _dt
+    days = w.zipf_days or max(1, w.n_keys)
+    dates = []
+    for day in range(days):
+        y, d = divmod(day, 365)
+        dt = _dt.date(2025, 1, 1) + _dt.timedelta(days=int(d))
+        dates.append(f"{dt.year + y:04d}-{dt.month:02d}-{dt.day:02d}")
+    if not w.zipf_lectures:
+        return [f"hll:unique:LECT{k:05d}:{dates[0]}" for k in range(w.n_keys)]
+    return [f"hll:unique:LECT{k // days:05d}:{dates[k % days]}" for k in range(w.n_keys)]
 
 
 def gen_params(w: Workload, seed: int | None = None, slot_base: int = 0,

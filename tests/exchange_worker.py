@@ -1,8 +1,10 @@
 """One rank of test_exchange_gpu.py (run under torch.distributed.run, gloo,
 every rank on this box's GPU): a slice of a C2-shaped stream over GLOBAL key
-slots, routed to the key owners by distributed.SwipeExchange, K1 on the
-device per rank.  Saves the answers (input order), this rank's registers and
-its stream for the parent's oracle check."""
+indices of a named key universe (distributed.KeyMap), routed to the key
+owners by distributed.SwipeExchange, K1 on the device per rank, then queried
+by name through distributed.ShardedSketch over a client that KeyMap.bind
+named.  Saves the answers (input order), this rank's registers, the
+cluster-wide query answers and its stream for the parent's oracle check."""
 import os
 import sys
 
@@ -19,12 +21,23 @@ def workload():
     return synthetic.Workload(**{**w.__dict__, "n_keys": NK})
 
 
+def names():
+    from rtsas_amd import synthetic
+    w = workload()
+    return [synthetic.key_name(w, k) for k in range(NK)]
+
+
+def groups(nm):
+    return [nm[i::5] for i in range(5)] + [nm, []]
+
+
 def main(out_dir):
     import torch
     import torch.distributed as dist
     import __graft_entry__ as ge
     ge.load_package()
-    from rtsas_amd.distributed import SwipeExchange, engine_k1
+    pkg = ge.load_package()
+    from rtsas_amd.distributed import KeyMap, ShardedSketch, SwipeExchange, engine_k1
     from rtsas_amd.engine import SketchEngine
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
@@ -34,8 +47,12 @@ def main(out_dir):
     eng.reserve(0, w.bf_error, w.bf_capacity)
     p = eng.gen_params(w)
     eng.preload(0, p, w.n_members)
-    nlocal = -(-NK // world)
-    eng.hll_reserve(nlocal)
+    nm = names()
+    km = KeyMap(nm, world)
+    client = pkg.SketchClient(context=eng.ctx)
+    km.bind(client, rank)
+    nlocal = km.slots_end(rank)
+    eng.hll_reserve(max(1, nlocal))
     n = N - 1000 * rank                      # uneven slices
     b = eng.swipe_batch(p, rank * N, n)
     buf, offs, slot = b.to_host()
@@ -43,12 +60,17 @@ def main(out_dir):
     assert (np.diff(offs.astype(np.int64)) == width).all()
     ids = torch.from_numpy(buf[:n * width].reshape(n, width).copy()).cuda()
     slots = torch.from_numpy(slot.astype(np.int64)).cuda()
-    ex = SwipeExchange(rank, world, engine_k1(eng), engine=eng)
+    ex = SwipeExchange(rank, world, engine_k1(eng), km, engine=eng)
     ans = ex.swipes(ids, slots)
     torch.cuda.synchronize()
     eng.sync()
+    sk = ShardedSketch(client, rank, world)
+    union = sk.pfcount_union(nm)
+    each = sk.pfcount_each(nm)
+    roll = sk.rollup(groups(nm))
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), ans=ans.cpu().numpy(), regs=eng.registers_all(nlocal),
-             buf=buf, offs=offs, slot=slot)
+             buf=buf, offs=offs, slot=slot, union=np.array([union], np.uint64), each=each, roll=roll,
+             mine=km.keys_of(rank))
     dist.barrier()
     dist.destroy_process_group()
 

@@ -1,11 +1,16 @@
-"""Unpartitioned input: distributed.SwipeExchange routes each
-rank's swipes to their key owners with all_to_all_single (alltoallv) and
-returns the answers in the input order.  world_size 2 and 3 on gloo / CPU
-tensors; K1 is replaced by the CPU oracle per rank (test infrastructure);
-the routing, the splits and the un-permutation are the product code under
-test.  Answers == BF.EXISTS of every swipe; each rank's registers == the
-single-process registers of the keys it owns (slot s -> rank s % world,
-local slot s // world)."""
+"""One key namespace across the multi-GPU paths: an
+unpartitioned C3-shaped stream -- 8-digit ids, 10 % invalid, Zipf(1.1)
+lectures x uniform days, README key names -- is ingested through
+distributed.SwipeExchange (alltoallv to the key owners of distributed.KeyMap),
+then queried by NAME through distributed.ShardedSketch: union PFCOUNT, the
+per-lecture rollup and PFCOUNT of every key must equal the one-shard oracle
+over the whole stream.  Every rank also answers BF.EXISTS for its own slice
+in input order.  The reference's counterpart is N Shared-subscription
+consumers against one Redis (attendance_processor.py:30-34, :127-129, :152).
+
+world_size 2 and 3 on gloo / CPU tensors; K1 and the register store are the
+CPU oracle per rank (test infrastructure); the key map, the routing, the
+splits, the un-permutation and the collective queries are the product code."""
 import os
 import socket
 
@@ -16,7 +21,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-NKEYS, N, W = 11, 3000, 8
+LECTURES, DAYS, N, W = 17, 6, 6000, 8
 
 
 def _free_port():
@@ -27,19 +32,37 @@ def _free_port():
     return p
 
 
+def _names():
+    import sys
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as ge
+    ge.load_package()
+    from rtsas_amd import synthetic
+    w = synthetic.Workload("t", 0.001, 1000, 10_000_000, 100_000_000, 1, 1, LECTURES * DAYS, 0.1,
+                           zipf_lectures=LECTURES, zipf_days=DAYS)
+    return [synthetic.key_name(w, k) for k in range(LECTURES * DAYS)]
+
+
+def _groups(names):
+    lect = [[n for n in names if n.split(":")[2] == f"LECT{l:05d}"] for l in range(LECTURES)]
+    return lect + [names, [], names[:1]]
+
+
 def _members():
-    return [str(10_000_000 + 7 * i).encode() for i in range(500)]
+    return [str(10_000_000 + 7919 * i).encode() for i in range(800)]
 
 
 def _stream(rank):
+    """This rank's slice of the stream: ids + GLOBAL key indices."""
     rng = np.random.default_rng(100 + rank)
     mem = _members()
-    ids = [mem[int(j)] if rng.random() < 0.8 else str(int(rng.integers(20_000_000, 99_999_999))).encode()
-           for j in rng.integers(0, len(mem), N - rank * 7)]   # uneven sizes per rank
+    n = N - rank * 113  # uneven slices
+    ids = [mem[int(j)] if rng.random() < 0.9 else str(int(rng.integers(20_000_000, 99_999_999))).encode()
+           for j in rng.integers(0, len(mem), n)]
     buf = np.frombuffer(b"".join(ids), np.uint8).reshape(-1, W).copy()
-    # a skewed key distribution (hot low slots), global slots
-    slots = np.minimum(rng.zipf(1.5, len(ids)) - 1, NKEYS - 1).astype(np.int64)
-    return buf, slots
+    lect = np.minimum(rng.zipf(1.1, n) - 1, LECTURES - 1)
+    gkey = (lect * DAYS + rng.integers(0, DAYS, n)).astype(np.int64)
+    return buf, gkey
 
 
 def _chain(orc):
@@ -51,19 +74,47 @@ def _chain(orc):
     return ch
 
 
+class _StoreOps:
+    """ShardedSketch's device ops over this rank's oracle register store,
+    resolving names through the rank's key table (as KeyMap.bind does for a
+    client)."""
+    device = torch.device("cpu")
+
+    def __init__(self, orc, regs, slot_of):
+        self.orc, self.regs, self.slot_of = orc, regs, slot_of
+
+    def merge_groups(self, groups):
+        t = torch.zeros((len(groups), 16384), dtype=torch.uint8)
+        for i, g in enumerate(groups):
+            acc = np.zeros(16384, np.uint8)
+            for k in g:
+                acc = np.maximum(acc, self.regs[self.slot_of[k.encode()]])
+            t[i] = torch.from_numpy(acc)
+        return t
+
+    def count_raw(self, t):
+        return np.array([self.orc.hll_count_regs(r.numpy()) for r in t], np.uint64)
+
+    def count_each(self, keys):
+        return np.array([self.orc.hll_count_regs(self.regs[self.slot_of[k.encode()]]) for k in keys],
+                        np.uint64)
+
+
 def _worker(rank, world, port, out_dir):
     import sys
     sys.path.insert(0, ROOT)
     import __graft_entry__ as ge
     ge.load_package()
     orc = ge.load_oracle()
-    from rtsas_amd.distributed import SwipeExchange
+    from rtsas_amd.distributed import KeyMap, ShardedSketch, SwipeExchange
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    names = _names()
+    km = KeyMap(names, world)
     chain = _chain(orc)
-    nlocal = -(-NKEYS // world)
-    regs = np.zeros((nlocal, 16384), np.uint8)
+    regs = np.zeros((km.slots_end(rank), 16384), np.uint8)
+    slot_of = {km.names[g]: int(km.local[g]) for g in km.keys_of(rank)}
 
     def k1(ids, local_slots):   # the oracle as this rank's K1
         m = ids.shape[0]
@@ -72,27 +123,61 @@ def _worker(rank, world, port, out_dir):
         v, _, _ = orc.process_swipes(chain, regs, local_slots.numpy().astype(np.uint32), buf, offs)
         return torch.from_numpy(v.astype(np.uint8))
 
-    ex = SwipeExchange(rank, world, k1)
-    buf, slots = _stream(rank)
-    ans = ex.swipes(torch.from_numpy(buf), torch.from_numpy(slots))
-    np.savez(os.path.join(out_dir, f"r{rank}.npz"), ans=ans.numpy(), regs=regs)
+    ex = SwipeExchange(rank, world, k1, km)
+    buf, gkey = _stream(rank)
+    ans = ex.swipes(torch.from_numpy(buf), torch.from_numpy(gkey))
+    sk = ShardedSketch(None, rank, world, ops=_StoreOps(orc, regs, slot_of))
+    union = sk.pfcount_union(names)
+    each = sk.pfcount_each(names)
+    roll = sk.rollup(_groups(names))
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), ans=ans.numpy(), union=np.array([union], np.uint64),
+             each=each, roll=roll, owned=np.array([km.count(rank)]))
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_exchange_equals_owner_routing(orc, tmp_path, world):
+def test_exchange_then_sharded_queries_equal_one_shard(orc, tmp_path, world):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    names = _names()
     chain = _chain(orc)
-    regs = np.zeros((NKEYS, 16384), np.uint8)
-    for r in range(world):   # the single-process run over every rank's stream
-        buf, slots = _stream(r)
+    regs = np.zeros((len(names), 16384), np.uint8)
+    for r in range(world):   # the single-process run over every rank's slice
+        buf, gkey = _stream(r)
         flat = np.concatenate([buf.reshape(-1), np.zeros(16, np.uint8)])
-        offs = np.arange(0, W * len(slots) + 1, W, dtype=np.uint32)
-        want, _, _ = orc.process_swipes(chain, regs, slots.astype(np.uint32), flat, offs)
+        offs = np.arange(0, W * len(gkey) + 1, W, dtype=np.uint32)
+        want, _, _ = orc.process_swipes(chain, regs, gkey.astype(np.uint32), flat, offs)
         got = np.load(tmp_path / f"r{r}.npz")["ans"]
         assert np.array_equal(got, want.astype(np.uint8)), f"rank {r} answers"
     assert regs.any()
-    for s in range(NKEYS):
-        rr = np.load(tmp_path / f"r{s % world}.npz")["regs"]
-        assert np.array_equal(rr[s // world], regs[s]), f"slot {s}"
+    want_each = [orc.hll_count_regs(regs[g]) for g in range(len(names))]
+    want_union = orc.hll_count_regs(regs.max(axis=0))
+    idx = {n: g for g, n in enumerate(names)}
+    want_roll = [orc.hll_count_regs(regs[[idx[n] for n in g]].max(axis=0)) if g else 0
+                 for g in _groups(names)]
+    owned = 0
+    for r in range(world):   # every rank got the same cluster-wide answers
+        d = np.load(tmp_path / f"r{r}.npz")
+        assert int(d["union"][0]) == want_union
+        assert d["each"].tolist() == want_each
+        assert d["roll"].tolist() == want_roll
+        assert 0 < int(d["owned"][0]) < len(names)
+        owned += int(d["owned"][0])
+    assert owned == len(names)
+
+
+def test_key_map_is_one_rule(pkg):
+    """KeyMap's owner is route()'s / owner()'s; local slots are dense per rank
+    in universe order; the vectorised hash equals the scalar one."""
+    from rtsas_amd.distributed import KeyMap, owner, route
+    from rtsas_amd.keyhash import murmur64a, murmur64a_many
+    names = [f"hll:unique:LECT{i:05d}:2025-03-{1 + i % 28:02d}" for i in range(500)] + ["k", "", "x" * 23]
+    km = KeyMap(names, 5, base=[3, 0, 7, 1, 2])
+    assert km.owner.tolist() == [owner(n, 5) for n in names] == route(names, 5).tolist()
+    for r in range(5):
+        g = km.keys_of(r)
+        assert (km.owner[g] == r).all()
+        assert km.local[g].tolist() == list(range(km.base[r], km.base[r] + g.size))
+    assert sum(km.count(r) for r in range(5)) == len(names)
+    enc = [n.encode() for n in names]
+    assert murmur64a_many(enc, 0x1234).tolist() == [murmur64a(b, 0x1234) for b in enc]

@@ -1,9 +1,12 @@
 """Unpartitioned swipes routed by alltoallv on the device path (SURVEY.md
 §8e): W ranks on this box's GPU (gloo transport; RCCL on a node), each with
-its own slice of the stream over global key slots.  distributed.SwipeExchange
-sends every swipe to its key's owner, K1 runs there, the answers come back in
-the input order.  Answers == the oracle's BF.EXISTS; every rank's registers ==
-the single-process registers of the keys it owns."""
+its own slice of the stream over global key indices of a named universe.
+distributed.SwipeExchange sends every swipe to its key's owner (distributed.
+KeyMap), K1 runs there, the answers come back in the input order; then
+distributed.ShardedSketch answers union PFCOUNT, PFCOUNT of every key and a
+rollup by key NAME.  Answers == the oracle's BF.EXISTS; every rank's
+registers == the single-process registers of the keys it owns; the
+cluster-wide queries == the one-shard oracle."""
 import os
 import subprocess
 import sys
@@ -18,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.parametrize("world", [2, 3])
 def test_exchange_on_device_equals_oracle(orc, engine, tmp_path, world):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from exchange_worker import NK, workload
+    from exchange_worker import NK, groups, names, workload
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
@@ -36,6 +39,16 @@ def test_exchange_on_device_equals_oracle(orc, engine, tmp_path, world):
         d = np.load(tmp_path / f"r{rk}.npz")
         want, _, _ = orc.process_swipes(chain, regs, d["slot"].astype(np.uint32), d["buf"], d["offs"])
         assert np.array_equal(d["ans"], want.astype(np.uint8)), f"rank {rk} answers"
-    for s in range(NK):
-        rr = np.load(tmp_path / f"r{s % world}.npz")["regs"]
-        assert np.array_equal(rr[s // world], regs[s]), f"slot {s}"
+    seen = 0
+    for rk in range(world):
+        d = np.load(tmp_path / f"r{rk}.npz")
+        for j, g in enumerate(d["mine"]):
+            assert np.array_equal(d["regs"][j], regs[g]), f"key {g} on rank {rk}"
+        seen += len(d["mine"])
+        nm = names()
+        idx = {n: i for i, n in enumerate(nm)}
+        assert int(d["union"][0]) == orc.hll_count_regs(regs.max(axis=0))
+        assert d["each"].tolist() == [orc.hll_count_regs(regs[g]) for g in range(NK)]
+        assert d["roll"].tolist() == [orc.hll_count_regs(regs[[idx[n] for n in g]].max(axis=0)) if g else 0
+                                      for g in groups(nm)]
+    assert seen == NK

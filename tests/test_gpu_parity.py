@@ -332,6 +332,34 @@ def test_slot_out_of_range_is_an_error(pkg, engine):
     assert rc == -7
 
 
+def test_sync_call_reports_only_its_own_slot_error(pkg, engine):
+    """An enqueue-only K1 with a bad slot is reported by the next ske_sync /
+    ske_check_errors, not blamed on a synchronous call that ran clean in
+    between (the device word is taken by atomic exchanges, never lost)."""
+    import rtsas_amd
+    from rtsas_amd._lib import SketchLibError, SKE_ERANGE
+    from rtsas_amd.engine import DeviceBatch
+    engine.reserve(0, 0.01, 1000)
+    buf, offs = rtsas_amd.pack_ints(list(range(100, 200)))
+    engine.ctx.call("ske_bf_madd", 0, buf.ctypes.data_as(C.c_void_p), offs.ctypes.data_as(C.c_void_p),
+                    100, None, 0)
+    engine.hll_reserve(4)
+    cap = engine.ctx.lib.ske_hll_capacity(engine.ctx.ptr)
+    bad = DeviceBatch.from_host(engine.ctx, buf, offs, np.full(100, cap + 3, np.uint32))
+    good = DeviceBatch.from_host(engine.ctx, buf, offs, np.zeros(100, np.uint32))
+    engine.swipes_async(0, bad)           # leaves the sticky word set
+    engine.swipes(0, good)                # synchronous and clean: must not raise
+    with pytest.raises(SketchLibError) as ei:
+        engine.check_errors()             # the earlier async error surfaces here
+    assert ei.value.code == SKE_ERANGE
+    engine.check_errors()                 # and only once
+    with pytest.raises(SketchLibError):
+        engine.swipes(0, bad)             # a synchronous call's own error
+    engine.sync()
+    bad.free()
+    good.free()
+
+
 def test_generator_matches_numpy_restatement(engine):
     from gen_ref import Gen
     from rtsas_amd import synthetic

@@ -11,7 +11,7 @@ GROUPS_=("FETCH_SIZE" "WRITE_SIZE" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" "TCC
  "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES" "SQ_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT")
 for c in "${GROUPS_[@]}"; do
   tag=$(echo $c | tr ' ' '_')
-  timeout -k 10 120 rocprofv3 --pmc $c -d gpurun_out/pmc_$TAG/$tag -o run --output-format csv -- python bench.py $ARGS --no-cpu --no-check > gpurun_out/pmc_$TAG/$tag.log 2>&1; rc=$?
+  timeout -k 10 120 rocprofv3 --pmc $c -d gpurun_out/pmc_$TAG/$tag -o run --output-format csv -- python bench.py $ARGS --no-cpu --secondary none --pass-replay 0 --no-check > gpurun_out/pmc_$TAG/$tag.log 2>&1; rc=$?
   echo "pmc [$c] rc=$rc"
   if [ $rc -ne 0 ]; then tail -3 gpurun_out/pmc_$TAG/$tag.log; exit $rc; fi
 done

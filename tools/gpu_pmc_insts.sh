@@ -9,7 +9,7 @@ GROUPS_=("SQ_INSTS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_
  "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_VSKIPPED GRBM_GUI_ACTIVE GRBM_COUNT")
 for c in "${GROUPS_[@]}"; do
   tag=$(echo $c | tr ' ' '_' | cut -c1-60)
-  timeout -k 10 300 rocprofv3 --pmc $c -d gpurun_out/pmci_$TAG/$tag -o run --output-format csv -- python bench.py --steps 12 --warmup 3 --no-cpu $BENCH_ARGS > gpurun_out/pmci_$TAG/$tag.log 2>&1; rc=$?
+  timeout -k 10 300 rocprofv3 --pmc $c -d gpurun_out/pmci_$TAG/$tag -o run --output-format csv -- python bench.py --steps 12 --warmup 3 --no-cpu --secondary none --pass-replay 0 $BENCH_ARGS > gpurun_out/pmci_$TAG/$tag.log 2>&1; rc=$?
   echo "pmc [$c] rc=$rc"
   if [ $rc -ne 0 ]; then tail -3 gpurun_out/pmci_$TAG/$tag.log; exit $rc; fi
 done

@@ -3,7 +3,7 @@
 # bench; per-kernel summaries of the partitioned K1's passes into
 # gpurun_out/pmc_<TAG>_{a,b,c}.json.   usage: TAG=c3 bash tools/gpu_pmc_part.sh
 TAG=${TAG:-c3}
-ARGS=${BENCH_ARGS:-"--config c3 --steps 8 --warmup 2 --no-cpu --streams 1 --graph 0"}
+ARGS=${BENCH_ARGS:-"--config c3 --steps 8 --warmup 2 --no-cpu --secondary none --pass-replay 0 --streams 1 --graph 0"}
 mkdir -p gpurun_out/pmc_$TAG
 export TMPDIR=/tmp
 GROUPS_=("FETCH_SIZE" "WRITE_SIZE" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum"

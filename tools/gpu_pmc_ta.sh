@@ -2,7 +2,7 @@
 # Address / data path counters (TA, TD, TCP) of the partitioned K1's passes,
 # one group per rocprofv3 --pmc run.   usage: TAG=c3ta bash tools/gpu_pmc_ta.sh
 TAG=${TAG:-c3ta}
-ARGS=${BENCH_ARGS:-"--config c3 --steps 6 --warmup 2 --no-cpu --streams 1 --graph 0"}
+ARGS=${BENCH_ARGS:-"--config c3 --steps 6 --warmup 2 --no-cpu --secondary none --pass-replay 0 --streams 1 --graph 0"}
 mkdir -p gpurun_out/pmc_$TAG
 export TMPDIR=/tmp
 GROUPS_=("TA_TA_BUSY_sum TA_BUFFER_WAVEFRONTS_sum GRBM_GUI_ACTIVE" "TD_TD_BUSY_sum TD_TC_STALL_sum"

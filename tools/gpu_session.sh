@@ -27,9 +27,9 @@ if [ -n "$PROF" ]; then
 fi
 IFS=';' read -ra SETS <<< "$MATRIX"
 for v in "${SETS[@]}"; do
-  timeout -k 10 300 python bench.py --no-cpu $v > gpurun_out/bench_m.log 2>&1; rc=$?
+  timeout -k 10 300 python bench.py --no-cpu --secondary none $v > gpurun_out/bench_m.log 2>&1; rc=$?
   if [ $rc -ne 0 ]; then echo "bench [$v] rc=$rc"; tail -5 gpurun_out/bench_m.log; exit $rc; fi
-  echo -n "[$v] "; python -c "import json; d=json.loads(open('gpurun_out/bench_m.log').read().strip().splitlines()[-1]); r=d['roofline']; print('%.3e swipes/s  step %.4f ms  kernel %.4f ms  enq %.1f us  %s tile=%s frac=%.2f' % (d['value'], d['ms_per_step'], r['kernel_ms'], d['host_enqueue_us_per_step'], d['config']['k1_variant'], d['config']['tile'], r['frac']))"
+  echo -n "[$v] "; python -c "import json; d=json.loads(open('gpurun_out/bench_m.log').read().strip().splitlines()[-1]); r=d['roofline']; print('%.3e swipes/s  step %.4f ms  kernel %s %.4f ms  enq %.1f us  %s frac=%.2f  passes %s' % (d['value'], d['ms_per_step'], r['kernel'], r['kernel_ms'], d['host_enqueue_us_per_step'], d['config']['k1_variant'], r['frac'], {k: round(v['ms'], 4) for k, v in r['passes'].items()}))"
 done
 if [ -n "$STAMPS" ]; then
   for t in ${STAMP_TILES:-2}; do
