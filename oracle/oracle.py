@@ -89,6 +89,15 @@ def lib():
                                         C.c_void_p, C.c_uint64, C.c_void_p, u64p, C.c_int]
     L.orc_hll_madd.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                C.c_void_p]
+    L.orc_chain_dump_header.restype = C.c_size_t
+    L.orc_chain_dump_header.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+    L.orc_chain_dump_chunk.restype = C.c_size_t
+    L.orc_chain_dump_chunk.argtypes = [C.c_void_p, C.POINTER(C.c_longlong), C.c_size_t,
+                                       C.POINTER(C.c_void_p)]
+    L.orc_chain_from_header.restype = C.c_void_p
+    L.orc_chain_from_header.argtypes = [C.c_char_p, C.c_size_t]
+    L.orc_chain_load_chunk.restype = C.c_int
+    L.orc_chain_load_chunk.argtypes = [C.c_void_p, C.c_longlong, C.c_char_p, C.c_size_t]
     _lib = L
     return L
 
@@ -156,14 +165,59 @@ def hll_decode_string(s: bytes) -> np.ndarray | None:
     return regs if rc == 0 else None
 
 
+MAX_SCANDUMP_SIZE = 10 * 1024 * 1024  # rebloom.c MAX_SCANDUMP_SIZE [recall]
+
+
 class Chain:
     """RedisBloom scalable chain (SB_NewChain options as rebloom.c uses)."""
 
-    def __init__(self, capacity: int, error: float, expansion: int = 2, nonscaling: bool = False):
+    def __init__(self, capacity: int, error: float, expansion: int = 2, nonscaling: bool = False,
+                 _ptr_=None):
+        if _ptr_ is not None:
+            self.p = _ptr_
+            return
         opts = OPT_FORCE64 | OPT_NOROUND | (OPT_NO_SCALING if nonscaling else 0)
         self.p = lib().orc_chain_new(capacity, error, opts, expansion)
         if not self.p:
             raise ValueError("orc_chain_new failed")
+
+    # ---- BF.SCANDUMP / BF.LOADCHUNK (RedisBloom src/sb.c, restated in C)
+    def scandump(self, it: int, max_chunk: int = MAX_SCANDUMP_SIZE) -> tuple[int, bytes]:
+        """BF.SCANDUMP key it -> (next iterator, data)."""
+        L = lib()
+        if it == 0:
+            n = L.orc_chain_dump_header(self.p, None, 0)
+            out = np.zeros(n, np.uint8)
+            L.orc_chain_dump_header(self.p, _ptr(out), n)
+            return 1, out.tobytes()
+        cur, data = C.c_longlong(it), C.c_void_p()
+        n = L.orc_chain_dump_chunk(self.p, C.byref(cur), max_chunk, C.byref(data))
+        return cur.value, (C.string_at(data.value, n) if n else b"")
+
+    def scandump_all(self, max_chunk: int = MAX_SCANDUMP_SIZE) -> list[tuple[int, bytes]]:
+        """Every (iterator, chunk) pair a client's SCANDUMP loop collects, header first."""
+        out, it = [], 0
+        while True:
+            it, data = self.scandump(it, max_chunk)
+            if it == 0:
+                return out
+            out.append((it, data))
+
+    @classmethod
+    def loadchunks(cls, chunks) -> "Chain":
+        """BF.LOADCHUNK of every (iterator, chunk) pair into a new chain."""
+        L = lib()
+        (it0, hdr), rest = chunks[0], chunks[1:]
+        assert it0 == 1
+        p = L.orc_chain_from_header(hdr, len(hdr))
+        if not p:
+            raise ValueError("ERR received bad data")
+        ch = cls(0, 0, _ptr_=p)
+        for it, data in rest:
+            rc = L.orc_chain_load_chunk(p, it, data, len(data))
+            if rc:
+                raise ValueError(f"LOADCHUNK rc {rc}")
+        return ch
 
     def __del__(self):
         if getattr(self, "p", None):

@@ -430,6 +430,145 @@ const uint8_t *orc_chain_link_bits(const orc_chain *c, int i) {
 }
 
 /* ======================================================================
+ * BF.SCANDUMP / BF.LOADCHUNK -- RedisBloom src/sb.c [recall]:
+ *   dumpedChainHeader (packed, little-endian on x86):
+ *     u64 size; u32 nfilters; u32 options; u32 growth;  dumpedChainLink[nfilters]
+ *   dumpedChainLink (packed), X_ENCODED_LINK's fields in declaration order:
+ *     u64 bytes; u64 bits; u64 size; double error; double bpe; u32 hashes;
+ *     u64 entries; u8 n2
+ *   SBChain_GetEncodedHeader -> reply (SB_CHUNKITER_INIT = 1, header);
+ *   SBChain_GetEncodedChunk: iter - 1 is a byte offset into the links' bit
+ *   arrays laid end to end (getLinkPos); a chunk never crosses a link and is
+ *   at most MAX_SCANDUMP_SIZE bytes; the next iterator is iter + len; past
+ *   the end: iterator 0, no data.  SB_NewChainFromHeader: the chain of the
+ *   header's links with zeroed bit arrays (force64 from the options);
+ *   SBChain_LoadEncodedChunk: the chunk goes to offset (iter - len) - 1.
+ * Written field by field here (no packed struct), as an encoder independent
+ * of the product's formats.bf_dump_header.
+ * ==================================================================== */
+static void put_le(uint8_t **p, uint64_t v, int n) {
+    for (int i = 0; i < n; i++) (*p)[i] = (uint8_t)(v >> (8 * i));
+    *p += n;
+}
+static uint64_t get_le(const uint8_t **p, int n) {
+    uint64_t v = 0;
+    for (int i = 0; i < n; i++) v |= (uint64_t)(*p)[i] << (8 * i);
+    *p += n;
+    return v;
+}
+static uint64_t dbl_bits(double d) {
+    uint64_t v;
+    memcpy(&v, &d, 8);
+    return v;
+}
+static double bits_dbl(uint64_t v) {
+    double d;
+    memcpy(&d, &v, 8);
+    return d;
+}
+
+size_t orc_chain_dump_header(const orc_chain *c, uint8_t *out, size_t cap) {
+    const size_t len = ORC_SB_HEADER_BYTES + (size_t)c->nlinks * ORC_SB_LINK_BYTES;
+    if (!out || cap < len) return len;
+    uint8_t *p = out;
+    put_le(&p, c->size, 8);
+    put_le(&p, (uint64_t)c->nlinks, 4);
+    put_le(&p, c->options, 4);
+    put_le(&p, c->growth, 4);
+    for (int i = 0; i < c->nlinks; i++) {
+        const orc_bloom *l = &c->links[i];
+        put_le(&p, l->bytes, 8);
+        put_le(&p, l->bits, 8);
+        put_le(&p, l->size, 8);
+        put_le(&p, dbl_bits(l->error), 8);
+        put_le(&p, dbl_bits(l->bpe), 8);
+        put_le(&p, (uint64_t)(uint32_t)l->hashes, 4);
+        put_le(&p, l->entries, 8);
+        put_le(&p, l->n2, 1);
+    }
+    return len;
+}
+
+/* getLinkPos(): the link holding byte iter - 1 of the concatenated arrays */
+static int link_pos(const orc_chain *c, long long iter, uint64_t *offset) {
+    if (iter < 1) return -1;
+    uint64_t cur = (uint64_t)(iter - 1), seek = 0;
+    for (int i = 0; i < c->nlinks; i++) {
+        if (seek + c->links[i].bytes > cur) {
+            *offset = cur - seek;
+            return i;
+        }
+        seek += c->links[i].bytes;
+    }
+    return -1;
+}
+
+size_t orc_chain_dump_chunk(const orc_chain *c, long long *iter, size_t max_chunk, const uint8_t **data) {
+    uint64_t off = 0;
+    const int i = link_pos(c, *iter, &off);
+    if (i < 0) {
+        *iter = 0;
+        *data = NULL;
+        return 0;
+    }
+    size_t len = max_chunk;
+    const uint64_t remaining = c->links[i].bytes - off;
+    if (remaining < len) len = (size_t)remaining;
+    *iter += (long long)len;
+    *data = c->links[i].bf + off;
+    return len;
+}
+
+orc_chain *orc_chain_from_header(const uint8_t *buf, size_t len) {
+    if (!buf || len < ORC_SB_HEADER_BYTES) return NULL;
+    const uint8_t *p = buf;
+    const uint64_t size = get_le(&p, 8);
+    const uint32_t nf = (uint32_t)get_le(&p, 4);
+    const uint32_t options = (uint32_t)get_le(&p, 4);
+    const uint32_t growth = (uint32_t)get_le(&p, 4);
+    if (nf == 0 || len < ORC_SB_HEADER_BYTES + (size_t)nf * ORC_SB_LINK_BYTES) return NULL;
+    orc_chain *c = (orc_chain *)calloc(1, sizeof(orc_chain));
+    if (!c) return NULL;
+    c->links = (orc_bloom *)calloc(nf, sizeof(orc_bloom));
+    if (!c->links) {
+        free(c);
+        return NULL;
+    }
+    c->nlinks = (int)nf;
+    c->size = size;
+    c->options = options;
+    c->growth = growth;
+    for (uint32_t i = 0; i < nf; i++) {
+        orc_bloom *l = &c->links[i];
+        l->bytes = get_le(&p, 8);
+        l->bits = get_le(&p, 8);
+        l->size = get_le(&p, 8);
+        l->error = bits_dbl(get_le(&p, 8));
+        l->bpe = bits_dbl(get_le(&p, 8));
+        l->hashes = (int)(uint32_t)get_le(&p, 4);
+        l->entries = get_le(&p, 8);
+        l->n2 = (uint8_t)get_le(&p, 1);
+        l->force64 = (options & ORC_BLOOM_OPT_FORCE64) ? 1 : 0;
+        l->bf = (uint8_t *)calloc(1, l->bytes ? l->bytes : 1);
+        if (!l->bf) {
+            orc_chain_free(c);
+            return NULL;
+        }
+    }
+    return c;
+}
+
+int orc_chain_load_chunk(orc_chain *c, long long iter, const uint8_t *buf, size_t len) {
+    if (!buf || iter <= 0 || iter < (long long)len) return -1; /* "ERR received bad data" */
+    uint64_t off = 0;
+    const int i = link_pos(c, iter - (long long)len, &off);
+    if (i < 0) return -2;                                      /* "ERR invalid offset - no link found" */
+    if (len > c->links[i].bytes - off) return -3;              /* "ERR invalid chunk - Too big ..." */
+    memcpy(c->links[i].bf + off, buf, len);
+    return 0;
+}
+
+/* ======================================================================
  * Batched helpers
  * ==================================================================== */
 void orc_chain_madd(orc_chain *c, const uint8_t *bytes, const uint32_t *offs, uint64_t n,

@@ -117,6 +117,20 @@ int orc_chain_link_info(const orc_chain *c, int i, uint64_t *entries, uint64_t *
                         uint64_t *bits, int *hashes, uint64_t *size, double *error);
 const uint8_t *orc_chain_link_bits(const orc_chain *c, int i);
 
+/* ---------------- BF.SCANDUMP / BF.LOADCHUNK (RedisBloom src/sb.c) ---------------- */
+#define ORC_SB_CHUNKITER_INIT 1
+#define ORC_SB_HEADER_BYTES 20 /* dumpedChainHeader: u64 size, u32 nfilters, u32 options, u32 growth */
+#define ORC_SB_LINK_BYTES 53   /* dumpedChainLink: u64 bytes, bits, size; f64 error, bpe; u32 hashes;
+                                  u64 entries; u8 n2 */
+/* SBChain_GetEncodedHeader: writes the header if cap allows; returns its length */
+size_t orc_chain_dump_header(const orc_chain *c, uint8_t *out, size_t cap);
+/* SBChain_GetEncodedChunk: *iter in/out (past the end: 0 and no data) */
+size_t orc_chain_dump_chunk(const orc_chain *c, long long *iter, size_t max_chunk, const uint8_t **data);
+/* SB_NewChainFromHeader (NULL on bad data) / SBChain_LoadEncodedChunk (0 ok,
+ * -1 bad data, -2 no link at that offset, -3 chunk too big for its link) */
+orc_chain *orc_chain_from_header(const uint8_t *buf, size_t len);
+int orc_chain_load_chunk(orc_chain *c, long long iter, const uint8_t *buf, size_t len);
+
 /* ---------------- batched helpers (ctypes-friendly) ---------------- */
 /* packed ids: bytes + offs[n+1] */
 void orc_chain_madd(orc_chain *c, const uint8_t *bytes, const uint32_t *offs, uint64_t n,

@@ -65,3 +65,71 @@ def test_bf_dump_header_round_trip(pkg, orc):
     assert p["size"] == c.size and p["growth"] == 2 and not p["nonscaling"]
     assert [(l["bytes"], l["entries"], l["hashes"]) for l in p["links"]] == \
         [(l["bytes"], l["entries"], l["hashes"]) for l in links]
+
+
+def _default_chain(orc):
+    """The reference's preload: 1000 unique 5-digit ids BF.ADDed one by one to
+    a key nothing reserved (data_generator.py:53-63), so RedisBloom's BF.ADD
+    auto-creates capacity 100 / error 0.01 / expansion 2 and grows 4 links."""
+    rng = np.random.default_rng(1003)
+    ch = orc.Chain(100, 0.01)
+    ids = [str(int(x)).encode() for x in rng.choice(np.arange(10000, 100000), 1000, replace=False)]
+    for i in ids:
+        ch.add(i)
+    return ch, ids
+
+
+@pytest.mark.parametrize("shape", ["default-chain", "c3-filter", "nonscaling"])
+def test_bf_dump_header_equals_oracle_bytes(pkg, orc, shape):
+    """formats.bf_dump_header / bf_parse_header against the oracle's own
+    field-by-field encoder of RedisBloom's dumpedChainHeader / dumpedChainLink
+    (oracle/sketch_oracle.c orc_chain_dump_header): byte for byte.  Parity
+    unpinned vs a live RedisBloom (layout [recall])."""
+    from rtsas_amd import formats
+    if shape == "default-chain":
+        ch, _ = _default_chain(orc)
+        assert ch.nlinks == 4
+    elif shape == "c3-filter":
+        ch = orc.Chain(10_000_000, 0.001)
+        for i in range(2000):
+            ch.add(str(10_000_000 + 37 * i).encode())
+    else:
+        ch = orc.Chain(500, 0.001, expansion=4, nonscaling=True)
+        for i in range(400):
+            ch.add(str(i).encode())
+    it, hdr = ch.scandump(0)
+    assert it == 1 and len(hdr) == 20 + 53 * ch.nlinks
+    p = formats.bf_parse_header(hdr)
+    assert p["size"] == ch.size and len(p["links"]) == ch.nlinks
+    assert p["options"] == (5 | (8 if shape == "nonscaling" else 0))
+    for i, L in enumerate(p["links"]):
+        info = ch.link_info(i)
+        for k in ("entries", "bytes", "bits", "hashes", "size", "error"):
+            assert L[k] == info[k], (i, k)
+        assert L["n2"] == 0                     # NOROUND: no power-of-two rounding
+    if shape == "default-chain":
+        assert [L["entries"] for L in p["links"]] == [100, 200, 400, 800]
+        assert [L["bytes"] for L in p["links"]] == [144, 312, 696, 1536]
+        assert [L["hashes"] for L in p["links"]] == [8, 9, 10, 11]
+    if shape == "c3-filter":
+        assert (p["links"][0]["bytes"], p["links"][0]["hashes"]) == (19_775_360, 11)
+    assert formats.bf_dump_header(p["size"], p["links"], p["growth"], p["nonscaling"]) == hdr
+
+
+def test_bf_scandump_chunks_round_trip_in_oracle(orc):
+    """The oracle's SCANDUMP chunk walk (getLinkPos: chunks never cross a link,
+    iterator = 1 + byte offset of the chunk's end) and LOADCHUNK replay."""
+    ch, ids = _default_chain(orc)
+    chunks = ch.scandump_all(max_chunk=100)
+    total = sum(ch.link_info(i)["bytes"] for i in range(ch.nlinks))
+    assert chunks[-1][0] == 1 + total
+    pos = 1
+    for it, data in chunks[1:]:
+        assert it == pos + len(data) and 0 < len(data) <= 100
+        pos = it
+    cp = orc.Chain.loadchunks(chunks)
+    assert cp.nlinks == ch.nlinks and cp.size == ch.size
+    for i in range(ch.nlinks):
+        assert cp.link_info(i) == ch.link_info(i)
+        assert np.array_equal(cp.link_bits(i), ch.link_bits(i))
+    assert all(cp.exists(i) for i in ids)

@@ -573,6 +573,54 @@ def test_bf_scandump_loadchunk_round_trip(client, orc, shape):
         client.execute_command("BF.LOADCHUNK", "dst", 1, chunks[0][1])
 
 
+@pytest.mark.parametrize("shape", ["default-chain", "c3-filter"])
+def test_bf_loadchunk_of_oracle_dump(client, orc, shape):
+    """BF.LOADCHUNK of a dump the ORACLE produced (oracle/sketch_oracle.c's
+    restatement of RedisBloom SBChain_GetEncodedHeader / GetEncodedChunk, an
+    encoder independent of formats.py): the reference's default 4-link chain
+    (1000 ids BF.ADDed to an auto-created key, data_generator.py:57-63) and
+    the C3 filter.  The device chain must then have the oracle's BF.INFO,
+    every link's bits, and its MEXISTS answers; and the device's own
+    BF.SCANDUMP must reproduce the oracle's chunks byte for byte.  Parity
+    unpinned vs a live RedisBloom (layout [recall])."""
+    rng = np.random.default_rng(23)
+    if shape == "default-chain":
+        ch = orc.Chain(100, 0.01)
+        ids = [int(x) for x in rng.choice(np.arange(10000, 100000), 1000, replace=False)]
+        for i in ids:
+            ch.add(str(i).encode())
+        assert ch.nlinks == 4
+        probe = ids + [int(x) for x in rng.integers(100000, 999999, 3000)]
+    else:
+        ch = orc.Chain(10_000_000, 0.001)
+        ids = rng.integers(10**7, 10**8, 300_000)
+        ch.madd_packed(*client_pack([int(x) for x in ids]))
+        probe = [int(x) for x in ids[:50_000]] + [int(x) for x in rng.integers(10**7, 10**8, 50_000)]
+    dump = ch.scandump_all(max_chunk=4096 if shape == "default-chain" else orc.MAX_SCANDUMP_SIZE)
+    for it, data in dump:
+        assert client.execute_command("BF.LOADCHUNK", "ld", it, data) == "OK"
+    info = client.bf_info("ld")
+    assert info["Number of filters"] == ch.nlinks
+    assert info["Number of items inserted"] == ch.size
+    links = client.bf_links("ld")
+    for i in range(ch.nlinks):
+        o = ch.link_info(i)
+        assert {k: links[i][k] for k in ("entries", "bytes", "bits", "hashes", "size")} == \
+            {k: o[k] for k in ("entries", "bytes", "bits", "hashes", "size")}, i
+        assert links[i]["error"] == o["error"]
+        assert np.array_equal(client.bf_link_bits("ld", i), ch.link_bits(i)), f"link {i} bits"
+    pb, po = client_pack(probe)
+    want, _ = ch.mexists_packed(pb, po)
+    assert client.execute_command("BF.MEXISTS", "ld", *probe) == want.astype(int).tolist()
+    got, it = [], 0
+    while True:
+        it, data = client.execute_command("BF.SCANDUMP", "ld", it)
+        if it == 0:
+            break
+        got.append((it, data))
+    assert got == ch.scandump_all()
+
+
 def test_pfmerge_many_sources_two_level(client):
     """PFMERGE of 3000 keys (the two-level parallel merge used past 256
     sources) == the register-wise max, dst's own registers included; and
