@@ -83,7 +83,7 @@ struct ske_ctx {
     int xr_finish_u = 1;  //   and in the finish pass
     uint32_t part_sub = 0;  // partitioned K1: swipes per sub-batch (0: default)
     int hll_mode = 0;       // partitioned K1's PFADD: 1 owned register lines, 0 CAS
-    int pb_pairs = 1;       // partitioned K1 pass B over slice pairs (one-link chains)
+    int pb_pairs = 2;       // partitioned K1 pass B: 2 slice pairs + fail lists, 1 + fail bytes, 0 slices
     int pa_tile = 10;       // partitioned K1 tile: 10 = 1024 swipes, 11 = 2048 (one-link k = 11 only)
     int pa_pre = 0;         // partitioned K1: pass A pre-checks the registers (measured slower: A +0.20, C -0.04 ms)
     int pa_grid = 0;        // partitioned K1 pass A blocks per CU (one-link k = 11; 0 = 2)
@@ -863,8 +863,9 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
         c->pa_grid = int(value);
         return SKE_OK;
     }
-    if (!strcmp(name, "pb_pairs")) {  // partitioned K1: pass B over slice pairs (1) or slices
-        if (value < 0 || value > 1) return SKE_EINVAL;
+    if (!strcmp(name, "pb_pairs")) {  // partitioned K1 pass B: 0 slices, 1 slice pairs + fail bytes,
+                                      // 2 slice pairs + fail lists (sketch_part.hip k_part_c_fl)
+        if (value < 0 || value > 2) return SKE_EINVAL;
         c->pb_pairs = int(value);
         return SKE_OK;
     }

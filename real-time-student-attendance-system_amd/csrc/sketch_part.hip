@@ -74,6 +74,8 @@ struct PartArgs {
     uint32_t *oldw;        // [n] pre: the register's aligned word as pass A read it (pass C's CAS expectation)
     uint32_t fixed_w, n, stride, ntiles, nslices, nlinks, ksum, nslots, fail_stride, off_stride;
     uint32_t pre;          // pass A pre-checks the register (k_part_a2, CAS pass C only)
+    uint16_t *flist;       // [nunits][fl_stride][kPbLanes] fail lists (pass B -> pass C), or nullptr
+    uint32_t nunits, fl_stride;
     uint32_t tile_log;     // swipes per tile = 1 << tile_log (10, or 11 for k_part_a2<11, 1024>)
     PartLink link[kPMaxLinks];
 };
@@ -483,7 +485,18 @@ constexpr uint32_t kOOR = 0x80000000u;  // a buffer offset past every range: loa
 // tested.
 constexpr uint32_t kPbQueue = 64;  // compacted fail stores per wave and group
 
-template <int SP, int R = 2 * SP>  // R: 16-byte pieces per lane and run (runs of SP slices)
+// Fail lists (FL, one-link chains in slice pairs, 1024-swipe tiles): instead
+// of one byte store per failing probe -- gfx950's L2 passes every store on to
+// memory, so 8.8 M scattered byte stores per C3 step were 8.8 M partial-line
+// fabric writes (WRITE_SIZE 251 MB for a 16 MB fail array, PMC r02) -- the
+// failing swipes of each (slice unit, tile) go to a fixed list of kPbLanes
+// u16 swipe indices, flist[unit][tile][], 0xffff = none.  A wave's round
+// covers kPbGroup consecutive tiles of one unit, so its lists are one
+// 128-byte span, written by one 2-byte-per-lane store instruction.  The
+// failures past a list's kPbLanes entries (Poisson(3.7) at C3: ~2 % of the
+// lists overflow) and those of the rare long runs keep the byte store; pass C
+// (k_part_c_fl) folds the lists of a tile into LDS flags.
+template <int SP, int R = 2 * SP, bool FL = false>  // R: 16-byte pieces per lane and run (runs of SP slices)
 __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const PartArgs A) {
     const uint32_t tmask = (1u << A.tile_log) - 1;
     __shared__ __attribute__((aligned(16))) uint8_t img[kPSliceBytes * SP];
@@ -501,11 +514,12 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
     constexpr uint32_t kWaves = kPbBlock / 64, kStep = kWaves * kPbGroup;
     const __amdgpu_buffer_rsrc_t rrec = part_rsrc(A.rec, A.ntiles * A.stride * 4);
     const __amdgpu_buffer_rsrc_t roff = part_rsrc(A.off, (A.nslices + 1) * A.off_stride * 4);
+    const __amdgpu_buffer_rsrc_t rfl = part_rsrc(A.flist, FL ? A.nunits * A.fl_stride * kPbLanes * 2 : 0);
     uint32_t *q = fq[wave];
     while (w < wend) {
         // slices g .. g + SP - 1 (SP = 2: one link only, host-checked), so
         // one run per tile covers them all
-        const uint32_t g = (w / gn) * SP, ta = gt0 + w % gn;
+        const uint32_t unit = w / gn, g = unit * SP, ta = gt0 + w % gn;
         const uint32_t tb = gt1 - ta < wend - w ? gt1 : ta + (wend - w);
         const uint32_t ge = g + SP < A.nslices ? g + SP : A.nslices;
         w += tb - ta;
@@ -590,22 +604,11 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                 okm |= __builtin_amdgcn_ubfe(img32[o >> 5], rr & 31, 1) << j;
             }
             uint32_t fm = vm & ~okm;
-            // compact the failing swipes of the wave: this lane's count, the
-            // wave's exclusive prefix, one store instruction per 64 of them
             const uint32_t tbase = (tg + k) << A.tile_log;
             const uint32_t cnt = __builtin_popcount(fm);
-            uint32_t incl = cnt;
-#pragma unroll
-            for (uint32_t o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += y;
-            }
-            const uint32_t nq = __shfl(incl, 63, 64);
-            uint32_t pos = incl - cnt;
-            while (fm) {
-                // record ctz(fm) by a select tree on its index bits (no compare chain)
-                const uint32_t j = __builtin_ctz(fm);
-                fm &= fm - 1;
+            // the record a lane's next failing probe sits in, by a select
+            // tree on its index bits (no compare chain)
+            auto pick = [&](uint32_t j) {
                 constexpr uint32_t kNR = 4 * R, kL = kNR <= 8 ? 3 : (kNR <= 16 ? 4 : 5);
                 uint32_t tt[1u << kL];
 #pragma unroll
@@ -616,18 +619,60 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
 #pragma unroll
                     for (uint32_t i = 0; i < ((1u << kL) >> (l + 1)); i++) tt[i] = bit ? tt[2 * i + 1] : tt[2 * i];
                 }
-                const uint32_t rr = tt[0];
-                const uint32_t at = tbase + ((rr >> kPSliceLog) & tmask);
-                if (pos < kPbQueue) q[pos] = at;
-                else __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail, at, 0, 0);  // overflow
-                pos++;
+                return tt[0];
+            };
+            if constexpr (FL) {
+                // this tile's failures (its kPbLanes lanes): positions by a
+                // segment prefix; the first kPbLanes go to the tile's list
+                uint32_t incl = cnt;
+#pragma unroll
+                for (uint32_t o = 1; o < kPbLanes; o <<= 1) {
+                    const uint32_t y = __shfl_up(incl, o, 64);
+                    if (qq >= o) incl += y;
+                }
+                const uint32_t tot = __shfl(incl, k * kPbLanes + kPbLanes - 1, 64);
+                uint32_t pos = incl - cnt;
+                while (fm) {
+                    const uint32_t j = __builtin_ctz(fm);
+                    fm &= fm - 1;
+                    const uint32_t at = (pick(j) >> kPSliceLog) & tmask;
+                    if (pos < kPbLanes) q[k * kPbLanes + pos] = at;
+                    else __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail, tbase + at, 0, 0);  // overflow
+                    pos++;
+                }
+                __builtin_amdgcn_wave_barrier();
+                // lane (k, qq) writes entry qq of tile tg + k's list (tiles past
+                // this block's range belong to another wave: not written)
+                const uint32_t v = qq < tot ? q[lane] : 0xffffu;
+                const uint32_t fo = ((unit * A.fl_stride + tg + k) * kPbLanes + qq) * 2;
+                __builtin_amdgcn_raw_buffer_store_b16(uint16_t(v), rfl, tg + k < tb ? fo : kOOR, 0, 0);
+                __builtin_amdgcn_wave_barrier();
+            } else {
+                // compact the failing swipes of the wave: this lane's count, the
+                // wave's exclusive prefix, one store instruction per 64 of them
+                uint32_t incl = cnt;
+#pragma unroll
+                for (uint32_t o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += y;
+                }
+                const uint32_t nq = __shfl(incl, 63, 64);
+                uint32_t pos = incl - cnt;
+                while (fm) {
+                    const uint32_t j = __builtin_ctz(fm);
+                    fm &= fm - 1;
+                    const uint32_t at = tbase + ((pick(j) >> kPSliceLog) & tmask);
+                    if (pos < kPbQueue) q[pos] = at;
+                    else __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail, at, 0, 0);  // overflow
+                    pos++;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (nq) {
+                    const uint32_t at = q[lane];
+                    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail, lane < nq ? at : kOOR, 0, 0);
+                }
+                __builtin_amdgcn_wave_barrier();
             }
-            __builtin_amdgcn_wave_barrier();
-            if (nq) {
-                const uint32_t at = q[lane];
-                __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail, lane < nq ? at : kOOR, 0, 0);
-            }
-            __builtin_amdgcn_wave_barrier();
             if (ec - s0 > 32 * R) {  // rare: a long run
                 const uint32_t base = (tg + k) * A.stride;
                 for (uint32_t i = s0 + 32 * R + qq; i < ec; i += kPbLanes) {
@@ -718,6 +763,83 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
             for (int u = 0; u < U; u++) {
                 const uint64_t i = base + uint64_t(u) * T + tid;
                 if (i < end) nt_st<16>(A.out + i, uint8_t(valid[u]));
+            }
+        }
+    }
+}
+
+// Pass C over pass B's fail lists (one-link chains, 1024-swipe tiles): a
+// block takes whole tiles of its XCD group; per tile it loads every slice
+// unit's list (16 B each) while the tile's fail bytes (list overflows), slots
+// and HLL words stream in, marks the listed swipes in LDS, and after one
+// barrier runs k_part_c's per-swipe answer and register max.  The LDS marks
+// carry the tile's index (double-buffered by tile parity), so nothing is ever
+// cleared: a mark from another tile never matches.
+template <int U>
+__global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
+    static_assert(kPcBlock * U == 1024, "one 1024-swipe tile per block iteration");
+    __shared__ uint16_t mark[2][1024];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t j = tid; j < 2 * 1024; j += kPcBlock) (&mark[0][0])[j] = 0;
+    __syncthreads();
+    uint32_t gt0, gt1;
+    part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
+    const uint32_t nblk = gridDim.x / kPGroups;
+    const __amdgpu_buffer_rsrc_t rfl = part_rsrc(A.flist, A.nunits * A.fl_stride * kPbLanes * 2);
+    uint32_t par = 0;
+    for (uint32_t t = gt0 + blockIdx.x / kPGroups; t < gt1; t += nblk, par ^= 1) {
+        uint16_t *mk = mark[par];
+        const uint16_t ep = uint16_t(t + 1);  // t < 2^16 - 1: sub-batches hold <= 16384 tiles
+        bool act[U];
+        uint32_t fb[U], sl[U], hv[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
+            act[u] = i < A.n;
+            fb[u] = act[u] ? nt_ld<16>(A.fail + i) : 1u;
+            sl[u] = act[u] ? nt_ld<16>(A.slot + i) : 0u;
+            hv[u] = act[u] ? nt_ld<16>(A.hllw + i) : 0u;
+        }
+        for (uint32_t un = tid; un < A.nunits; un += kPcBlock) {
+            const part_u32x4 e = __builtin_bit_cast(part_u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                 rfl, (un * A.fl_stride + t) * kPbLanes * 2, 0, 0));
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const uint32_t lo = e[c] & 0xffffu, hi = e[c] >> 16;
+                if (lo != 0xffffu) mk[lo & 1023u] = ep;
+                if (hi != 0xffffu) mk[hi & 1023u] = ep;
+            }
+        }
+        __syncthreads();
+        bool valid[U];
+        uint32_t *w[U];
+        uint32_t rank[U], sh[U], cur[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            valid[u] = act[u] && fb[u] == 0 && mk[uint32_t(u) * kPcBlock + tid] != ep;
+            w[u] = nullptr;
+            rank[u] = sh[u] = 0;
+            if (valid[u]) {
+                if (sl[u] >= A.nslots) {
+                    atomicOr(A.err, 1u);
+                } else {
+                    const uint32_t ridx = hv[u] & 0xffffu;
+                    w[u] = reinterpret_cast<uint32_t *>(A.regs + (uint64_t(sl[u]) << kHllP) + (ridx & ~3u));
+                    sh[u] = (ridx & 3) * 8;
+                    rank[u] = hv[u] >> 16;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) cur[u] = w[u] ? nt_ld<32>(w[u]) : 0xffffffffu;
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (w[u]) part_reg_max(w[u], sh[u], rank[u], cur[u]);
+        if (A.out) {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
+                if (act[u]) nt_st<16>(A.out + i, uint8_t(valid[u]));
             }
         }
     }
@@ -1232,6 +1354,11 @@ static hipError_t part_scratch(PartArgs *A, uint64_t n, uint32_t sub, Scratch *s
     if (e == hipSuccess) A->hllw = (uint32_t *)scratch_get(scr, 31, size_t(m) * 4, &e);
     if (e == hipSuccess) A->oldw = (uint32_t *)scratch_get(scr, 42, size_t(m) * 4, &e);
     A->fail_stride = fstride;
+    // pass B -> C fail lists of slice pairs (one-link chains)
+    A->nunits = (A->nslices + 1) / 2;
+    A->fl_stride = A->off_stride;
+    if (e == hipSuccess && A->nlinks == 1)
+        A->flist = (uint16_t *)scratch_get(scr, 44, size_t(A->nunits) * A->fl_stride * kPbLanes * 2, &e);
     if (e == hipSuccess) {
         HllArgs H{};
         e = hll_scratch(&H, m, scr);
@@ -1313,6 +1440,11 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
     // (VALU / LDS bound, its memory path has room), so pass C touches only the
     // registers that rise (k_part_a2 of 1024-swipe tiles, CAS PFADD)
     A.pre = (pre_opt && hll_mode == 0 && one11 && A.tile_log == 10) ? 1u : 0u;
+    // pass B -> C through fail lists (pb_pairs 2): one-link chains probed in
+    // slice pairs over 1024-swipe tiles, PFADD by CAS from pass C's own
+    // pre-check, passes in stream order (the lists are one buffer)
+    const bool flist = pb_pairs == 2 && A.nlinks == 1 && A.tile_log == 10 && hll_mode == 0 && !A.pre && !side &&
+                       A.flist != nullptr;
     const uint32_t tile = 1u << A.tile_log;
 #define SKE_CK(x)                        \
     do {                                 \
@@ -1337,6 +1469,9 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             hipLaunchKernelGGL(k_part_hscan, dim3(kH1), dim3(1024), 0, sc, H);
             hipLaunchKernelGGL(k_part_hd, dim3(unsigned(cus) * 2), dim3(1024), 0, sc, H);
             hipLaunchKernelGGL(k_part_he, dim3(unsigned(cus) * 2), dim3(kHeBlock), 0, sc, P, H);
+        } else if (flist) {
+            const unsigned gc = (part_grid(ms, 1024, cus * 8) + kPGroups - 1) / kPGroups * kPGroups;
+            hipLaunchKernelGGL(k_part_c_fl<4>, dim3(gc), dim3(kPcBlock), 0, sc, P);
         } else {
             const unsigned gc = (part_grid(ms, kPcBlock * 2, cus * 8) + kPGroups - 1) / kPGroups * kPGroups;
             hipLaunchKernelGGL(k_part_c<2>, dim3(gc), dim3(kPcBlock), 0, sc, P);
@@ -1399,6 +1534,8 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             if (hook) hook(hook_user, 1, 0, st);
             if (pairs && A.tile_log == 11)  // runs of ~148 records
                 hipLaunchKernelGGL((k_part_b<2, 6>), dim3(gb), dim3(kPbBlock), 0, st, A);
+            else if (flist)
+                hipLaunchKernelGGL((k_part_b<2, 4, true>), dim3(gb), dim3(kPbBlock), 0, st, A);
             else if (pairs)
                 hipLaunchKernelGGL(k_part_b<2>, dim3(gb), dim3(kPbBlock), 0, st, A);
             else

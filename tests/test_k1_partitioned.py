@@ -162,6 +162,39 @@ def test_graph_replay_then_direct_launch_other_stream(engine, orc):
     assert np.array_equal(engine.registers_all(w.n_keys), regs)
 
 
+@pytest.mark.parametrize("invalid", [0.1, 0.5, 1.0])
+@pytest.mark.parametrize("pb_mode", [2, 1])
+def test_fail_lists_and_overflow_vs_oracle(engine, orc, invalid, pb_mode):
+    """Pass B -> C through fail lists (pb_pairs 2, the default) or fail bytes
+    (1) on the C3 filter: at 100 % invalid every (slice pair, tile) list
+    overflows into the fail bytes many times over, at 10 % a few do; a
+    ragged last tile; answers and registers == the oracle."""
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import DeviceBuffer
+    w = synthetic.WORKLOADS["c3"]
+    w = synthetic.Workload(**{**w.__dict__, "n_members": 300_000, "n_keys": 97, "zipf_lectures": 0,
+                              "zipf_days": 0, "invalid_frac": invalid})
+    engine.set_option("pb_pairs", pb_mode)
+    engine.reserve(0, w.bf_error, w.bf_capacity)
+    p = engine.gen_params(w, seed=4242)
+    engine.preload(0, p, w.n_members)
+    engine.hll_reserve(w.n_keys)
+    assert engine.variant(0) == 3
+    b = engine.swipe_batch(p, 7, 700_000 + 333)
+    out = DeviceBuffer(engine.ctx, b.n)
+    engine.swipes(0, b, out)
+    chain = orc.Chain(w.bf_capacity, w.bf_error)
+    mb = engine.members_batch(p, 0, w.n_members).to_host()
+    chain.madd_packed(mb[0], mb[1])
+    regs = np.zeros((w.n_keys, 16384), np.uint8)
+    buf, offs, slot = b.to_host()
+    v, nvalid, _ = orc.process_swipes(chain, regs, slot.astype(np.uint32), buf, offs)
+    assert np.array_equal(out.to_host(np.uint8, b.n), v)
+    assert np.array_equal(engine.registers_all(w.n_keys), regs)
+    if invalid == 1.0:
+        assert nvalid < b.n // 500   # only Bloom false positives remain
+
+
 def test_hll_reserve_refused_while_graph_alive(engine):
     from rtsas_amd._lib import SketchLibError, SKE_EBUSY
     from rtsas_amd.engine import DeviceBuffer
