@@ -166,6 +166,7 @@ class ShardedSketch:
         self.ops = ops if ops is not None else LibsketchOps(client)
         backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
         self.use_reduce_scatter = backend == "nccl"
+        self.solo = world == 1  # one shard (no process group needed): collectives are identities
 
     def _owned(self, keys: Sequence) -> np.ndarray:
         keys = list(keys)
@@ -182,6 +183,8 @@ class ShardedSketch:
     def _all_reduce(self, t, op):
         """RCCL reduces device tensors in place; gloo (CPU tests, or ranks
         rehearsed on one GPU) gets a host copy of a device tensor."""
+        if self.solo:
+            return t
         if self.use_reduce_scatter or t.device.type == "cpu":
             self.dist.all_reduce(t, op=op, group=self.group)
             return t
@@ -204,6 +207,8 @@ class ShardedSketch:
         counts = np.zeros(len(keys), np.int64)
         if idx.size:
             counts[idx] = self.ops.count_each([keys[i] for i in idx]).astype(np.int64)
+        if self.solo:
+            return counts.astype(np.uint64)
         t = torch.from_numpy(counts)
         if self.use_reduce_scatter:
             t = t.to(self.ops.device)
@@ -219,6 +224,8 @@ class ShardedSketch:
         m = iter(self._owned(flat).tolist())
         padded = [[k for k in g if next(m)] for g in groups] + [[]] * (per * self.world - G)
         t = self.ops.merge_groups(padded)
+        if self.solo:
+            return self.ops.count_raw(t)[:G].astype(np.uint64)
         if self.use_reduce_scatter:
             mine = torch.empty((per, HLL_REGISTERS), dtype=t.dtype, device=t.device)
             self.dist.reduce_scatter_tensor(mine, t, op=self._max(), group=self.group)

@@ -118,3 +118,33 @@ def test_routing_is_a_function_of_the_key(pkg):
     assert r[1000:].tolist() == r[:10].tolist()
     counts = np.bincount(r[:1000], minlength=8)
     assert counts.min() > 80          # balanced shards
+
+
+def test_one_shard_needs_no_process_group(orc):
+    """world == 1 (one GPU, no torch.distributed group): the collectives are
+    identities and the queries equal the oracle's."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as ge
+    ge.load_package()
+    from rtsas_amd.distributed import ShardedSketch
+    assert not dist.is_initialized()
+    keys, elems, groups = _dataset()
+    store = {}
+    for k in keys:
+        h = orc.HLL()
+        h.add(*elems[k])
+        store[k] = h
+    sh = ShardedSketch(None, 0, 1, ops=OracleOps(orc, store))
+    u = orc.HLL()
+    for h in store.values():
+        u.merge(h)
+    assert sh.pfcount_union(keys) == u.count()
+    assert sh.pfcount_each(keys).tolist() == [store[k].count() for k in keys]
+    want = []
+    for g in groups:
+        m = orc.HLL()
+        for k in g:
+            m.merge(store[k])
+        want.append(m.count())
+    assert sh.rollup(groups).tolist() == want
