@@ -457,6 +457,149 @@ __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part
     }
 }
 
+// Pass A of the fail-list path (one link, k = KM, slice pairs, 1024-swipe
+// tiles, 512 threads x 2 swipes): the same hashing, probes and counting sort
+// as k_part_a2 with fewer instructions per probe record (VALU issue bounds
+// pass A: 93 M wave-instructions per C3 step, PMC r02):
+//   * records are (bit offset in the slice PAIR: 20 bits) | swipe << 20,
+//     one v_and_or per probe (pass B of the pair reads the offset as is);
+//   * a counter counts in 4s from a bias of (its LDS word index) << 18, so an
+//     atomic's return value >> 16 is its own byte offset in the counter
+//     array; after the scan the counter holds 4 * start - bias, so a
+//     record's byte offset in the tile's LDS record array is the atomic's
+//     return value plus that word: one shift and one add per record;
+//   * full tiles take a probe loop without the past-the-batch select.
+// Counters of the two tile parities are one array (bias index par*2048 + g).
+template <int KM>
+__global__ void __launch_bounds__(512, 2) k_part_a3(const PartArgs A) {
+    constexpr uint32_t kT = 512, kU = 2, kTile = 1024;
+    constexpr uint32_t kCnt = kPMaxSlices + 1;  // counters per tile parity
+    constexpr int kPer = kCnt / kT;
+    static_assert(kCnt % kT == 0 && 4u * kTile * KM < 65536u, "a rank * 4 stays below bit 16");
+    __shared__ __attribute__((aligned(16))) uint32_t srec[kTile * KM];
+    __shared__ uint32_t cnt[2 * kCnt];
+    __shared__ uint32_t swsum[kT / 64];
+    __shared__ uint32_t stot;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t S = A.nslices;
+    for (uint32_t c = tid; c < 2 * kCnt; c += kT) cnt[c] = c << 18;
+    __syncthreads();
+    auto offsets = [&](uint32_t t, uint32_t u, uint32_t &b, uint32_t &e) {
+        const uint32_t i = t * kTile + u * kT + tid;
+        const uint32_t ic = i < A.n ? i : A.n - 1;
+        b = A.offs ? nt_ld<2>(A.offs + ic) : ic * A.fixed_w;
+        e = A.offs ? nt_ld<2>(A.offs + ic + 1) : b + A.fixed_w;
+    };
+    uint32_t gt0, gt1;
+    part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
+    const uint32_t tstep = gridDim.x / kPGroups;
+    const __amdgpu_buffer_rsrc_t rbytes = part_rsrc(A.bytes, 0xfffffff0u);
+    const PartLink &L = A.link[0];
+    uint32_t par = 0, nb_[kU], ne_[kU];
+    PartId it[kU];
+    {
+        const uint32_t t = gt0 + blockIdx.x / kPGroups;
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            offsets(t < gt1 ? t : gt0, u, nb_[u], ne_[u]);
+            part_id_load(rbytes, nb_[u], ne_[u], it[u]);
+        }
+    }
+    const uint8_t *cntb = reinterpret_cast<const uint8_t *>(cnt);
+    uint8_t *srecb = reinterpret_cast<uint8_t *>(srec);
+    for (uint32_t t = gt0 + blockIdx.x / kPGroups; t < gt1; t += tstep, par ^= 1) {
+        const uint32_t cb = par * kCnt;
+        uint32_t *cp = cnt + cb;
+        uint32_t rv[kU][KM], rp[kU][KM];
+        const uint32_t tn = t + tstep < gt1 ? t + tstep : t;
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) offsets(tn, u, nb_[u], ne_[u]);
+        const bool full = (t + 1) * kTile <= A.n;  // block-uniform
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t lu = u * kT + tid;
+            const uint32_t i = t * kTile + lu;
+            const bool act = i < A.n;
+            uint64_t ha, hb, hh;
+            part_hash3(A.bytes, it[u], ha, hb, hh);
+            if (act) {
+                uint32_t idx, rank;
+                hll_patlen(hh, idx, rank);
+                nt_st<8>(A.hllw + i, idx | (rank << 16));
+                nt_st<8>(A.fail + i, uint8_t(0));
+            }
+            const uint32_t lu20 = lu << 20;
+            ProbeWalk32 wk;
+            wk.init(ha, hb, part_div(L));
+            if (full) {
+#pragma unroll
+                for (int q = 0; q < KM; q++) {
+                    const uint32_t x = wk.x;
+                    rv[u][q] = (x & 0xfffffu) | lu20;
+                    rp[u][q] = atomicAdd(&cp[__builtin_amdgcn_ubfe(x, kPSliceLog, 12)], 4u);
+                    if (q + 1 < KM) wk.step(L.d);
+                }
+            } else {
+                // a lane past the batch counts into slice S, left out of the
+                // scan: its records land past the tile's total, never copied
+#pragma unroll
+                for (int q = 0; q < KM; q++) {
+                    const uint32_t x = wk.x;
+                    rv[u][q] = (x & 0xfffffu) | lu20;
+                    rp[u][q] = atomicAdd(&cp[act ? __builtin_amdgcn_ubfe(x, kPSliceLog, 12) : S], 4u);
+                    if (q + 1 < KM) wk.step(L.d);
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this swipe's atomics, once
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) part_id_load(rbytes, nb_[u], ne_[u], it[u]);  // the next tile's ids
+        // exclusive scan of the counts of slices 0..S
+        uint32_t v[kPer], s = 0;
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+            const uint32_t c = cb + tid * kPer + j;
+            v[j] = (cnt[c] - (c << 18)) >> 2;
+            s += v[j];
+        }
+        uint32_t incl = s;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= uint32_t(o)) incl += y;
+        }
+        if (lane == 63) swsum[wave] = incl;
+        __syncthreads();
+        uint32_t run = incl - s;
+        for (uint32_t w = 0; w < wave; w++) run += swsum[w];
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+            const uint32_t g = tid * kPer + j, c = cb + g;
+            if (g <= S) A.off[size_t(g) * A.off_stride + t] = run;  // run starts (pass B)
+            if (g == S) stot = run;
+            cnt[c] = 4 * run - (c << 18);
+            run += v[j];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++)
+#pragma unroll
+            for (int q = 0; q < KM; q++) {
+                const uint32_t r = rp[u][q];
+                *reinterpret_cast<uint32_t *>(srecb + (r + *reinterpret_cast<const uint32_t *>(cntb + (r >> 16)))) =
+                    rv[u][q];
+            }
+        const uint32_t nb = (cb ^ kCnt);
+        for (uint32_t g = tid; g <= S; g += kT) cnt[nb + g] = (nb + g) << 18;
+        __syncthreads();
+        const uint32_t total = stot;
+        part_u32x4 *dst = reinterpret_cast<part_u32x4 *>(A.rec + size_t(t) * A.stride);
+        const part_u32x4 *src = reinterpret_cast<const part_u32x4 *>(srec);
+        for (uint32_t j = tid; j * 4 < total; j += kT) nt_st<4>(dst + j, src[j]);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // pass B: LDS-resident slices, probe their runs
 // ---------------------------------------------------------------------------
@@ -600,7 +743,9 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
 #pragma unroll
             for (uint32_t j = 0; j < 4 * R; j++) {
                 const uint32_t rr = rec[j];
-                const uint32_t o = SP == 1 ? (rr & kPSliceMask) : ((rr & kPSliceMask) | ((rr >> A.tile_log) & kPSliceBits));
+                const uint32_t o = FL ? (rr & 0xfffffu)  // k_part_a3: the offset in the pair
+                                      : SP == 1 ? (rr & kPSliceMask)
+                                                : ((rr & kPSliceMask) | ((rr >> A.tile_log) & kPSliceBits));
                 okm |= __builtin_amdgcn_ubfe(img32[o >> 5], rr & 31, 1) << j;
             }
             uint32_t fm = vm & ~okm;
@@ -635,7 +780,7 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                 while (fm) {
                     const uint32_t j = __builtin_ctz(fm);
                     fm &= fm - 1;
-                    const uint32_t at = (pick(j) >> kPSliceLog) & tmask;
+                    const uint32_t at = (pick(j) >> 20) & tmask;  // k_part_a3's swipe field
                     if (pos < kPbLanes) q[k * kPbLanes + pos] = at;
                     else __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail, tbase + at, 0, 0);  // overflow
                     pos++;
@@ -677,10 +822,12 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                 const uint32_t base = (tg + k) * A.stride;
                 for (uint32_t i = s0 + 32 * R + qq; i < ec; i += kPbLanes) {
                     const uint32_t rr = __builtin_amdgcn_raw_buffer_load_b32(rrec, (base + i) * 4, 0, 0);
-                    const uint32_t o = SP == 1 ? (rr & kPSliceMask) : ((rr & kPSliceMask) | ((rr >> A.tile_log) & kPSliceBits));
+                    const uint32_t o = FL ? (rr & 0xfffffu)
+                                          : SP == 1 ? (rr & kPSliceMask)
+                                                    : ((rr & kPSliceMask) | ((rr >> A.tile_log) & kPSliceBits));
                     if (!((img[o >> 3] >> (o & 7)) & 1))
                         __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail,
-                                                             tbase + ((rr >> kPSliceLog) & tmask), 0, 0);
+                                                             tbase + ((rr >> (FL ? 20 : kPSliceLog)) & tmask), 0, 0);
                 }
             }
 #pragma unroll
@@ -778,70 +925,93 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
 template <int U>
 __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
     static_assert(kPcBlock * U == 1024, "one 1024-swipe tile per block iteration");
+    constexpr uint32_t kFlPer = 4;  // lists per thread: nunits <= 1024 (kPMaxSlices / 2)
     __shared__ uint16_t mark[2][1024];
     const uint32_t tid = threadIdx.x;
     for (uint32_t j = tid; j < 2 * 1024; j += kPcBlock) (&mark[0][0])[j] = 0;
-    __syncthreads();
     uint32_t gt0, gt1;
     part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
     const uint32_t nblk = gridDim.x / kPGroups;
     const __amdgpu_buffer_rsrc_t rfl = part_rsrc(A.flist, A.nunits * A.fl_stride * kPbLanes * 2);
-    uint32_t par = 0;
-    for (uint32_t t = gt0 + blockIdx.x / kPGroups; t < gt1; t += nblk, par ^= 1) {
-        uint16_t *mk = mark[par];
-        const uint16_t ep = uint16_t(t + 1);  // t < 2^16 - 1: sub-batches hold <= 16384 tiles
-        bool act[U];
+    // a tile's inputs: its fail lists (one 16-B list per slice unit) and its
+    // swipes' fail bytes, slots and HLL words; the next tile's are loaded
+    // while this tile's registers are raised
+    struct In {
+        part_u32x4 e[kFlPer];
         uint32_t fb[U], sl[U], hv[U];
+    };
+    auto load = [&](uint32_t t, In &in) {
+        const bool live = t < gt1;
+#pragma unroll
+        for (uint32_t j = 0; j < kFlPer; j++) {
+            const uint32_t un = tid + j * kPcBlock;
+            const bool ok = live && un < A.nunits;
+            in.e[j] = __builtin_bit_cast(part_u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                        rfl, ok ? (un * A.fl_stride + t) * kPbLanes * 2 : kOOR, 0, 0));
+        }
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
-            act[u] = i < A.n;
-            fb[u] = act[u] ? nt_ld<16>(A.fail + i) : 1u;
-            sl[u] = act[u] ? nt_ld<16>(A.slot + i) : 0u;
-            hv[u] = act[u] ? nt_ld<16>(A.hllw + i) : 0u;
+            const bool act = live && i < A.n;
+            in.fb[u] = act ? nt_ld<16>(A.fail + i) : 1u;
+            in.sl[u] = act ? nt_ld<16>(A.slot + i) : 0u;
+            in.hv[u] = act ? nt_ld<16>(A.hllw + i) : 0u;
         }
-        for (uint32_t un = tid; un < A.nunits; un += kPcBlock) {
-            const part_u32x4 e = __builtin_bit_cast(part_u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                 rfl, (un * A.fl_stride + t) * kPbLanes * 2, 0, 0));
+    };
+    __syncthreads();
+    uint32_t par = 0;
+    uint32_t t = gt0 + blockIdx.x / kPGroups;
+    In cur;
+    load(t, cur);
+    for (; t < gt1; t += nblk, par ^= 1) {
+        uint16_t *mk = mark[par];
+        const uint16_t ep = uint16_t(t + 1);  // t < 2^16 - 1: sub-batches hold <= 16384 tiles
 #pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const uint32_t lo = e[c] & 0xffffu, hi = e[c] >> 16;
-                if (lo != 0xffffu) mk[lo & 1023u] = ep;
-                if (hi != 0xffffu) mk[hi & 1023u] = ep;
+        for (uint32_t j = 0; j < kFlPer; j++) {
+#pragma unroll
+            for (int c = 0; c < 4; c++) {  // a list past nunits loaded as zeros: entry 0 ...
+                const uint32_t lo = cur.e[j][c] & 0xffffu, hi = cur.e[j][c] >> 16;
+                const bool ok = tid + j * kPcBlock < A.nunits;  // ... so only real lists mark
+                if (ok && lo != 0xffffu) mk[lo & 1023u] = ep;
+                if (ok && hi != 0xffffu) mk[hi & 1023u] = ep;
             }
         }
+        In nxt;
+        load(t + nblk, nxt);
         __syncthreads();
         bool valid[U];
         uint32_t *w[U];
-        uint32_t rank[U], sh[U], cur[U];
+        uint32_t rank[U], sh[U], cur_w[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            valid[u] = act[u] && fb[u] == 0 && mk[uint32_t(u) * kPcBlock + tid] != ep;
+            const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
+            valid[u] = i < A.n && cur.fb[u] == 0 && mk[uint32_t(u) * kPcBlock + tid] != ep;
             w[u] = nullptr;
             rank[u] = sh[u] = 0;
             if (valid[u]) {
-                if (sl[u] >= A.nslots) {
+                if (cur.sl[u] >= A.nslots) {
                     atomicOr(A.err, 1u);
                 } else {
-                    const uint32_t ridx = hv[u] & 0xffffu;
-                    w[u] = reinterpret_cast<uint32_t *>(A.regs + (uint64_t(sl[u]) << kHllP) + (ridx & ~3u));
+                    const uint32_t ridx = cur.hv[u] & 0xffffu;
+                    w[u] = reinterpret_cast<uint32_t *>(A.regs + (uint64_t(cur.sl[u]) << kHllP) + (ridx & ~3u));
                     sh[u] = (ridx & 3) * 8;
-                    rank[u] = hv[u] >> 16;
+                    rank[u] = cur.hv[u] >> 16;
                 }
             }
         }
 #pragma unroll
-        for (int u = 0; u < U; u++) cur[u] = w[u] ? nt_ld<32>(w[u]) : 0xffffffffu;
+        for (int u = 0; u < U; u++) cur_w[u] = w[u] ? nt_ld<32>(w[u]) : 0xffffffffu;
 #pragma unroll
         for (int u = 0; u < U; u++)
-            if (w[u]) part_reg_max(w[u], sh[u], rank[u], cur[u]);
+            if (w[u]) part_reg_max(w[u], sh[u], rank[u], cur_w[u]);
         if (A.out) {
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
-                if (act[u]) nt_st<16>(A.out + i, uint8_t(valid[u]));
+                if (i < A.n) nt_st<16>(A.out + i, uint8_t(valid[u]));
             }
         }
+        cur = nxt;
     }
 }
 
@@ -1443,7 +1613,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
     // pass B -> C through fail lists (pb_pairs 2): one-link chains probed in
     // slice pairs over 1024-swipe tiles, PFADD by CAS from pass C's own
     // pre-check, passes in stream order (the lists are one buffer)
-    const bool flist = pb_pairs == 2 && A.nlinks == 1 && A.tile_log == 10 && hll_mode == 0 && !A.pre && !side &&
+    const bool flist = pb_pairs == 2 && one11 && A.tile_log == 10 && hll_mode == 0 && !A.pre && !side &&
                        A.flist != nullptr;
     const uint32_t tile = 1u << A.tile_log;
 #define SKE_CK(x)                        \
@@ -1506,7 +1676,9 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             const unsigned per_cu = km <= 11 ? (a_grid ? unsigned(a_grid) : 2u) : 1;
             const unsigned ga = unsigned(cus) * per_cu / kPGroups * kPGroups;  // blocks past a group's tiles exit
             if (hook) hook(hook_user, 0, 0, st);
-            if (one11 && A.tile_log == 11)  // RESERVE 0.001 (C3/C5): one link, k = 11
+            if (flist)  // the fail-list path's own record format (k_part_a3 -> k_part_b<2, 4, true>)
+                hipLaunchKernelGGL(k_part_a3<11>, dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(512), 0, st, A);
+            else if (one11 && A.tile_log == 11)  // RESERVE 0.001 (C3/C5): one link, k = 11
                 hipLaunchKernelGGL((k_part_a2<11, 1024>), dim3(unsigned(cus) / kPGroups * kPGroups), dim3(1024),
                                    0, st, A);
             else if (one11 && A.pre)
