@@ -82,6 +82,14 @@ struct PartArgs {
 
 __device__ __forceinline__ Divisor part_div(const PartLink &L) { return Divisor{L.d, L.m, L.t, L.sh, 0}; }
 
+// A workgroup barrier for hand-offs through LDS only: it waits for this
+// wave's LDS operations (lgkmcnt(0)) and not for its global loads and stores
+// in flight, which __syncthreads() drains too (vmcnt(0)).  The partitioned
+// passes share nothing through global memory inside a block, so the next
+// tile's prefetched ids (pass A), the next round's records (pass B) and the
+// register CASes (pass C) stay in flight across their barriers.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Tiles are dealt to kPGroups contiguous groups, and every pass gives the
 // blocks b with b % kPGroups == x the tiles of group x.  Blocks are dealt
 // round-robin over the 8 XCDs, so a group's fail bytes (2 MB at C3) are
@@ -483,7 +491,7 @@ __global__ void __launch_bounds__(512, 2) k_part_a3(const PartArgs A) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t S = A.nslices;
     for (uint32_t c = tid; c < 2 * kCnt; c += kT) cnt[c] = c << 18;
-    __syncthreads();
+    lds_barrier();
     auto offsets = [&](uint32_t t, uint32_t u, uint32_t &b, uint32_t &e) {
         const uint32_t i = t * kTile + u * kT + tid;
         const uint32_t ic = i < A.n ? i : A.n - 1;
@@ -552,7 +560,7 @@ __global__ void __launch_bounds__(512, 2) k_part_a3(const PartArgs A) {
             }
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this swipe's atomics, once
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++) part_id_load(rbytes, nb_[u], ne_[u], it[u]);  // the next tile's ids
         // exclusive scan of the counts of slices 0..S
@@ -570,7 +578,7 @@ __global__ void __launch_bounds__(512, 2) k_part_a3(const PartArgs A) {
             if (lane >= uint32_t(o)) incl += y;
         }
         if (lane == 63) swsum[wave] = incl;
-        __syncthreads();
+        lds_barrier();
         uint32_t run = incl - s;
         for (uint32_t w = 0; w < wave; w++) run += swsum[w];
 #pragma unroll
@@ -581,7 +589,7 @@ __global__ void __launch_bounds__(512, 2) k_part_a3(const PartArgs A) {
             cnt[c] = 4 * run - (c << 18);
             run += v[j];
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++)
 #pragma unroll
@@ -592,7 +600,7 @@ __global__ void __launch_bounds__(512, 2) k_part_a3(const PartArgs A) {
             }
         const uint32_t nb = (cb ^ kCnt);
         for (uint32_t g = tid; g <= S; g += kT) cnt[nb + g] = (nb + g) << 18;
-        __syncthreads();
+        lds_barrier();
         const uint32_t total = stot;
         part_u32x4 *dst = reinterpret_cast<part_u32x4 *>(A.rec + size_t(t) * A.stride);
         const part_u32x4 *src = reinterpret_cast<const part_u32x4 *>(srec);
@@ -671,10 +679,10 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
         const PartLink &L = A.link[l];
         const uint32_t b0 = (g - L.slice0) * kPSliceBytes;
         const uint32_t nb = L.nbytes16 - b0 < kPSliceBytes * SP ? L.nbytes16 - b0 : kPSliceBytes * SP;
-        __syncthreads();  // every wave is done with the previous slice
+        lds_barrier();  // every wave is done with the previous slice
         for (uint32_t o = threadIdx.x * 16; o < nb; o += kPbBlock * 16)
             *reinterpret_cast<uint4 *>(img + o) = *reinterpret_cast<const uint4 *>(L.bf + b0 + o);
-        __syncthreads();
+        lds_barrier();
         const __amdgpu_buffer_rsrc_t rfail = part_rsrc(A.fail + size_t(l) * A.fail_stride, A.fail_stride);
         const uint32_t orow = g * A.off_stride, erow = ge * A.off_stride;
         // run boundaries of 8 rounds at once: lane L holds those of tile
@@ -958,7 +966,7 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
             in.hv[u] = act ? nt_ld<16>(A.hllw + i) : 0u;
         }
     };
-    __syncthreads();
+    lds_barrier();
     uint32_t par = 0;
     uint32_t t = gt0 + blockIdx.x / kPGroups;
     In cur;
@@ -978,7 +986,7 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
         }
         In nxt;
         load(t + nblk, nxt);
-        __syncthreads();
+        lds_barrier();
         bool valid[U];
         uint32_t *w[U];
         uint32_t rank[U], sh[U], cur_w[U];
@@ -1001,9 +1009,18 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
         }
 #pragma unroll
         for (int u = 0; u < U; u++) cur_w[u] = w[u] ? nt_ld<32>(w[u]) : 0xffffffffu;
+        // every raising CAS of the tile in flight at once, then settled (a
+        // lost race retries from the word the CAS returned)
+        uint32_t seen[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            seen[u] = cur_w[u];
+            if (w[u] && ((cur_w[u] >> sh[u]) & 0xffu) < rank[u])
+                seen[u] = atomicCAS(w[u], cur_w[u], (cur_w[u] & ~(0xffu << sh[u])) | (rank[u] << sh[u]));
+        }
 #pragma unroll
         for (int u = 0; u < U; u++)
-            if (w[u]) part_reg_max(w[u], sh[u], rank[u], cur_w[u]);
+            if (w[u] && seen[u] != cur_w[u]) part_reg_max(w[u], sh[u], rank[u], seen[u]);
         if (A.out) {
 #pragma unroll
             for (int u = 0; u < U; u++) {
