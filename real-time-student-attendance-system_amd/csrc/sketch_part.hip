@@ -924,111 +924,115 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
 }
 
 // Pass C over pass B's fail lists (one-link chains, 1024-swipe tiles): a
-// block takes whole tiles of its XCD group; per tile it loads every slice
-// unit's list (16 B each) while the tile's fail bytes (list overflows), slots
-// and HLL words stream in, marks the listed swipes in LDS, and after one
-// barrier runs k_part_c's per-swipe answer and register max.  The LDS marks
-// carry the tile's index (double-buffered by tile parity), so nothing is ever
-// cleared: a mark from another tile never matches.
+// block takes runs of kPbGroup consecutive tiles of its XCD group (the span
+// one pass-B round writes, so a unit's lists for the run are one 128-byte
+// line, loaded by 8 lanes together), marks the listed swipes in LDS, and
+// after one barrier runs k_part_c's per-swipe answer and register max over
+// the run's tiles -- the next tile's fail bytes (list overflows), slots and
+// HLL words in flight while a tile's CASes are, every CAS of a tile issued
+// before any is settled.  Marks carry the run's index: nothing is cleared.
 template <int U>
 __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
-    static_assert(kPcBlock * U == 1024, "one 1024-swipe tile per block iteration");
-    constexpr uint32_t kFlPer = 4;  // lists per thread: nunits <= 1024 (kPMaxSlices / 2)
-    __shared__ uint16_t mark[2][1024];
+    static_assert(kPcBlock * U == 1024, "one 1024-swipe tile per sub-step");
+    constexpr uint32_t kRun = kPbGroup;  // tiles per block iteration
+    __shared__ uint16_t mark[kRun * 1024];
     const uint32_t tid = threadIdx.x;
-    for (uint32_t j = tid; j < 2 * 1024; j += kPcBlock) (&mark[0][0])[j] = 0;
+    for (uint32_t j = tid; j < kRun * 1024; j += kPcBlock) mark[j] = 0;
     uint32_t gt0, gt1;
     part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
     const uint32_t nblk = gridDim.x / kPGroups;
+    const uint32_t npieces = A.nunits * kRun;  // 16-B lists of one run
     const __amdgpu_buffer_rsrc_t rfl = part_rsrc(A.flist, A.nunits * A.fl_stride * kPbLanes * 2);
-    // a tile's inputs: its fail lists (one 16-B list per slice unit) and its
-    // swipes' fail bytes, slots and HLL words; the next tile's are loaded
-    // while this tile's registers are raised
     struct In {
-        part_u32x4 e[kFlPer];
         uint32_t fb[U], sl[U], hv[U];
     };
-    auto load = [&](uint32_t t, In &in) {
-        const bool live = t < gt1;
-#pragma unroll
-        for (uint32_t j = 0; j < kFlPer; j++) {
-            const uint32_t un = tid + j * kPcBlock;
-            const bool ok = live && un < A.nunits;
-            in.e[j] = __builtin_bit_cast(part_u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                        rfl, ok ? (un * A.fl_stride + t) * kPbLanes * 2 : kOOR, 0, 0));
-        }
+    auto load = [&](uint32_t t, uint32_t tend, In &in) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
-            const bool act = live && i < A.n;
+            const bool act = t < tend && i < A.n;
             in.fb[u] = act ? nt_ld<16>(A.fail + i) : 1u;
             in.sl[u] = act ? nt_ld<16>(A.slot + i) : 0u;
             in.hv[u] = act ? nt_ld<16>(A.hllw + i) : 0u;
         }
     };
     lds_barrier();
-    uint32_t par = 0;
-    uint32_t t = gt0 + blockIdx.x / kPGroups;
-    In cur;
-    load(t, cur);
-    for (; t < gt1; t += nblk, par ^= 1) {
-        uint16_t *mk = mark[par];
-        const uint16_t ep = uint16_t(t + 1);  // t < 2^16 - 1: sub-batches hold <= 16384 tiles
+    for (uint32_t r0 = gt0 + (blockIdx.x / kPGroups) * kRun; r0 < gt1; r0 += nblk * kRun) {
+        const uint32_t r1 = r0 + kRun < gt1 ? r0 + kRun : gt1;
+        const uint16_t ep = uint16_t(r0 / kRun + 1);  // < 2^16: sub-batches hold <= 16384 tiles
+        In cur;
+        load(r0, r1, cur);
+        // the run's lists: piece p = (unit p / kRun, tile r0 + p % kRun)
+        for (uint32_t p0 = 0; p0 < npieces; p0 += 4 * kPcBlock) {
+            part_u32x4 e[4];
+            bool ok[4];
 #pragma unroll
-        for (uint32_t j = 0; j < kFlPer; j++) {
-#pragma unroll
-            for (int c = 0; c < 4; c++) {  // a list past nunits loaded as zeros: entry 0 ...
-                const uint32_t lo = cur.e[j][c] & 0xffffu, hi = cur.e[j][c] >> 16;
-                const bool ok = tid + j * kPcBlock < A.nunits;  // ... so only real lists mark
-                if (ok && lo != 0xffffu) mk[lo & 1023u] = ep;
-                if (ok && hi != 0xffffu) mk[hi & 1023u] = ep;
+            for (int j = 0; j < 4; j++) {
+                const uint32_t p = p0 + uint32_t(j) * kPcBlock + tid;
+                const uint32_t un = p / kRun, tt = r0 + p % kRun;
+                ok[j] = p < npieces && tt < r1;
+                e[j] = __builtin_bit_cast(part_u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                         rfl, ok[j] ? (un * A.fl_stride + tt) * kPbLanes * 2 : kOOR, 0, 0));
             }
-        }
-        In nxt;
-        load(t + nblk, nxt);
-        lds_barrier();
-        bool valid[U];
-        uint32_t *w[U];
-        uint32_t rank[U], sh[U], cur_w[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
-            valid[u] = i < A.n && cur.fb[u] == 0 && mk[uint32_t(u) * kPcBlock + tid] != ep;
-            w[u] = nullptr;
-            rank[u] = sh[u] = 0;
-            if (valid[u]) {
-                if (cur.sl[u] >= A.nslots) {
-                    atomicOr(A.err, 1u);
-                } else {
-                    const uint32_t ridx = cur.hv[u] & 0xffffu;
-                    w[u] = reinterpret_cast<uint32_t *>(A.regs + (uint64_t(cur.sl[u]) << kHllP) + (ridx & ~3u));
-                    sh[u] = (ridx & 3) * 8;
-                    rank[u] = cur.hv[u] >> 16;
+            for (int j = 0; j < 4; j++) {
+                const uint32_t base = ((p0 + uint32_t(j) * kPcBlock + tid) % kRun) * 1024;
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const uint32_t lo = e[j][c] & 0xffffu, hi = e[j][c] >> 16;
+                    if (ok[j] && lo != 0xffffu) mark[base + (lo & 1023u)] = ep;
+                    if (ok[j] && hi != 0xffffu) mark[base + (hi & 1023u)] = ep;
                 }
             }
         }
-#pragma unroll
-        for (int u = 0; u < U; u++) cur_w[u] = w[u] ? nt_ld<32>(w[u]) : 0xffffffffu;
-        // every raising CAS of the tile in flight at once, then settled (a
-        // lost race retries from the word the CAS returned)
-        uint32_t seen[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            seen[u] = cur_w[u];
-            if (w[u] && ((cur_w[u] >> sh[u]) & 0xffu) < rank[u])
-                seen[u] = atomicCAS(w[u], cur_w[u], (cur_w[u] & ~(0xffu << sh[u])) | (rank[u] << sh[u]));
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++)
-            if (w[u] && seen[u] != cur_w[u]) part_reg_max(w[u], sh[u], rank[u], seen[u]);
-        if (A.out) {
+        lds_barrier();
+        for (uint32_t t = r0; t < r1; t++) {
+            In nxt;
+            load(t + 1, r1, nxt);
+            const uint16_t *mk = mark + (t - r0) * 1024;
+            bool valid[U];
+            uint32_t *w[U];
+            uint32_t rank[U], sh[U], cw[U], seen[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
-                if (i < A.n) nt_st<16>(A.out + i, uint8_t(valid[u]));
+                valid[u] = i < A.n && cur.fb[u] == 0 && mk[uint32_t(u) * kPcBlock + tid] != ep;
+                w[u] = nullptr;
+                rank[u] = sh[u] = 0;
+                if (valid[u]) {
+                    if (cur.sl[u] >= A.nslots) {
+                        atomicOr(A.err, 1u);
+                    } else {
+                        const uint32_t ridx = cur.hv[u] & 0xffffu;
+                        w[u] = reinterpret_cast<uint32_t *>(A.regs + (uint64_t(cur.sl[u]) << kHllP) + (ridx & ~3u));
+                        sh[u] = (ridx & 3) * 8;
+                        rank[u] = cur.hv[u] >> 16;
+                    }
+                }
             }
+#pragma unroll
+            for (int u = 0; u < U; u++) cw[u] = w[u] ? nt_ld<32>(w[u]) : 0xffffffffu;
+            // every raising CAS of the tile in flight at once, then settled
+            // (a lost race retries from the word the CAS returned)
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                seen[u] = cw[u];
+                if (w[u] && ((cw[u] >> sh[u]) & 0xffu) < rank[u])
+                    seen[u] = atomicCAS(w[u], cw[u], (cw[u] & ~(0xffu << sh[u])) | (rank[u] << sh[u]));
+            }
+            if (A.out) {
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
+                    if (i < A.n) nt_st<16>(A.out + i, uint8_t(valid[u]));
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (w[u] && seen[u] != cw[u]) part_reg_max(w[u], sh[u], rank[u], seen[u]);
+            cur = nxt;
         }
-        cur = nxt;
+        lds_barrier();  // the marks are rewritten by the next run
     }
 }
 
@@ -1657,7 +1661,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             hipLaunchKernelGGL(k_part_hd, dim3(unsigned(cus) * 2), dim3(1024), 0, sc, H);
             hipLaunchKernelGGL(k_part_he, dim3(unsigned(cus) * 2), dim3(kHeBlock), 0, sc, P, H);
         } else if (flist) {
-            const unsigned gc = (part_grid(ms, 1024, cus * 8) + kPGroups - 1) / kPGroups * kPGroups;
+            const unsigned gc = (part_grid(ms, 1024 * kPbGroup, cus * 8) + kPGroups - 1) / kPGroups * kPGroups;
             hipLaunchKernelGGL(k_part_c_fl<4>, dim3(gc), dim3(kPcBlock), 0, sc, P);
         } else {
             const unsigned gc = (part_grid(ms, kPcBlock * 2, cus * 8) + kPGroups - 1) / kPGroups * kPGroups;
