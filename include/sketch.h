@@ -206,6 +206,17 @@ int ske_swipes_fixed(ske_ctx *ctx, uint32_t fid, const uint32_t *slot, const uin
                      uint32_t width, uint64_t n, uint8_t *out_valid, int mem);
 int ske_swipes_fixed_async(ske_ctx *ctx, uint32_t fid, const uint32_t *slot,
                            const uint8_t *bytes, uint32_t width, uint64_t n, uint8_t *out_valid);
+/* Fixed-width swipes with the answers packed 1 bit per swipe (bit i & 7 of
+ * out_bits[i >> 3], LSB first -- numpy packbits(bitorder="little")).  Same
+ * BF.EXISTS / PFADD semantics as ske_swipes.  With host memory the batch is
+ * pipelined in chunks: a chunk's ids and slots cross the host link while K1
+ * runs on the previous one; the link carries width + 4 bytes per swipe in and
+ * 1/8 byte out (the offsets-and-bytes form: width + 9).  Synchronous; reports
+ * this call's own out-of-range slots (SKE_ERANGE).
+ *   replaces the per-event pair attendance_processor.py:109-113 + :127-129
+ *   for a batch of fixed-digit student ids (every config's ids) */
+int ske_swipes_fixed_bits(ske_ctx *ctx, uint32_t fid, const uint32_t *slot, const uint8_t *bytes,
+                          uint32_t width, uint64_t n, uint8_t *out_bits, int mem);
 /* Swipes that arrive NOT partitioned by key owner (one
  * alltoallv per batch; distributed.SwipeExchange; no reference counterpart --
  * the reference's Shared subscription hands any event to any consumer,

@@ -606,6 +606,26 @@ class SketchClient:
                           _ptr(valid), SKE_MEM_HOST)
         return valid.astype(bool)
 
+    def swipes_fixed(self, bf_key, slots: np.ndarray, ids: np.ndarray) -> np.ndarray:
+        """``swipes_slots`` for ids of one fixed width: ``ids`` is a [n, width]
+        uint8 array of the ids' bytes (e.g. 8-digit student ids as redis-py
+        encodes them).  Through ske_swipes_fixed_bits: no offsets cross the
+        host link and the answers come back 1 bit per swipe, in chunks that
+        overlap the copies with the kernels."""
+        ids = np.ascontiguousarray(ids, dtype=np.uint8)
+        if ids.ndim != 2:
+            raise ValueError("ids must be a [n, width] uint8 array")
+        n, width = ids.shape
+        bits = np.zeros((n + 7) // 8, np.uint8)
+        bkey = encode(bf_key)
+        if n and width and self.keys.expect(bkey, "bf"):
+            s = np.ascontiguousarray(slots, dtype=np.uint32)
+            if s.shape != (n,):
+                raise ValueError("one slot per id")
+            self.ctx.call("ske_swipes_fixed_bits", self.keys.fid[bkey], _ptr(s), _ptr(ids), width, n,
+                          _ptr(bits), SKE_MEM_HOST)
+        return np.unpackbits(bits, count=n, bitorder="little").astype(bool)
+
     # ------------------------------------------------------------ ingest (§8f row 3)
     def ingest(self, bf_key, messages: Sequence, hll_key_prefix: str = "hll:unique:",
                key_form: str = "readme") -> tuple[np.ndarray, np.ndarray]:

@@ -120,6 +120,10 @@ struct ske_ctx {
     hipEvent_t many_join[SKE_MANY_MAX_BRANCHES - 1] = {};
     hipEvent_t many_fork = nullptr;
     int many_n = 0;
+    // host-fed chunk pipeline (ske_swipes_fixed_bits): a copy stream and one
+    // event per chunk in flight (lazy)
+    hipStream_t copy_st = nullptr;
+    std::vector<hipEvent_t> chunk_ev;
     // ingest key table (open addressing on the 128-bit key hash)
     uint64_t *kt_key = nullptr;  // 2 per entry, kh0 == 0: empty
     uint32_t *kt_slot = nullptr;
@@ -727,6 +731,8 @@ int ske_close(ske_ctx *c) {
     if (c->many_fork) (void)hipEventDestroy(c->many_fork);
     for (hipEvent_t e : c->part_ev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->chunk_ev) (void)hipEventDestroy(e);
+    if (c->copy_st) (void)hipStreamDestroy(c->copy_st);
     if (c->kt_key) (void)hipFree(c->kt_key);
     if (c->kt_slot) (void)hipFree(c->kt_slot);
     if (c->stats) (void)hipFree(c->stats);
@@ -1474,6 +1480,67 @@ int ske_swipes_fixed(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8
     if (rc) return rc;
     if (out_valid && mem != SKE_MEM_DEVICE)
         HIPCHK(c, hipMemcpyAsync(out_valid, dout, n, hipMemcpyDeviceToHost, c->st));
+    return check_call_err(c);
+}
+
+// Fixed-width swipes with bit-packed answers.  Host inputs are cut into
+// chunks of kFeedChunk swipes: the chunk's ids and slots go host -> device on
+// a copy stream (sketch_host.cpp's pinned double buffer for pageable memory)
+// while K1 runs on the previous chunk on the context stream; each chunk's
+// answers are packed to bits on the device and copied back (1 bit per swipe).
+// Per swipe the host link carries width + 4 bytes in and 1/8 byte out.
+constexpr uint64_t kFeedChunk = uint64_t(4) << 20;
+
+int ske_swipes_fixed_bits(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *bytes, uint32_t width,
+                          uint64_t n, uint8_t *out_bits, int mem) {
+    if (!c || !slot || !bytes || width == 0 || width > 4096) return SKE_EINVAL;
+    Filter *F = get_filter(c, fid);
+    if (!F) return SKE_EINVAL;
+    if (n == 0) return SKE_OK;
+    if (const int erc = err_begin(c)) return erc;  // earlier enqueue-only calls' slot errors
+    int rc = SKE_OK;
+    // the answers (bytes, 8-B aligned for the packer) always on the device
+    uint8_t *dans = (uint8_t *)stage_buf(c, 4, n + 16, &rc);
+    if (rc) return rc;
+    if (mem == SKE_MEM_DEVICE) {
+        rc = ske_swipes_fixed_async(c, fid, slot, bytes, width, n, dans);
+        if (rc) return rc;
+        if (out_bits) HIPCHK(c, launch_pack_bits(dans, n, out_bits, c->cus, c->st));
+        return check_call_err(c);
+    }
+    uint8_t *db = (uint8_t *)stage_buf(c, 0, n * width + 16, &rc);
+    uint32_t *ds = rc ? nullptr : (uint32_t *)stage_buf(c, 2, n * 4 + 16, &rc);
+    uint8_t *dbits = rc ? nullptr : (uint8_t *)stage_buf(c, 3, (n + 7) / 8 + 16, &rc);
+    if (rc) return rc;
+    if (!c->copy_st) HIPCHK(c, hipStreamCreateWithFlags(&c->copy_st, hipStreamNonBlocking));
+    if (!c->hs) c->hs = stager_new();
+    const uint64_t nchunks = (n + kFeedChunk - 1) / kFeedChunk;
+    while (c->chunk_ev.size() < nchunks) {
+        hipEvent_t e = nullptr;
+        HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->chunk_ev.push_back(e);
+    }
+    // the copy stream starts behind everything already on the context stream
+    // (earlier users of the staging buffers)
+    HIPCHK(c, hipEventRecord(c->chunk_ev[0], c->st));
+    HIPCHK(c, hipStreamWaitEvent(c->copy_st, c->chunk_ev[0], 0));
+    for (uint64_t j = 0; j < nchunks; j++) {
+        const uint64_t s0 = j * kFeedChunk, m = n - s0 < kFeedChunk ? n - s0 : kFeedChunk;
+        HIPCHK(c, stage_h2d(c->hs, db + s0 * width, bytes + s0 * width, m * width, c->copy_st, false, nullptr));
+        HIPCHK(c, stage_h2d(c->hs, ds + s0, slot + s0, m * 4, c->copy_st, false, nullptr));
+        HIPCHK(c, hipEventRecord(c->chunk_ev[j], c->copy_st));
+        HIPCHK(c, hipStreamWaitEvent(c->st, c->chunk_ev[j], 0));
+        rc = ske_swipes_fixed_async(c, fid, ds + s0, db + s0 * width, width, m, dans + s0);
+        if (rc) {
+            (void)hipStreamSynchronize(c->copy_st);  // the copies may still read the caller's buffers
+            return rc;
+        }
+        if (out_bits) {
+            HIPCHK(c, launch_pack_bits(dans + s0, m, dbits + s0 / 8, c->cus, c->st));
+            HIPCHK(c, hipMemcpyAsync(out_bits + s0 / 8, dbits + s0 / 8, (m + 7) / 8, hipMemcpyDeviceToHost, c->st));
+        }
+    }
+    HIPCHK(c, hipStreamSynchronize(c->copy_st));
     return check_call_err(c);
 }
 

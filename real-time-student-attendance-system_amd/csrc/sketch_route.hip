@@ -155,6 +155,33 @@ hipError_t launch_route(const uint8_t *ids, uint32_t width, const uint32_t *slot
     return hipGetLastError();
 }
 
+// out[j] bit b = (in[8j + b] != 0): answers packed LSB first (numpy's
+// packbits(bitorder="little")), 1 bit per swipe on the device-to-host leg
+__global__ void __launch_bounds__(256) k_pack_bits(const uint8_t *in, uint64_t n, uint8_t *out) {
+    const uint64_t nb = (n + 7) / 8;
+    for (uint64_t j = uint64_t(blockIdx.x) * 256 + threadIdx.x; j < nb; j += uint64_t(gridDim.x) * 256) {
+        uint32_t v = 0;
+        if (8 * j + 8 <= n) {
+            const uint2 w = *reinterpret_cast<const uint2 *>(in + 8 * j);
+#pragma unroll
+            for (int b = 0; b < 4; b++) v |= uint32_t(((w.x >> (8 * b)) & 0xffu) != 0) << b;
+#pragma unroll
+            for (int b = 0; b < 4; b++) v |= uint32_t(((w.y >> (8 * b)) & 0xffu) != 0) << (4 + b);
+        } else {
+            for (uint64_t b = 0; 8 * j + b < n; b++) v |= uint32_t(in[8 * j + b] != 0) << b;
+        }
+        out[j] = uint8_t(v);
+    }
+}
+
+hipError_t launch_pack_bits(const uint8_t *in, uint64_t n, uint8_t *out, int cus, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint64_t g = ((n + 7) / 8 + 255) / 256;
+    const unsigned grid = unsigned(g < uint64_t(cus) * 8 ? g : uint64_t(cus) * 8);
+    hipLaunchKernelGGL(k_pack_bits, dim3(grid), dim3(256), 0, st, in, n, out);
+    return hipGetLastError();
+}
+
 uint64_t route_hist_words(uint64_t n, uint32_t world) { return uint64_t(world) * ((n + kRtTile - 1) / kRtTile); }
 
 hipError_t launch_route_return(const uint8_t *ans, const uint32_t *pos, uint64_t n, uint8_t *out, int cus,

@@ -330,3 +330,78 @@ def test_host_staged_large_batch_equals_device_resident(engine, orc):
     assert np.array_equal(out, dout.to_host(np.uint8, n))
     assert np.array_equal(engine.registers_all(2 * w.n_keys)[w.n_keys:], host_regs)
     assert out.sum() > 0.8 * n
+
+
+@pytest.mark.parametrize("mem", ["host", "device"])
+def test_fixed_bits_feed_equals_device_resident(pkg, engine, orc, mem):
+    """ske_swipes_fixed_bits: fixed-width ids, answers 1 bit per swipe, host
+    batches pipelined in 4M-swipe chunks (copy stream beside K1).  Over 9M + 5
+    swipes (three chunks, a ragged last byte) on the C3 filter its answers and
+    registers equal the device-resident ske_swipes of the same batch on
+    another context, and the oracle's on a sample."""
+    import ctypes as C
+    from rtsas_amd import synthetic
+    from rtsas_amd._lib import SKE_MEM_DEVICE, SKE_MEM_HOST
+    from rtsas_amd.engine import DeviceBuffer, SketchEngine
+    w = synthetic.WORKLOADS["c3"]
+    w = synthetic.Workload(**{**w.__dict__, "n_members": 300_000, "n_keys": 500, "zipf_lectures": 0,
+                              "zipf_days": 0})
+    n = 9 * 1024 * 1024 + 5
+    engines = [engine, SketchEngine(0)]
+    for e in engines:
+        e.reserve(0, w.bf_error, w.bf_capacity)
+        p = e.gen_params(w)
+        e.preload(0, p, w.n_members)
+        e.hll_reserve(w.n_keys)
+        assert e.variant(0) == 3
+    ref, fed = engines
+    b = ref.swipe_batch(ref.gen_params(w), 0, n)
+    out = DeviceBuffer(ref.ctx, n)
+    ref.swipes(0, b, out)
+    want = out.to_host(np.uint8, n)
+    buf, offs, slot = b.to_host()
+    width = int(offs[1] - offs[0])
+    ids = np.ascontiguousarray(buf[:n * width].reshape(n, width))
+    bits = np.zeros((n + 7) // 8, np.uint8)
+    if mem == "host":
+        fed.ctx.call("ske_swipes_fixed_bits", 0, slot.ctypes.data_as(C.c_void_p), ids.ctypes.data_as(C.c_void_p), width, n,
+                     bits.ctypes.data_as(C.c_void_p), SKE_MEM_HOST)
+    else:
+        fb = fed.swipe_batch(fed.gen_params(w), 0, n)
+        dbits = DeviceBuffer(fed.ctx, bits.size)
+        fed.ctx.call("ske_swipes_fixed_bits", 0, C.c_void_p(fb.slot.ptr), C.c_void_p(fb.bytes.ptr), width, n,
+                     C.c_void_p(dbits.ptr), SKE_MEM_DEVICE)
+        bits = dbits.to_host(np.uint8, bits.size)
+    got = np.unpackbits(bits, count=n, bitorder="little")
+    assert np.array_equal(got, want)
+    assert np.array_equal(fed.registers_all(w.n_keys), ref.registers_all(w.n_keys))
+    # the oracle on the first 200k swipes (answers depend on the Bloom only)
+    chain = orc.Chain(w.bf_capacity, w.bf_error)
+    mb = ref.members_batch(ref.gen_params(w), 0, w.n_members).to_host()
+    chain.madd_packed(mb[0], mb[1])
+    k = 200_000
+    v, _ = chain.mexists_packed(buf[:k * width + 16], offs[:k + 1])
+    assert np.array_equal(got[:k], v)
+
+
+def test_client_swipes_fixed(client, orc):
+    """SketchClient.swipes_fixed (the facade's fixed-width, bit-packed form)
+    == swipes_slots == the oracle."""
+    rng = np.random.default_rng(5)
+    members = rng.choice(np.arange(10_000_000, 99_999_999), 50_000, replace=False)
+    client.execute_command("BF.RESERVE", "bf", 0.001, 10_000_000)
+    from rtsas_amd import pack_ints
+    client.bf_madd_packed("bf", *pack_ints(members))
+    ids = np.where(rng.random(300_001) < 0.9, rng.choice(members, 300_001), rng.integers(10**7, 10**8, 300_001))
+    keys = [f"hll:unique:L{k}:2025-10-03" for k in range(9)]
+    slots = np.asarray([client.key_slot(k) for k in keys], np.uint32)[rng.integers(0, 9, ids.size)]
+    buf, offs = pack_ints(ids)
+    fixed = buf.reshape(-1, 8)
+    got = client.swipes_fixed("bf", slots, fixed)
+    chain = orc.Chain(10_000_000, 0.001)
+    chain.madd_packed(*pack_ints(members))
+    want, _ = chain.mexists_packed(np.concatenate([buf, np.zeros(16, np.uint8)]), offs)
+    assert np.array_equal(got, want.astype(bool))
+    regs = [client.hll_registers(k) for k in keys]
+    assert np.array_equal(client.swipes_slots("bf", slots, buf, offs), got)   # replay: same answers
+    assert all(np.array_equal(client.hll_registers(k), r) for k, r in zip(keys, regs))   # idempotent

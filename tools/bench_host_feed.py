@@ -60,6 +60,32 @@ def main():
                 "answers_equal_device_resident": bool(np.array_equal(got, want))}
 
     res = [run(buf, offs, slot, np.zeros(n, np.uint8), "pageable numpy")]
+    # fixed-width ids, answers 1 bit per swipe, chunked copy/compute pipeline
+    width = int(offs[1] - offs[0])
+    ids = np.ascontiguousarray(buf[:n * width].reshape(n, width))
+
+    def run_bits(bids, bslot, bbits, label):
+        ptr = lambda a: C.c_void_p(a.ctypes.data if isinstance(a, np.ndarray) else a.data_ptr())
+        call = lambda: eng.ctx.call("ske_swipes_fixed_bits", 0, ptr(bslot), ptr(bids), width, n, ptr(bbits),
+                                    SKE_MEM_HOST)
+        call()
+        ts = []
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            call()
+            ts.append(time.perf_counter() - t0)
+        got = bbits if isinstance(bbits, np.ndarray) else bbits.numpy()
+        t = float(np.median(ts))
+        nbytes = int(n * width + bslot.nbytes + (n + 7) // 8)
+        return {"label": label, "ms_per_step": t * 1e3, "swipes_per_s": n / t, "host_bytes_per_step": nbytes,
+                "GB_per_s_host_link": nbytes / t / 1e9,
+                "answers_equal_device_resident": bool(np.array_equal(
+                    np.unpackbits(got, count=n, bitorder="little"), want))}
+    res.append(run_bits(ids, slot, np.zeros((n + 7) // 8, np.uint8), "fixed width + bit answers, pageable numpy"))
+    pid = torch.from_numpy(ids.reshape(-1)).pin_memory()
+    pslot = torch.from_numpy(slot).pin_memory()
+    pbits = torch.zeros((n + 7) // 8, dtype=torch.uint8).pin_memory()
+    res.append(run_bits(pid, pslot, pbits, "fixed width + bit answers, pinned torch"))
     pb = torch.from_numpy(buf).pin_memory()
     po = torch.from_numpy(offs).pin_memory()
     ps = torch.from_numpy(slot).pin_memory()
