@@ -18,7 +18,9 @@
  *     device buffers; pageable inputs above 8 MB go through two pinned 32 MB
  *     buffers filled by up to 8 host threads the context starts on first use)
  *     or SKE_MEM_DEVICE (HIP device pointers, e.g. torch-ROCm data_ptr(), used
- *     in place on the context stream).
+ *     in place on the context stream).  SKE_MEM_HOST inputs must not be
+ *     modified until the call returns (pinned ones are read by the DMA engine
+ *     directly; the offsets are checked on the copy that is moved).
  *   - packed items: `bytes` + `offs[n+1]` (u32 byte offsets, offs[0] may be
  *     non-zero).  Device byte buffers must stay readable up to the next 8-byte
  *     boundary after bytes+offs[n] (any hipMalloc / torch allocation is).

@@ -187,6 +187,19 @@ class SketchClient:
     def exists(self, *names) -> int:
         return sum(encode(n) in self.keys.kind for n in names)
 
+    def scan_iter(self, match=None, count=None, _type=None):
+        """SCAN over the key table, redis-py's iterator form (one pass, sorted;
+        MATCH in Redis' glob syntax: *, ?, [..]).  (redis-py's ``keys()`` is
+        not offered: ``self.keys`` is the key table.)"""
+        import fnmatch
+        import re
+        pat = encode(match if match is not None else "*")
+        rx = re.compile(fnmatch.translate(pat.decode("latin-1")).encode("latin-1"), re.S)
+        for k in sorted(self.keys.kind):
+            if rx.match(k) and (_type is None or self.keys.kind[k] == {"string": "hll", "MBbloom--": "bf"}.get(
+                    _type, _type)):
+                yield k.decode() if self.decode_responses else k
+
     def type(self, name):
         k = self.keys.type_of(encode(name))
         return self._s({"bf": BF_TYPE_NAME, "hll": "string", None: "none"}[k])

@@ -83,7 +83,9 @@ class CopyPool {
             if (b > a) {
                 if (dst) memcpy(dst + a, src + a, b - a);
                 if (mono) {
-                    const uint32_t *u = reinterpret_cast<const uint32_t *>(src);
+                    // the copy that the DMA will move is the one checked
+                    // (fresh in this thread's cache), not the caller's buffer
+                    const uint32_t *u = reinterpret_cast<const uint32_t *>(dst ? static_cast<const char *>(dst) : src);
                     uint32_t bad = 0;
                     // element a/4 is compared with its predecessor (the slice boundary)
                     for (size_t k = std::max<size_t>(a / 4, 1); k < b / 4; k++) bad |= uint32_t(u[k] < u[k - 1]);
@@ -166,7 +168,9 @@ static bool u32_monotone(const uint32_t *u, size_t n) {
 }
 
 // Host -> device copy of `bytes` on `st` (enqueued; the caller's buffer may
-// be reused once the stream has passed this copy).  mono: the source is a u32
+// be reused once the stream has passed this copy, and must not be modified
+// before: a pinned caller buffer is read by the DMA engine directly, and its
+// offsets are checked while the DMA runs).  mono: the source is a u32
 // array that must never decrease -> *ok = false otherwise (the copy is still
 // made; the caller must not launch a kernel on it).
 hipError_t stage_h2d(HostStager *s, void *dst, const void *src, size_t bytes, hipStream_t st, bool mono,
@@ -211,10 +215,11 @@ hipError_t stage_h2d(HostStager *s, void *dst, const void *src, size_t bytes, hi
         if (s->busy[k] && (e = hipEventSynchronize(s->ev[k])) != hipSuccess) return e;
         s->busy[k] = false;
         good &= pool->copy(s->pin[k], src8 + off, len, mono);
+        const char *pk = static_cast<const char *>(s->pin[k]);
         if (mono && off) {  // the chunk boundary (chunks hold whole u32 elements)
-            good &= *reinterpret_cast<const uint32_t *>(src8 + off) >= prev_last;
+            good &= *reinterpret_cast<const uint32_t *>(pk) >= prev_last;
         }
-        if (mono) prev_last = *reinterpret_cast<const uint32_t *>(src8 + off + len - 4);
+        if (mono) prev_last = *reinterpret_cast<const uint32_t *>(pk + len - 4);
         if ((e = hipMemcpyAsync(dst8 + off, s->pin[k], len, hipMemcpyHostToDevice, st)) != hipSuccess) return e;
         if ((e = hipEventRecord(s->ev[k], st)) != hipSuccess) return e;
         s->busy[k] = true;

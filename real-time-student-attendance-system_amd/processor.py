@@ -34,9 +34,6 @@ class AttendanceProcessor:
         self.redis_client = client or SketchClient(decode_responses=True, device=self.config.device)
         self.acked = 0
         self.nacked = 0
-        # lecture_id -> the day keys its valid events were counted into
-        # (README key form), for get_attendance_stats(lecture_id)
-        self._lecture_keys: dict = {}
 
     # attendance_processor.py:74-92
     def _setup_bloom_filter(self):
@@ -110,10 +107,8 @@ class AttendanceProcessor:
             rows.append({"student_id": student_id, "lecture_id": lecture_id, "timestamp": ts})
         if rows:
             valid = self.redis_client.swipes(cfg.bloom_filter_key, keys, ids)
-            for r, k, v in zip(rows, keys, valid):
+            for r, v in zip(rows, valid):
                 r["is_valid"] = bool(v)
-                if v:
-                    self._lecture_keys.setdefault(r["lecture_id"], set()).add(k)
             self.acked += len(rows)
         return rows
 
@@ -136,15 +131,17 @@ class AttendanceProcessor:
     def get_attendance_stats(self, lecture_id: str, day: str | None = None) -> dict:
         """PFCOUNT of the lecture's key (:151-152).  In the README key form a
         lecture is counted per day: with a day, that day's key; without one
-        (the reference's signature), the union of every day key this
-        processor counted the lecture's valid events into -- PFCOUNT k1 k2 ..."""
+        (the reference's signature), the union of every day key of the
+        lecture in the store (SCAN MATCH prefix+lecture:*, so a fresh
+        processor on the same store answers the same) -- PFCOUNT k1 k2 ..."""
         prefix = self.config.hll_key_prefix
         if self.config.hll_key_form == "code":
             key = f"{prefix}{lecture_id}" + (f":{day}" if day else "")
             return {"unique_attendees": self.redis_client.pfcount(key)}
         if day is not None:
             return {"unique_attendees": self.redis_client.pfcount(f"{prefix}{lecture_id}:{day}")}
-        keys = sorted(self._lecture_keys.get(lecture_id, ()))
+        pat = "".join("[" + ch + "]" if ch in "*?[]\\" else ch for ch in f"{prefix}{lecture_id}:")
+        keys = [k for k in self.redis_client.scan_iter(match=pat + "*", _type="string")]
         return {"unique_attendees": self.redis_client.pfcount(*keys) if keys else 0}
 
 

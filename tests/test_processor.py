@@ -79,6 +79,12 @@ class OracleClient:
                 u.merge(self.hlls[k])
         return u.count()
 
+    def scan_iter(self, match=None, count=None, _type=None):
+        import fnmatch
+        for k in sorted(self.hlls):
+            if fnmatch.fnmatchcase(k, match or "*") and _type in (None, "string"):
+                yield k
+
 
 def test_setup_quirk_and_batches(pkg, orc):
     """BF.EXISTS on the missing key answers 0, so the reference's BF.RESERVE
@@ -182,6 +188,13 @@ def test_stats_without_day_unions_the_lecture_days(pkg, orc):
     assert len(days) == 3
     assert p.get_attendance_stats("CS101-L1")["unique_attendees"] == cl.pfcount(*days)
     assert p.get_attendance_stats("CS999")["unique_attendees"] == 0
+    # the day keys come from the store: a fresh processor (another process, a
+    # restart) on the same store answers the same
+    q = pkg.AttendanceProcessor(client=cl)
+    assert q.get_attendance_stats("CS101-L1")["unique_attendees"] == cl.pfcount(*days)
+    # a lecture id that is a prefix of another is not mixed in
+    cl.hlls["hll:unique:CS101-L10:2025-03-17"] = cl.hlls[days[0]]
+    assert q.get_attendance_stats("CS101-L1")["unique_attendees"] == cl.pfcount(*days)
 
 
 def test_non_faithful_setup_reserves(pkg, orc):
