@@ -51,10 +51,21 @@ class CopyPool {
         gen_++;
         cv_.notify_all();
         done_.wait(g, [this] { return pending_ == 0; });
+        if (mono && dst) {  // the slice boundaries, on the finished copy
+            const size_t per = slice_bytes(n);
+            const uint32_t *u = reinterpret_cast<const uint32_t *>(dst);
+            for (size_t a = per; a < n; a += per)
+                if (u[a / 4] < u[a / 4 - 1]) bad_.store(true);
+        }
         return !bad_.load();
     }
 
   private:
+    // each thread's slice: 64-B aligned (whole u32 elements for the check)
+    size_t slice_bytes(size_t n) const {
+        const size_t T = th_.size();
+        return ((n + T - 1) / T + 63) & ~size_t(63);
+    }
     void stop() {
         {
             std::lock_guard<std::mutex> g(m_);
@@ -76,9 +87,7 @@ class CopyPool {
             const size_t n = n_;
             const bool mono = mono_;
             g.unlock();
-            const size_t T = th_.size();
-            // slices on 64-B boundaries (whole u32 elements for the check)
-            const size_t per = ((n + T - 1) / T + 63) & ~size_t(63);
+            const size_t per = slice_bytes(n);
             const size_t a = std::min(n, per * size_t(i)), b = std::min(n, a + per);
             if (b > a) {
                 if (dst) memcpy(dst + a, src + a, b - a);
@@ -87,8 +96,11 @@ class CopyPool {
                     // (fresh in this thread's cache), not the caller's buffer
                     const uint32_t *u = reinterpret_cast<const uint32_t *>(dst ? static_cast<const char *>(dst) : src);
                     uint32_t bad = 0;
-                    // element a/4 is compared with its predecessor (the slice boundary)
-                    for (size_t k = std::max<size_t>(a / 4, 1); k < b / 4; k++) bad |= uint32_t(u[k] < u[k - 1]);
+                    // inside the slice; with a destination the slice
+                    // boundaries are compared once every slice is copied
+                    // (the neighbour's elements may not be there yet)
+                    const size_t k0 = dst ? a / 4 + 1 : std::max<size_t>(a / 4, 1);
+                    for (size_t k = k0; k < b / 4; k++) bad |= uint32_t(u[k] < u[k - 1]);
                     if (bad) bad_.store(true);
                 }
             }

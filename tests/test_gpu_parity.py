@@ -748,3 +748,51 @@ def test_host_staged_swipes_reject_decreasing_offsets(engine, pkg, orc):
     want, _, _ = orc.process_swipes(chain, regs, slot, ib, io)
     assert np.array_equal(out, want)
     assert np.array_equal(engine.registers_all(8), regs)
+
+
+@pytest.mark.parametrize("defect", [None, "mid-slice", "slice-boundary", "chunk-boundary"])
+def test_host_staged_large_offsets_checked_on_the_pinned_copy(engine, pkg, orc, defect):
+    """Pageable offsets above 8 MB go through the copy threads and the pinned
+    double buffer (sketch_host.cpp): the monotone check runs on the copy the
+    DMA moves.  A clean 12M-swipe batch (48 MB of offsets: two 32 MB chunks, 8
+    thread slices each) answers == the device path; one decrease inside a
+    thread's slice, exactly at a slice boundary, or at the chunk boundary is
+    refused (SKE_EINVAL) with the registers untouched."""
+    from rtsas_amd._lib import SKE_EINVAL, SKE_MEM_HOST
+    from rtsas_amd.engine import DeviceBatch, DeviceBuffer
+    rng = np.random.default_rng(3)
+    engine.reserve(0, 0.01, 100_000)
+    members = rng.choice(np.arange(10**6, 10**7), 50_000, replace=False)
+    mb, mo = pkg.pack_ints(members)
+    engine.ctx.call("ske_bf_madd", 0, C.c_void_p(mb.ctypes.data), C.c_void_p(mo.ctypes.data),
+                    members.size, None, SKE_MEM_HOST)
+    engine.hll_reserve(16)
+    n = 12_000_000
+    ids = np.where(rng.random(n) < 0.9, rng.choice(members, n), rng.integers(10**6, 10**7, n))
+    buf, offs = pkg.pack_ints(ids)
+    slot = rng.integers(0, 16, n).astype(np.uint32)
+    out = np.zeros(n, np.uint8)
+    ptr = lambda a: C.c_void_p(a.ctypes.data)
+    if defect is not None:
+        bad = offs.copy()
+        # 32 MB chunks of u32 = 8M elements; 8 slices of 4 MB = 1M elements
+        k = {"mid-slice": 1_234_567, "slice-boundary": 3 << 20, "chunk-boundary": 8 << 20}[defect]
+        bad[k] = bad[k - 1] - 1
+        with pytest.raises(pkg.SketchLibError) as ei:
+            engine.ctx.call("ske_swipes", 0, ptr(slot), ptr(buf), ptr(bad), n, ptr(out), SKE_MEM_HOST)
+        assert ei.value.code == SKE_EINVAL
+        assert not engine.registers_all(16).any()
+        return
+    engine.ctx.call("ske_swipes", 0, ptr(slot), ptr(buf), ptr(offs), n, ptr(out), SKE_MEM_HOST)
+    regs_host = engine.registers_all(16)
+    from rtsas_amd.engine import SketchEngine
+    e2 = SketchEngine(0)
+    e2.reserve(0, 0.01, 100_000)
+    e2.ctx.call("ske_bf_madd", 0, C.c_void_p(mb.ctypes.data), C.c_void_p(mo.ctypes.data),
+                members.size, None, SKE_MEM_HOST)
+    e2.hll_reserve(16)
+    b = DeviceBatch.from_host(e2.ctx, buf, offs, slot)
+    dout = DeviceBuffer(e2.ctx, n)
+    e2.swipes(0, b, dout)
+    assert np.array_equal(out, dout.to_host(np.uint8, n))
+    assert np.array_equal(regs_host, e2.registers_all(16))
