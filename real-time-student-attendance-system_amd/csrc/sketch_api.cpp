@@ -87,6 +87,7 @@ struct ske_ctx {
     int pa_tile = 10;       // partitioned K1 tile: 10 = 1024 swipes, 11 = 2048 (one-link k = 11 only)
     int pa_pre = 0;         // partitioned K1: pass A pre-checks the registers (measured slower: A +0.20, C -0.04 ms)
     int pa_grid = 0;        // partitioned K1 pass A blocks per CU (one-link k = 11; 0 = 2)
+    int pa_threads = 512;   // fail-list pass A (k_part_a3) threads per 1024-swipe tile: 512 or 1024
     int part_overlap = 0;   // many-batch calls: partitioned K1 pass C on a side stream (measured slower)
     hipEvent_t part_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool lds_ok = false;
@@ -591,7 +592,7 @@ int launch_part(ske_ctx *c, const ChainDev &ch, const PartBatch *bt, uint32_t nb
     };
     c->hook_arg = &hs;
     e = launch_swipes_part(ch, bt, nb, c->regs, c->nslots, c->scratch, c->err, c->cus, c->part_sub, c->hll_mode,
-                           c->pb_pairs, c->pa_tile, c->pa_pre, pipelined ? c->part_overlap : 0, c->pa_grid, c->st, side, c->part_ev, c->timing && !c->capturing ? +hook : nullptr, c);
+                           c->pb_pairs, c->pa_tile, c->pa_pre, pipelined ? c->part_overlap : 0, c->pa_grid, c->st, side, c->part_ev, c->timing && !c->capturing ? +hook : nullptr, c, c->pa_threads);
     if (e != hipSuccess) {
         c->last_hip = std::string("launch_swipes_part: ") + hipGetErrorString(e);
         scratch_user_end(c, cid);
@@ -862,6 +863,11 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
     if (!strcmp(name, "pa_precheck")) {  // partitioned K1: register pre-check in pass A (1) or pass C
         if (value < 0 || value > 1) return SKE_EINVAL;
         c->pa_pre = int(value);
+        return SKE_OK;
+    }
+    if (!strcmp(name, "pa_threads")) {  // fail-list pass A: threads per 1024-swipe tile
+        if (value != 512 && value != 1024) return SKE_EINVAL;
+        c->pa_threads = int(value);
         return SKE_OK;
     }
     if (!strcmp(name, "pa_grid")) {  // partitioned K1: pass A blocks per CU (0 = default)

@@ -155,7 +155,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
                               uint32_t nslots, Scratch *scr, unsigned int *err, int cus, uint32_t sub,
                               int hll_mode, int pb_pairs, int tile_opt, int pre_opt, int ovl, int a_grid, hipStream_t st, hipStream_t side,
                               hipEvent_t *ev,
-                              PassHook hook = nullptr, void *hook_user = nullptr);
+                              PassHook hook = nullptr, void *hook_user = nullptr, int a3_threads = 512);
 
 
 // sketch_order.hip -- order-exact paths (replies that depend on item order)

@@ -478,9 +478,9 @@ __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part
 //     return value plus that word: one shift and one add per record;
 //   * full tiles take a probe loop without the past-the-batch select.
 // Counters of the two tile parities are one array (bias index par*2048 + g).
-template <int KM>
-__global__ void __launch_bounds__(512, 2) k_part_a3(const PartArgs A) {
-    constexpr uint32_t kT = 512, kU = 2, kTile = 1024;
+template <int KM, uint32_t kT = 512>
+__global__ void __launch_bounds__(kT, 2) k_part_a3(const PartArgs A) {
+    constexpr uint32_t kU = 1024 / kT, kTile = 1024;
     constexpr uint32_t kCnt = kPMaxSlices + 1;  // counters per tile parity
     constexpr int kPer = kCnt / kT;
     static_assert(kCnt % kT == 0 && 4u * kTile * KM < 65536u, "a rank * 4 stays below bit 16");
@@ -1601,7 +1601,7 @@ hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratc
 hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t nb, uint8_t *regs,
                               uint32_t nslots, Scratch *scr, unsigned int *err, int cus, uint32_t sub_opt,
                               int hll_mode, int pb_pairs, int tile_opt, int pre_opt, int ovl, int a_grid, hipStream_t st, hipStream_t side,
-                              hipEvent_t *ev, PassHook hook, void *hook_user) {
+                              hipEvent_t *ev, PassHook hook, void *hook_user, int a3_threads) {
     PartArgs A{};
     if (!part_plan(ch, &A)) return hipErrorInvalidValue;
     const uint32_t sub = part_sub(sub_opt);
@@ -1697,8 +1697,11 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             const unsigned per_cu = km <= 11 ? (a_grid ? unsigned(a_grid) : 2u) : 1;
             const unsigned ga = unsigned(cus) * per_cu / kPGroups * kPGroups;  // blocks past a group's tiles exit
             if (hook) hook(hook_user, 0, 0, st);
-            if (flist)  // the fail-list path's own record format (k_part_a3 -> k_part_b<2, 4, true>)
-                hipLaunchKernelGGL(k_part_a3<11>, dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(512), 0, st, A);
+            if (flist && a3_threads == 1024)  // the fail-list path's own record format (k_part_a3 -> k_part_b<2, 4, true>)
+                hipLaunchKernelGGL((k_part_a3<11, 1024>), dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(1024), 0,
+                                   st, A);
+            else if (flist)
+                hipLaunchKernelGGL((k_part_a3<11, 512>), dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(512), 0, st, A);
             else if (one11 && A.tile_log == 11)  // RESERVE 0.001 (C3/C5): one link, k = 11
                 hipLaunchKernelGGL((k_part_a2<11, 1024>), dim3(unsigned(cus) / kPGroups * kPGroups), dim3(1024),
                                    0, st, A);
