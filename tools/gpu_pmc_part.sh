@@ -3,7 +3,10 @@
 # bench; per-kernel summaries of the partitioned K1's passes into
 # gpurun_out/pmc_<TAG>_{a,b,c}.json.   usage: TAG=c3 bash tools/gpu_pmc_part.sh
 TAG=${TAG:-c3}
-ARGS=${BENCH_ARGS:-"--config c3 --steps 8 --warmup 2 --no-cpu --secondary none --pass-replay 0 --streams 1 --graph 0"}
+# the bench's own steps (20 timed after 5 warm-up; the summaries skip the
+# warm-up dispatches), so per-dispatch counters describe the timed steps
+ARGS=${BENCH_ARGS:-"--config c3 --steps 20 --warmup 5 --no-cpu --no-check --secondary none --pass-replay 0 --streams 1 --graph 0"}
+SKIP=${SKIP:-5}
 mkdir -p gpurun_out/pmc_$TAG
 export TMPDIR=/tmp
 GROUPS_=("FETCH_SIZE" "WRITE_SIZE" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum"
@@ -15,6 +18,7 @@ for c in "${GROUPS_[@]}"; do
   echo "pmc [$c] rc=$rc"
   if [ $rc -ne 0 ]; then tail -3 gpurun_out/pmc_$TAG/$tag.log; exit $rc; fi
 done
-for k in a b c; do
-  python tools/pmc_summary.py gpurun_out/pmc_$TAG "k_part_$k" gpurun_out/pmc_${TAG}_$k.json 2 > /dev/null && echo "summary $k written"
-done
+python tools/pmc_summary.py gpurun_out/pmc_$TAG "k_part_a" gpurun_out/pmc_${TAG}_a.json $SKIP > /dev/null && echo "summary a written"
+# pass B reads its records and image with 16-B-per-lane loads: FETCH_SIZE x 2
+python tools/pmc_summary.py --wide 1 gpurun_out/pmc_$TAG "k_part_b" gpurun_out/pmc_${TAG}_b.json $SKIP > /dev/null && echo "summary b written"
+python tools/pmc_summary.py gpurun_out/pmc_$TAG "k_part_c" gpurun_out/pmc_${TAG}_c.json $SKIP > /dev/null && echo "summary c written"

@@ -1,11 +1,18 @@
 """Summarise rocprofv3 --pmc passes for one kernel into a JSON file.
 
-usage: python tools/pmc_summary.py [--launch] <pmc_root_dir> <kernel-substring> <out.json> [skip]
+usage: python tools/pmc_summary.py [--launch] [--wide F] <pmc_root_dir> <kernel-substring> <out.json> [skip]
 
 Each sub-directory of <pmc_root_dir> is one rocprofv3 pass
 (<pass>/run_counter_collection.csv).  Per counter the value is averaged over
 the dispatches of the kernel, skipping the first `skip` (warm-up) ones.
 HBM-side bytes per dispatch: FETCH_SIZE and WRITE_SIZE are in KB.
+
+--wide F: the share F (0..1) of the kernel's fetched bytes that come from
+16-B-per-lane streaming loads (pass B's probe records and LDS image: 1).  On
+gfx950 FETCH_SIZE reports exactly half of such streams (MI355X_MICROARCH.md,
+HBM section), so the corrected read bytes are FETCH_SIZE * (1 + F); the
+summary keeps the raw value too ("hbm_bytes_per_dispatch" raw,
+"hbm_bytes_corrected" with the correction).
 
 --launch: the substring matches several kernels that together make one
 launch of the path (the XCD-partitioned K1: hash, region and finish passes);
@@ -22,7 +29,7 @@ import os
 import sys
 
 
-def summarise(root: str, kernel: str, skip: int = 3) -> dict:
+def summarise(root: str, kernel: str, skip: int = 3, wide: float = 0.0) -> dict:
     counters: dict[str, list[float]] = collections.defaultdict(list)
     meta = {}
     for f in sorted(glob.glob(os.path.join(root, "*", "run_counter_collection.csv"))):
@@ -46,6 +53,8 @@ def summarise(root: str, kernel: str, skip: int = 3) -> dict:
     m = out["mean"]
     if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
         out["hbm_bytes_per_dispatch"] = (m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024
+        out["fetch_wide_fraction"] = wide
+        out["hbm_bytes_corrected"] = (m["FETCH_SIZE"] * (1.0 + wide) + m["WRITE_SIZE"]) * 1024
     if "SQ_LDS_BANK_CONFLICT" in m and m.get("SQ_LDS_IDX_ACTIVE"):
         out["lds_bank_conflict_rate"] = m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"]
     if "TCC_HIT_sum" in m and "TCC_MISS_sum" in m:
@@ -75,12 +84,17 @@ def summarise_launch(root: str, kernel: str, skip: int = 3) -> dict:
 
 if __name__ == "__main__":
     argv = sys.argv[1:]
-    launch = argv and argv[0] == "--launch"
+    launch = "--launch" in argv
     if launch:
-        argv = argv[1:]
+        argv.remove("--launch")
+    wide = 0.0
+    if "--wide" in argv:
+        i = argv.index("--wide")
+        wide = float(argv[i + 1])
+        del argv[i:i + 2]
     root, kern, path = argv[:3]
     skip = int(argv[3]) if len(argv) > 3 else 3
-    res = (summarise_launch if launch else summarise)(root, kern, skip)
+    res = summarise_launch(root, kern, skip) if launch else summarise(root, kern, skip, wide)
     with open(path, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res["mean"], indent=1))
