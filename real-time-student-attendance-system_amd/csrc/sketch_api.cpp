@@ -870,8 +870,10 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
         c->pa_threads = int(value);
         return SKE_OK;
     }
-    if (!strcmp(name, "pa_grid")) {  // partitioned K1: pass A blocks per CU (0 = default)
-        if (value < 0 || value > 2) return SKE_EINVAL;
+    if (!strcmp(name, "pa_grid")) {  // partitioned K1: pass A blocks per CU (0 = default); fail-list
+                                     // pass A of <= 511 slices: 3 three blocks per CU on a small
+                                     // counter table, 4 that table at two blocks per CU
+        if (value < 0 || value > 4) return SKE_EINVAL;
         c->pa_grid = int(value);
         return SKE_OK;
     }

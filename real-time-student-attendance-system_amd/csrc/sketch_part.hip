@@ -479,14 +479,17 @@ __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part
 //   * full tiles take a probe loop without the past-the-batch select.
 // Counters of the two tile parities are one array (bias index par*2048 + g).
 // SKE_A3_ABLATE (diagnostic builds only, answers wrong): 1 no record copy-out,
-// 2 no placement / copy-out, 4 counting by plain LDS adds into a per-lane word
+// 2 no placement / copy-out, 4 counting by plain LDS reads, 8 counting atomics at
+// bank-conflict-free addresses, 16 placement base reads at bank-conflict-free addresses
 #ifndef SKE_A3_ABLATE
 #define SKE_A3_ABLATE 0
 #endif
-template <int KM, uint32_t kT = 512>
-__global__ void __launch_bounds__(kT, 2) k_part_a3(const PartArgs A) {
+template <int KM, uint32_t kT = 512, uint32_t kCnt = kPMaxSlices + 1, int kMinBlocks = 2>
+__global__ void __launch_bounds__(kT, kMinBlocks * kT / 256) k_part_a3(const PartArgs A) {  // waves per SIMD
+    // kCnt: counters per tile parity (slices + the past-the-batch sink); 512
+    // for chains of <= 511 slices (C3/C5: 303) shrinks the block's LDS to
+    // 49 KiB, so three blocks fit a CU
     constexpr uint32_t kU = 1024 / kT, kTile = 1024;
-    constexpr uint32_t kCnt = kPMaxSlices + 1;  // counters per tile parity
     constexpr int kPer = kCnt / kT;
     static_assert(kCnt % kT == 0 && 4u * kTile * KM < 65536u, "a rank * 4 stays below bit 16");
     __shared__ __attribute__((aligned(16))) uint32_t srec[kTile * KM];
@@ -551,6 +554,8 @@ __global__ void __launch_bounds__(kT, 2) k_part_a3(const PartArgs A) {
                     rv[u][q] = (x & 0xfffffu) | lu20;
                     if constexpr ((SKE_A3_ABLATE & 4) != 0) {
                         rp[u][q] = cp[__builtin_amdgcn_ubfe(x, kPSliceLog, 12)];
+                    } else if constexpr ((SKE_A3_ABLATE & 8) != 0) {  // bank-conflict-free atomics
+                        rp[u][q] = atomicAdd(&cp[(lane & 31) | ((__builtin_amdgcn_ubfe(x, kPSliceLog, 12) & 7) << 5)], 4u);
                     } else {
                         rp[u][q] = atomicAdd(&cp[__builtin_amdgcn_ubfe(x, kPSliceLog, 12)], 4u);
                     }
@@ -605,8 +610,14 @@ __global__ void __launch_bounds__(kT, 2) k_part_a3(const PartArgs A) {
 #pragma unroll
                 for (int q = 0; q < KM; q++) {
                     const uint32_t r = rp[u][q];
-                    *reinterpret_cast<uint32_t *>(srecb + (r + *reinterpret_cast<const uint32_t *>(cntb + (r >> 16)))) =
-                        rv[u][q];
+                    if constexpr ((SKE_A3_ABLATE & 16) != 0)  // bank-conflict-free base reads
+                        *reinterpret_cast<uint32_t *>(srecb + ((r + cnt[(lane & 31) | ((r >> 18) & 0x3e0u)]) & 0x7ffcu)) = rv[u][q];
+                    else if constexpr ((SKE_A3_ABLATE & 8) != 0)
+                        *reinterpret_cast<uint32_t *>(
+                            srecb + ((r + *reinterpret_cast<const uint32_t *>(cntb + (r >> 16))) & 0x7ffcu)) = rv[u][q];
+                    else
+                        *reinterpret_cast<uint32_t *>(srecb + (r + *reinterpret_cast<const uint32_t *>(cntb + (r >> 16)))) =
+                            rv[u][q];
                 }
         } else {
             uint32_t x = 0;
@@ -619,7 +630,7 @@ __global__ void __launch_bounds__(kT, 2) k_part_a3(const PartArgs A) {
         const uint32_t nb = (cb ^ kCnt);
         for (uint32_t g = tid; g <= S; g += kT) cnt[nb + g] = (nb + g) << 18;
         lds_barrier();
-        const uint32_t total = (SKE_A3_ABLATE & 3) ? 0u : stot;
+        const uint32_t total = (SKE_A3_ABLATE & 3) ? 0u : (SKE_A3_ABLATE & 24) ? min(stot, kTile * KM) : stot;
         part_u32x4 *dst = reinterpret_cast<part_u32x4 *>(A.rec + size_t(t) * A.stride);
         const part_u32x4 *src = reinterpret_cast<const part_u32x4 *>(srec);
         for (uint32_t j = tid; j * 4 < total; j += kT) nt_st<4>(dst + j, src[j]);
@@ -1718,6 +1729,12 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             if (flist && a3_threads == 1024)  // the fail-list path's own record format (k_part_a3 -> k_part_b<2, 4, true>)
                 hipLaunchKernelGGL((k_part_a3<11, 1024>), dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(1024), 0,
                                    st, A);
+            else if (flist && A.nslices < 512 && a_grid == 3)  // small counter table: three blocks per CU
+                hipLaunchKernelGGL((k_part_a3<11, 512, 512, 3>), dim3(unsigned(cus) * 3 / kPGroups * kPGroups), dim3(512),
+                                   0, st, A);
+            else if (flist && A.nslices < 512 && a_grid == 4)  // small counter table, two blocks per CU (A/B)
+                hipLaunchKernelGGL((k_part_a3<11, 512, 512, 2>), dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(512),
+                                   0, st, A);
             else if (flist)
                 hipLaunchKernelGGL((k_part_a3<11, 512>), dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(512), 0, st, A);
             else if (one11 && A.tile_log == 11)  // RESERVE 0.001 (C3/C5): one link, k = 11
