@@ -872,8 +872,9 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
     }
     if (!strcmp(name, "pa_grid")) {  // partitioned K1: pass A blocks per CU (0 = default); fail-list
                                      // pass A of <= 511 slices: 3 three blocks per CU on a small
-                                     // counter table, 4 that table at two blocks per CU
-        if (value < 0 || value > 4) return SKE_EINVAL;
+                                     // counter table, 4 that table at two blocks per CU; < 320
+                                     // slices: 5 the counters in 16 copies (k_part_a4)
+        if (value < 0 || value > 5) return SKE_EINVAL;
         c->pa_grid = int(value);
         return SKE_OK;
     }

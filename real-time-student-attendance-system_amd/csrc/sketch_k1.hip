@@ -35,6 +35,11 @@ namespace ske {
 #define SKE_K1_NT 0
 #endif
 template <int BIT> __device__ __forceinline__ constexpr int k1_aux() { return (SKE_K1_NT & BIT) ? 2 : 0; }
+// SKE_K1_ABLATE (diagnostic builds only, registers may be wrong): 1 a raise is a
+// plain byte store instead of the CAS (prices the atomics' round trips)
+#ifndef SKE_K1_ABLATE
+#define SKE_K1_ABLATE 0
+#endif
 
 constexpr uint32_t kK1Block = 1024;     // threads per block, one block per CU
 constexpr uint32_t kK1Waves = kK1Block / 64;
@@ -358,9 +363,12 @@ __device__ __forceinline__ void k1_commit(const K1Args &A, const K1View &V, cons
             pd.prev[u] = h.cur[u];
             pd.rank[u] = h.rank[u];
             pd.sh[u] = h.sh[u];
-            if (need)
+            if constexpr ((SKE_K1_ABLATE & 1) != 0) {
+                if (need) reinterpret_cast<uint8_t *>(h.w[u])[h.sh[u] >> 3] = uint8_t(h.rank[u]);
+            } else if (need) {
                 pd.prev[u] = atomicCAS(h.w[u], h.cur[u],
                                        (h.cur[u] & ~(0xffu << h.sh[u])) | (h.rank[u] << h.sh[u]));
+            }
         }
     }
     if (V.out) {

@@ -637,6 +637,158 @@ __global__ void __launch_bounds__(kT, kMinBlocks * kT / 256) k_part_a3(const Par
     }
 }
 
+// k_part_a4: k_part_a3 with the slice counters spread over kCp = 16 copies,
+// counter (slice s, copy lane & 15) at word s * 16 + (lane & 15).  A counting
+// atomic or a placement read of 32 lanes then meets at most 2 distinct words
+// per bank (lanes l and l + 16 share a copy; banks are (word mod 32) for
+// ds_add / ds_read_b32, MI355X_MICROARCH.md §LDS) instead of the ~3.5 of 32
+// random counters; the run of slice s is the copies' runs in copy order, so
+// the scan runs over slices * 16 words (10 per thread, read as 8-byte pairs:
+// lane t's pair starts at bank 10t mod 64, all distinct).  One counter table
+// (20 KiB for <= 319 slices) keeps two blocks per CU: it is reset to its bias
+// after placement, behind one more barrier per tile.
+template <int KM, uint32_t kT = 512, uint32_t kSl = 320>
+__global__ void __launch_bounds__(kT, 2 * kT / 256) k_part_a4(const PartArgs A) {
+    constexpr uint32_t kU = 1024 / kT, kTile = 1024, kCp = 16, kW = kSl * kCp;
+    constexpr uint32_t kPer = kW / kT;
+    static_assert(kW % kT == 0 && kPer % 2 == 0 && kPer < kCp && 4u * kTile * KM < 65536u && kW < 16384u,
+                  "bias << 18 stays in 32 bits; a rank * 4 below bit 16; at most one slice start per thread");
+    __shared__ __attribute__((aligned(16))) uint32_t srec[kTile * KM];
+    __shared__ __attribute__((aligned(16))) uint32_t cnt[kW];
+    __shared__ uint32_t swsum[kT / 64];
+    __shared__ uint32_t stot;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t S = A.nslices;
+    const uint32_t cpy = (lane & (kCp - 1)) << 2;  // this lane's copy, in bytes
+    const uint32_t w0 = tid * kPer;                // the scan's words of this thread
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) cnt[w0 + j] = (w0 + j) << 18;
+    lds_barrier();
+    auto offsets = [&](uint32_t t, uint32_t u, uint32_t &b, uint32_t &e) {
+        const uint32_t i = t * kTile + u * kT + tid;
+        const uint32_t ic = i < A.n ? i : A.n - 1;
+        b = A.offs ? nt_ld<2>(A.offs + ic) : ic * A.fixed_w;
+        e = A.offs ? nt_ld<2>(A.offs + ic + 1) : b + A.fixed_w;
+    };
+    uint32_t gt0, gt1;
+    part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
+    const uint32_t tstep = gridDim.x / kPGroups;
+    const __amdgpu_buffer_rsrc_t rbytes = part_rsrc(A.bytes, 0xfffffff0u);
+    const PartLink &L = A.link[0];
+    uint32_t nb_[kU], ne_[kU];
+    PartId it[kU];
+    {
+        const uint32_t t = gt0 + blockIdx.x / kPGroups;
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            offsets(t < gt1 ? t : gt0, u, nb_[u], ne_[u]);
+            part_id_load(rbytes, nb_[u], ne_[u], it[u]);
+        }
+    }
+    uint8_t *cntb = reinterpret_cast<uint8_t *>(cnt);
+    uint8_t *srecb = reinterpret_cast<uint8_t *>(srec);
+    for (uint32_t t = gt0 + blockIdx.x / kPGroups; t < gt1; t += tstep) {
+        uint32_t rv[kU][KM], rp[kU][KM];
+        const uint32_t tn = t + tstep < gt1 ? t + tstep : t;
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) offsets(tn, u, nb_[u], ne_[u]);
+        const bool full = (t + 1) * kTile <= A.n;  // block-uniform
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t lu = u * kT + tid;
+            const uint32_t i = t * kTile + lu;
+            const bool act = i < A.n;
+            uint64_t ha, hb, hh;
+            part_hash3(A.bytes, it[u], ha, hb, hh);
+            if (act) {
+                uint32_t idx, rank;
+                hll_patlen(hh, idx, rank);
+                nt_st<8>(A.hllw + i, idx | (rank << 16));
+                nt_st<8>(A.fail + i, uint8_t(0));
+            }
+            const uint32_t lu20 = lu << 20;
+            ProbeWalk32 wk;
+            wk.init(ha, hb, part_div(L));
+            if (full) {
+#pragma unroll
+                for (int q = 0; q < KM; q++) {
+                    const uint32_t x = wk.x;
+                    rv[u][q] = (x & 0xfffffu) | lu20;
+                    rp[u][q] = atomicAdd(reinterpret_cast<uint32_t *>(
+                                             cntb + ((__builtin_amdgcn_ubfe(x, kPSliceLog, 12) << 6) | cpy)), 4u);
+                    if (q + 1 < KM) wk.step(L.d);
+                }
+            } else {
+                // a lane past the batch counts into slice S, left out of the
+                // scan's total: its records land past it, never copied
+#pragma unroll
+                for (int q = 0; q < KM; q++) {
+                    const uint32_t x = wk.x;
+                    rv[u][q] = (x & 0xfffffu) | lu20;
+                    const uint32_t s = act ? __builtin_amdgcn_ubfe(x, kPSliceLog, 12) : S;
+                    rp[u][q] = atomicAdd(reinterpret_cast<uint32_t *>(cntb + ((s << 6) | cpy)), 4u);
+                    if (q + 1 < KM) wk.step(L.d);
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this swipe's atomics, once
+        }
+        lds_barrier();
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) part_id_load(rbytes, nb_[u], ne_[u], it[u]);  // the next tile's ids
+        // exclusive scan of the counts of words (slice, copy) 0 .. (S + 1) * 16
+        uint32_t v[kPer], s = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; j += 2) {
+            const uint2 c2 = *reinterpret_cast<const uint2 *>(cnt + w0 + j);
+            v[j] = (c2.x - ((w0 + j) << 18)) >> 2;
+            v[j + 1] = (c2.y - ((w0 + j + 1) << 18)) >> 2;
+            s += v[j] + v[j + 1];
+        }
+        uint32_t incl = s;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= uint32_t(o)) incl += y;
+        }
+        if (lane == 63) swsum[wave] = incl;
+        lds_barrier();
+        uint32_t run = incl - s;
+        for (uint32_t w = 0; w < wave; w++) run += swsum[w];
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; j += 2) {
+            uint2 b2;
+            const uint32_t wa = w0 + j, wb = wa + 1;
+            if ((wa & (kCp - 1)) == 0 && (wa >> 4) <= S) A.off[size_t(wa >> 4) * A.off_stride + t] = run;
+            if (wa == S * kCp) stot = run;
+            b2.x = 4 * run - (wa << 18);
+            run += v[j];
+            if ((wb & (kCp - 1)) == 0 && (wb >> 4) <= S) A.off[size_t(wb >> 4) * A.off_stride + t] = run;
+            if (wb == S * kCp) stot = run;
+            b2.y = 4 * run - (wb << 18);
+            run += v[j + 1];
+            *reinterpret_cast<uint2 *>(cnt + wa) = b2;
+        }
+        lds_barrier();
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++)
+#pragma unroll
+            for (int q = 0; q < KM; q++) {
+                const uint32_t r = rp[u][q];
+                *reinterpret_cast<uint32_t *>(srecb + (r + *reinterpret_cast<const uint32_t *>(cntb + (r >> 16)))) =
+                    rv[u][q];
+            }
+        lds_barrier();
+        const uint32_t total = stot;
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; j += 2)
+            *reinterpret_cast<uint2 *>(cnt + w0 + j) = make_uint2((w0 + j) << 18, (w0 + j + 1) << 18);
+        part_u32x4 *dst = reinterpret_cast<part_u32x4 *>(A.rec + size_t(t) * A.stride);
+        const part_u32x4 *src = reinterpret_cast<const part_u32x4 *>(srec);
+        for (uint32_t j = tid; j * 4 < total; j += kT) nt_st<4>(dst + j, src[j]);
+        lds_barrier();  // the counters are reset before the next tile counts
+    }
+}
+
 // ---------------------------------------------------------------------------
 // pass B: LDS-resident slices, probe their runs
 // ---------------------------------------------------------------------------
@@ -1728,6 +1880,9 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             if (hook) hook(hook_user, 0, 0, st);
             if (flist && a3_threads == 1024)  // the fail-list path's own record format (k_part_a3 -> k_part_b<2, 4, true>)
                 hipLaunchKernelGGL((k_part_a3<11, 1024>), dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(1024), 0,
+                                   st, A);
+            else if (flist && A.nslices < 320 && a_grid == 5)  // slice counters in 16 copies
+                hipLaunchKernelGGL((k_part_a4<11, 512, 320>), dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(512), 0,
                                    st, A);
             else if (flist && A.nslices < 512 && a_grid == 3)  // small counter table: three blocks per CU
                 hipLaunchKernelGGL((k_part_a3<11, 512, 512, 3>), dim3(unsigned(cus) * 3 / kPGroups * kPGroups), dim3(512),

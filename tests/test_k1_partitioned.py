@@ -195,6 +195,37 @@ def test_fail_lists_and_overflow_vs_oracle(engine, orc, invalid, pb_mode):
         assert nvalid < b.n // 500   # only Bloom false positives remain
 
 
+@pytest.mark.parametrize("invalid", [0.1, 1.0])
+@pytest.mark.parametrize("pa_grid", [3, 4, 5])
+def test_pass_a_counter_layouts_vs_oracle(engine, orc, invalid, pa_grid):
+    """The fail-list pass A's counter-table forms on the C3 filter (303
+    slices): a 512-entry table at three (3) or two (4) blocks per CU, and the
+    slice counters spread over 16 copies (5, k_part_a4); a ragged last tile;
+    answers and registers == the oracle."""
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import DeviceBuffer
+    w = synthetic.WORKLOADS["c3"]
+    w = synthetic.Workload(**{**w.__dict__, "n_members": 300_000, "n_keys": 97, "zipf_lectures": 0,
+                              "zipf_days": 0, "invalid_frac": invalid})
+    engine.set_option("pa_grid", pa_grid)
+    engine.reserve(0, w.bf_error, w.bf_capacity)
+    p = engine.gen_params(w, seed=4243)
+    engine.preload(0, p, w.n_members)
+    engine.hll_reserve(w.n_keys)
+    assert engine.variant(0) == 3
+    b = engine.swipe_batch(p, 11, 900_000 + 517)
+    out = DeviceBuffer(engine.ctx, b.n)
+    engine.swipes(0, b, out)
+    chain = orc.Chain(w.bf_capacity, w.bf_error)
+    mb = engine.members_batch(p, 0, w.n_members).to_host()
+    chain.madd_packed(mb[0], mb[1])
+    regs = np.zeros((w.n_keys, 16384), np.uint8)
+    buf, offs, slot = b.to_host()
+    v, _, _ = orc.process_swipes(chain, regs, slot.astype(np.uint32), buf, offs)
+    assert np.array_equal(out.to_host(np.uint8, b.n), v)
+    assert np.array_equal(engine.registers_all(w.n_keys), regs)
+
+
 def test_hll_reserve_refused_while_graph_alive(engine):
     from rtsas_amd._lib import SketchLibError, SKE_EBUSY
     from rtsas_amd.engine import DeviceBuffer
