@@ -218,7 +218,7 @@ def cpu_baseline(orc, chain, w, b0, seconds, key_name):
                                            "(attendance_processor.py:100-137 without transport)"}}
 
 
-def verify(engine, orc, chain, w, km, rank, world, dist, dev, exchange):
+def verify(engine, orc, chain, w, km, rank, world, dist, dev, exchange, prefix="VERIFY", under=None):
     """The shipped multi-GPU classes on a verification stream, against the
     CPU oracle over the WHOLE stream (no collective on the expected side).
 
@@ -229,15 +229,17 @@ def verify(engine, orc, chain, w, km, rank, world, dist, dev, exchange):
     routing by owner()); --exchange: each rank hands its slice of the stream
     to distributed.SwipeExchange.  Then distributed.ShardedSketch, over a
     client that KeyMap.bind named, answers union PFCOUNT, PFCOUNT of every key
-    and a rollup (RCCL at N > 1)."""
+    and a rollup (RCCL at N > 1).  `under`: a KeyMap whose slots the
+    verification keys go above (default: the workload's)."""
     import numpy as np
     import torch
     import rtsas_amd
     from rtsas_amd import synthetic
     from rtsas_amd.distributed import KeyMap, ShardedSketch, SwipeExchange, engine_k1
     from rtsas_amd.engine import DeviceBatch, DeviceBuffer
-    names = [f"hll:unique:VERIFY{j:03d}:2025-10-03" for j in range(VERIFY_KEYS)]
-    vk = KeyMap(names, world, base=[km.slots_end(r) for r in range(world)])
+    names = [f"hll:unique:{prefix}{j:03d}:2025-10-03" for j in range(VERIFY_KEYS)]
+    under = km if under is None else under
+    vk = KeyMap(names, world, base=[under.slots_end(r) for r in range(world)])
     engine.hll_reserve(vk.slots_end(rank))
     client = rtsas_amd.SketchClient(context=engine.ctx)
     vk.bind(client, rank)
@@ -286,6 +288,7 @@ def verify(engine, orc, chain, w, km, rank, world, dist, dev, exchange):
                       device=dev if dist.is_initialized() and dist.get_backend() == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    verify.last_map = vk
     return {"ok": bool(ok.item()), "stream_swipes": n, "keys": VERIFY_KEYS, "keys_owned": int(mine.size),
             "input": "SwipeExchange slice" if exchange else "owner-routed",
             "answers": ok_answers, "owned_registers": ok_regs,
@@ -707,8 +710,14 @@ def main():
         orc = ge.load_oracle()
         chain = oracle_chain(run.engine, orc, run.w, run.p)
         if not args.no_check:
-            line["check"] = verify(run.engine, orc, chain, run.w, run.km, rank, world, dist, dev,
-                                   bool(args.exchange))
+            chk = verify(run.engine, orc, chain, run.w, run.km, rank, world, dist, dev, bool(args.exchange))
+            if world > 1 and not args.exchange:
+                # the unpartitioned-input path too (SwipeExchange: alltoallv over
+                # RCCL at N > 1) on a third key universe, then the same queries
+                x = verify(run.engine, orc, chain, run.w, run.km, rank, world, dist, dev, True,
+                           prefix="VERIFYX", under=verify.last_map)
+                chk = {**chk, "ok": chk["ok"] and x["ok"], "exchange": x}
+            line["check"] = chk
         if want_cpu:
             line["cpu_baseline"] = cpu_baseline(orc, chain, run.w, run.batches[0], args.cpu_seconds,
                                                 lambda s: run.names[int(run.km.keys_of(0)[s])])
