@@ -871,9 +871,10 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
         return SKE_OK;
     }
     if (!strcmp(name, "pa_grid")) {  // partitioned K1: pass A blocks per CU (0 = default); fail-list
-                                     // pass A of <= 511 slices: 3 three blocks per CU on a small
-                                     // counter table, 4 that table at two blocks per CU; < 320
-                                     // slices: 5 the counters in 16 copies (k_part_a4)
+                                     // pass A of <= 511 slices: 0 / 4 a 512-entry counter table at
+                                     // two blocks per CU, 3 that table at three blocks per CU, 2 the
+                                     // 2048-entry table; < 320 slices: 5 the counters in 16 copies
+                                     // (k_part_a4); A/B in DESIGN.md §3
         if (value < 0 || value > 5) return SKE_EINVAL;
         c->pa_grid = int(value);
         return SKE_OK;

@@ -36,7 +36,8 @@ namespace ske {
 #endif
 template <int BIT> __device__ __forceinline__ constexpr int k1_aux() { return (SKE_K1_NT & BIT) ? 2 : 0; }
 // SKE_K1_ABLATE (diagnostic builds only, registers may be wrong): 1 a raise is a
-// plain byte store instead of the CAS (prices the atomics' round trips)
+// plain byte store instead of the CAS (prices the atomics' round trips), 2 the
+// CAS issued without using its return value (no settle)
 #ifndef SKE_K1_ABLATE
 #define SKE_K1_ABLATE 0
 #endif
@@ -348,25 +349,9 @@ __device__ __forceinline__ void k1_probe(const K1Args &A, const lds_u8 *img, K1H
 // tile's hash and probes, so the atomic's round trip to memory is hidden.
 // The pre-check may be stale, never too high (registers only grow): a stale
 // word makes the CAS fail, and k1_settle finishes the byte max in a loop.
-//
-// The answers are stored first, by instructions every wave issues (an empty
-// range when the call has no answer array): vmcnt counts memory operations in
-// issue order, and the compiler counts only the operations every path issues,
-// so the next tile's last id-word load -- issued just before this commit and
-// waited for in the next hash -- must be followed by unconditional operations
-// before the (exec-branched) CASes.  With the CASes right behind it, that wait
-// drained them: every tile that raised a register waited for its CAS's
-// memory-side round trip right after issuing it (the cold-slab C2 steps).
 template <bool kHll, int U>
 __device__ __forceinline__ void k1_commit(const K1Args &A, const K1View &V, const K1Hot<U> &h,
                                           const uint32_t *valid, K1Pend<U> &pd) {
-    {
-        const __amdgpu_buffer_rsrc_t r_out = k1_rsrc(V.out, V.out ? V.n : 0u);
-#pragma unroll
-        for (int u = 0; u < U; u++)  // lanes past the chunk store out of range (dropped)
-            __builtin_amdgcn_raw_buffer_store_b8(uint8_t(valid[u]), r_out, h.act[u] ? h.idx[u] : 0xffffffffu,
-                                                 0, k1_aux<4>());
-    }
     if constexpr (kHll) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -381,11 +366,20 @@ __device__ __forceinline__ void k1_commit(const K1Args &A, const K1View &V, cons
             pd.sh[u] = h.sh[u];
             if constexpr ((SKE_K1_ABLATE & 1) != 0) {
                 if (need) reinterpret_cast<uint8_t *>(h.w[u])[h.sh[u] >> 3] = uint8_t(h.rank[u]);
+            } else if constexpr ((SKE_K1_ABLATE & 2) != 0) {  // the CAS without its return (no settle)
+                if (need) (void)atomicCAS(h.w[u], h.cur[u], (h.cur[u] & ~(0xffu << h.sh[u])) | (h.rank[u] << h.sh[u]));
             } else if (need) {
                 pd.prev[u] = atomicCAS(h.w[u], h.cur[u],
                                        (h.cur[u] & ~(0xffu << h.sh[u])) | (h.rank[u] << h.sh[u]));
             }
         }
+    }
+    if (V.out) {
+        const __amdgpu_buffer_rsrc_t r_out = k1_rsrc(V.out, V.n);
+#pragma unroll
+        for (int u = 0; u < U; u++)  // lanes past the chunk store out of range (dropped)
+            __builtin_amdgcn_raw_buffer_store_b8(uint8_t(valid[u]), r_out, h.act[u] ? h.idx[u] : 0xffffffffu,
+                                                 0, k1_aux<4>());
     }
 }
 

@@ -1887,7 +1887,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             else if (flist && A.nslices < 512 && a_grid == 3)  // small counter table: three blocks per CU
                 hipLaunchKernelGGL((k_part_a3<11, 512, 512, 3>), dim3(unsigned(cus) * 3 / kPGroups * kPGroups), dim3(512),
                                    0, st, A);
-            else if (flist && A.nslices < 512 && a_grid == 4)  // small counter table, two blocks per CU (A/B)
+            else if (flist && A.nslices < 512 && (a_grid == 0 || a_grid == 4))  // small counter table, two blocks per CU
                 hipLaunchKernelGGL((k_part_a3<11, 512, 512, 2>), dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(512),
                                    0, st, A);
             else if (flist)
