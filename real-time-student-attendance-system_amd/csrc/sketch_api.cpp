@@ -90,6 +90,10 @@ struct ske_ctx {
     int pa_threads = 512;   // fail-list pass A (k_part_a3) threads per 1024-swipe tile: 512 or 1024
     int part_overlap = 0;   // many-batch calls: partitioned K1 pass C on a side stream (measured slower)
     hipEvent_t part_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // part_overlap 3: CU-masked streams, [0] pass A on the CUs pass C does not
+    // use, [1] pass C on part_ccus CUs (every (cus / part_ccus)-th CU)
+    hipStream_t cu_st[2] = {nullptr, nullptr};
+    int part_ccus = 64, cu_st_ccus = 0;
     bool lds_ok = false;
     bool k1_ok = false;       // short-id LDS K1 (sketch_k1.hip) usable
     int k1_legacy = 0;        // 1: always the generic LDS kernel (A/B diagnostics)
@@ -558,7 +562,22 @@ int launch_part(ske_ctx *c, const ChainDev &ch, const PartBatch *bt, uint32_t nb
     if (nmax == 0) return SKE_OK;
     hipError_t e = part_reserve(ch, nmax, c->part_sub, c->scratch);
     if (e != hipSuccess) return scratch_error(c, e);
-    hipStream_t side = nullptr;
+    hipStream_t side = nullptr, side_a = nullptr;
+    const bool cu_split = pipelined && c->part_overlap == 3;
+    if (cu_split && (!c->cu_st[0] || c->cu_st_ccus != c->part_ccus)) {
+        for (hipStream_t &x : c->cu_st)
+            if (x) {
+                (void)hipStreamDestroy(x);
+                x = nullptr;
+            }
+        const int step = c->cus / c->part_ccus;
+        const uint32_t nw = uint32_t((c->cus + 31) / 32);
+        std::vector<uint32_t> ma(nw, 0), mc(nw, 0);
+        for (int i = 0; i < c->cus; i++) ((i % step == 0) ? mc : ma)[i / 32] |= 1u << (i % 32);
+        HIPCHK(c, hipExtStreamCreateWithCUMask(&c->cu_st[0], nw, ma.data()));
+        HIPCHK(c, hipExtStreamCreateWithCUMask(&c->cu_st[1], nw, mc.data()));
+        c->cu_st_ccus = c->part_ccus;
+    }
     if (pipelined) {
         if (c->many_n < 1) {
             HIPCHK(c, hipStreamCreateWithFlags(&c->many_st[0], hipStreamNonBlocking));
@@ -568,6 +587,10 @@ int launch_part(ske_ctx *c, const ChainDev &ch, const PartBatch *bt, uint32_t nb
         for (int i = 0; i < 4; i++)
             if (!c->part_ev[i]) HIPCHK(c, hipEventCreateWithFlags(&c->part_ev[i], hipEventDisableTiming));
         side = c->many_st[0];
+        if (cu_split) {
+            side_a = c->cu_st[0];
+            side = c->cu_st[1];
+        }
     }
     unsigned long long cid = 0;
     int rc = scratch_user_begin(c, &cid);
@@ -592,7 +615,8 @@ int launch_part(ske_ctx *c, const ChainDev &ch, const PartBatch *bt, uint32_t nb
     };
     c->hook_arg = &hs;
     e = launch_swipes_part(ch, bt, nb, c->regs, c->nslots, c->scratch, c->err, c->cus, c->part_sub, c->hll_mode,
-                           c->pb_pairs, c->pa_tile, c->pa_pre, pipelined ? c->part_overlap : 0, c->pa_grid, c->st, side, c->part_ev, c->timing && !c->capturing ? +hook : nullptr, c, c->pa_threads);
+                           c->pb_pairs, c->pa_tile, c->pa_pre, pipelined ? c->part_overlap : 0, c->pa_grid, c->st, side, c->part_ev, c->timing && !c->capturing ? +hook : nullptr, c, c->pa_threads,
+                           side_a, cu_split ? c->cus / (c->cus / c->part_ccus) : 0);
     if (e != hipSuccess) {
         c->last_hip = std::string("launch_swipes_part: ") + hipGetErrorString(e);
         scratch_user_end(c, cid);
@@ -730,6 +754,8 @@ int ske_close(ske_ctx *c) {
         (void)hipEventDestroy(c->many_join[i]);
     }
     if (c->many_fork) (void)hipEventDestroy(c->many_fork);
+    for (hipStream_t x : c->cu_st)
+        if (x) (void)hipStreamDestroy(x);
     for (hipEvent_t e : c->part_ev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->chunk_ev) (void)hipEventDestroy(e);
@@ -850,9 +876,15 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
         c->hll_mode = int(value);
         return SKE_OK;
     }
-    if (!strcmp(name, "part_overlap")) {  // many-batch calls: pass C beside the next B (1) or A (2)
-        if (value < 0 || value > 2) return SKE_EINVAL;
+    if (!strcmp(name, "part_overlap")) {  // many-batch calls: pass C beside the next B (1) or A (2),
+                                          // or beside the next A on CU-partitioned streams (3)
+        if (value < 0 || value > 3) return SKE_EINVAL;
         c->part_overlap = int(value);
+        return SKE_OK;
+    }
+    if (!strcmp(name, "part_ccus")) {  // part_overlap 3: CUs given to pass C (a divisor of the CU count)
+        if (value < 8 || value > c->cus / 2 || c->cus % value) return SKE_EINVAL;
+        c->part_ccus = int(value);
         return SKE_OK;
     }
     if (!strcmp(name, "pa_tile")) {  // partitioned K1 tile: log2 swipes, 10 or 11

@@ -150,12 +150,15 @@ struct PartBatch {
     uint64_t n;
     uint8_t *out;          // may be nullptr
 };
-// side == nullptr: every pass on st; else pass C on `side` (ev: 4 events)
+// side == nullptr: every pass on st; else pass C on `side` (ev: 4 events);
+// ovl 3: pass A on `side_a`, B on st, C on `side` (CU-masked streams: C on
+// c_cus CUs, A on the others)
 hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t nb, uint8_t *regs,
                               uint32_t nslots, Scratch *scr, unsigned int *err, int cus, uint32_t sub,
                               int hll_mode, int pb_pairs, int tile_opt, int pre_opt, int ovl, int a_grid, hipStream_t st, hipStream_t side,
                               hipEvent_t *ev,
-                              PassHook hook = nullptr, void *hook_user = nullptr, int a3_threads = 512);
+                              PassHook hook = nullptr, void *hook_user = nullptr, int a3_threads = 512,
+                              hipStream_t side_a = nullptr, int c_cus = 0);
 
 
 // sketch_order.hip -- order-exact paths (replies that depend on item order)

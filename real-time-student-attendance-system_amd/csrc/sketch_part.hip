@@ -1755,6 +1755,8 @@ static hipError_t part_scratch_c(PartArgs *A, uint32_t m, int set, Scratch *scr)
     A->fail = (uint8_t *)scratch_get(scr, 38, size_t(A->fail_stride) * A->nlinks, &e);
     if (e == hipSuccess) A->hllw = (uint32_t *)scratch_get(scr, 39, size_t(m) * 4, &e);
     if (e == hipSuccess) A->oldw = (uint32_t *)scratch_get(scr, 43, size_t(m) * 4, &e);
+    if (e == hipSuccess && A->nlinks == 1)
+        A->flist = (uint16_t *)scratch_get(scr, 45, size_t(A->nunits) * A->fl_stride * kPbLanes * 2, &e);
     return e;
 }
 
@@ -1782,7 +1784,8 @@ hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratc
 hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t nb, uint8_t *regs,
                               uint32_t nslots, Scratch *scr, unsigned int *err, int cus, uint32_t sub_opt,
                               int hll_mode, int pb_pairs, int tile_opt, int pre_opt, int ovl, int a_grid, hipStream_t st, hipStream_t side,
-                              hipEvent_t *ev, PassHook hook, void *hook_user, int a3_threads) {
+                              hipEvent_t *ev, PassHook hook, void *hook_user, int a3_threads,
+                              hipStream_t side_a, int c_cus) {
     PartArgs A{};
     if (!part_plan(ch, &A)) return hipErrorInvalidValue;
     const uint32_t sub = part_sub(sub_opt);
@@ -1794,10 +1797,16 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
     // (set 1 too, even when not pipelined: see part_reserve)
     uint8_t *fail0 = A.fail;
     uint32_t *hllw0 = A.hllw, *oldw0 = A.oldw;
+    uint16_t *flist0 = A.flist;
     e = part_scratch_c(&A, uint32_t(nmax < sub ? nmax : sub), 1, scr);
     if (e != hipSuccess) return e;
     uint8_t *fail1 = A.fail;
     uint32_t *hllw1 = A.hllw, *oldw1 = A.oldw;
+    uint16_t *flist1 = A.flist;
+    A.flist = flist0;
+    // ovl 3: pass A of unit u + 1 on side_a (the CUs pass C does not use)
+    // beside pass C of unit u on side (c_cus CUs); pass B on st, alone
+    const bool split = side && side_a && ovl == 3 && c_cus > 0 && c_cus < cus;
     A.regs = regs;
     A.nslots = nslots;
     A.err = err;
@@ -1815,8 +1824,8 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
     // pass B -> C through fail lists (pb_pairs 2): one-link chains probed in
     // slice pairs over 1024-swipe tiles, PFADD by CAS from pass C's own
     // pre-check, passes in stream order (the lists are one buffer)
-    const bool flist = pb_pairs == 2 && one11 && A.tile_log == 10 && hll_mode == 0 && !A.pre && !side &&
-                       A.flist != nullptr;
+    const bool flist = pb_pairs == 2 && one11 && A.tile_log == 10 && hll_mode == 0 && !A.pre && (!side || split) &&
+                       A.flist != nullptr && (!split || flist1 != nullptr);
     const uint32_t tile = 1u << A.tile_log;
 #define SKE_CK(x)                        \
     do {                                 \
@@ -1842,7 +1851,8 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             hipLaunchKernelGGL(k_part_hd, dim3(unsigned(cus) * 2), dim3(1024), 0, sc, H);
             hipLaunchKernelGGL(k_part_he, dim3(unsigned(cus) * 2), dim3(kHeBlock), 0, sc, P, H);
         } else if (flist) {
-            const unsigned gc = (part_grid(ms, 1024 * kPbGroup, cus * 8) + kPGroups - 1) / kPGroups * kPGroups;
+            const unsigned gc = (part_grid(ms, 1024 * kPbGroup, (split ? c_cus : cus) * 8) + kPGroups - 1) / kPGroups *
+                                kPGroups;
             hipLaunchKernelGGL(k_part_c_fl<4>, dim3(gc), dim3(kPcBlock), 0, sc, P);
         } else {
             const unsigned gc = (part_grid(ms, kPcBlock * 2, cus * 8) + kPGroups - 1) / kPGroups * kPGroups;
@@ -1866,6 +1876,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             A.fail = set ? fail1 : fail0;
             A.hllw = set ? hllw1 : hllw0;
             A.oldw = set ? oldw1 : oldw0;
+            if (split) A.flist = set ? flist1 : flist0;
             A.fixed_w = B.fixed_w;
             A.n = ms;
             A.ntiles = (ms + tile - 1) / tile;
@@ -1874,38 +1885,51 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             A.slot = B.slot + s0;
             A.out = B.out ? B.out + s0 : nullptr;
             // pass C of unit u - 2 was the last reader of this scratch set
-            if (side && u >= 2) SKE_CK(hipStreamWaitEvent(st, ev[2 + set], 0));
+            hipStream_t sa = st;  // pass A's stream
+            if (split) {
+                // after the work before this call (u = 0) or pass B of unit u - 1
+                // (the probe records and run table), and pass C of unit u - 2
+                sa = side_a;
+                if (u == 0) SKE_CK(hipEventRecord(ev[1], st));
+                SKE_CK(hipStreamWaitEvent(sa, ev[1], 0));
+                if (u >= 2) SKE_CK(hipStreamWaitEvent(sa, ev[2 + set], 0));
+            } else if (side && u >= 2) {
+                SKE_CK(hipStreamWaitEvent(st, ev[2 + set], 0));
+            }
+            const unsigned acus = unsigned(split ? cus - c_cus : cus);
             const unsigned per_cu = km <= 11 ? (a_grid ? unsigned(a_grid) : 2u) : 1;
             const unsigned ga = unsigned(cus) * per_cu / kPGroups * kPGroups;  // blocks past a group's tiles exit
-            if (hook) hook(hook_user, 0, 0, st);
+            if (hook) hook(hook_user, 0, 0, sa);
             if (flist && a3_threads == 1024)  // the fail-list path's own record format (k_part_a3 -> k_part_b<2, 4, true>)
-                hipLaunchKernelGGL((k_part_a3<11, 1024>), dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(1024), 0,
-                                   st, A);
+                hipLaunchKernelGGL((k_part_a3<11, 1024>), dim3(acus * 2 / kPGroups * kPGroups), dim3(1024), 0, sa, A);
             else if (flist && A.nslices < 320 && a_grid == 5)  // slice counters in 16 copies
-                hipLaunchKernelGGL((k_part_a4<11, 512, 320>), dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(512), 0,
-                                   st, A);
+                hipLaunchKernelGGL((k_part_a4<11, 512, 320>), dim3(acus * 2 / kPGroups * kPGroups), dim3(512), 0, sa, A);
             else if (flist && A.nslices < 512 && a_grid == 3)  // small counter table: three blocks per CU
-                hipLaunchKernelGGL((k_part_a3<11, 512, 512, 3>), dim3(unsigned(cus) * 3 / kPGroups * kPGroups), dim3(512),
-                                   0, st, A);
+                hipLaunchKernelGGL((k_part_a3<11, 512, 512, 3>), dim3(acus * 3 / kPGroups * kPGroups), dim3(512), 0, sa,
+                                   A);
             else if (flist && A.nslices < 512 && (a_grid == 0 || a_grid == 4))  // small counter table, two blocks per CU
-                hipLaunchKernelGGL((k_part_a3<11, 512, 512, 2>), dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(512),
-                                   0, st, A);
+                hipLaunchKernelGGL((k_part_a3<11, 512, 512, 2>), dim3(acus * 2 / kPGroups * kPGroups), dim3(512), 0, sa,
+                                   A);
             else if (flist)
-                hipLaunchKernelGGL((k_part_a3<11, 512>), dim3(unsigned(cus) * 2 / kPGroups * kPGroups), dim3(512), 0, st, A);
+                hipLaunchKernelGGL((k_part_a3<11, 512>), dim3(acus * 2 / kPGroups * kPGroups), dim3(512), 0, sa, A);
             else if (one11 && A.tile_log == 11)  // RESERVE 0.001 (C3/C5): one link, k = 11
                 hipLaunchKernelGGL((k_part_a2<11, 1024>), dim3(unsigned(cus) / kPGroups * kPGroups), dim3(1024),
-                                   0, st, A);
+                                   0, sa, A);
             else if (one11 && A.pre)
                 hipLaunchKernelGGL((k_part_a2<11, kA2Threads, 2, true>),
-                                   dim3(unsigned(cus) * per_cu / kPGroups * kPGroups), dim3(kA2Threads), 0, st, A);
+                                   dim3(unsigned(cus) * per_cu / kPGroups * kPGroups), dim3(kA2Threads), 0, sa, A);
             else if (one11)
                 hipLaunchKernelGGL((k_part_a2<11>), dim3(unsigned(cus) * per_cu / kPGroups * kPGroups),
-                                   dim3(kA2Threads), 0, st, A);
+                                   dim3(kA2Threads), 0, sa, A);
             else if (km <= 11)
-                hipLaunchKernelGGL(k_part_a<11>, dim3(ga), dim3(kPaBlock), 0, st, A);
+                hipLaunchKernelGGL(k_part_a<11>, dim3(ga), dim3(kPaBlock), 0, sa, A);
             else
-                hipLaunchKernelGGL(k_part_a<22>, dim3(ga), dim3(kPaBlock), 0, st, A);
-            if (hook) hook(hook_user, 0, 1, st);
+                hipLaunchKernelGGL(k_part_a<22>, dim3(ga), dim3(kPaBlock), 0, sa, A);
+            if (hook) hook(hook_user, 0, 1, sa);
+            if (split) {  // pass B behind pass A
+                SKE_CK(hipEventRecord(ev[0], sa));
+                SKE_CK(hipStreamWaitEvent(st, ev[0], 0));
+            }
             if (side && ovl == 1 && have_prev) {  // C(u - 1) behind A(u) (and so behind B(u - 1))
                 SKE_CK(hipEventRecord(ev[set], st));
                 SKE_CK(hipStreamWaitEvent(side, ev[set], 0));
@@ -1927,7 +1951,13 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             else
                 hipLaunchKernelGGL(k_part_b<1>, dim3(gb), dim3(kPbBlock), 0, st, A);
             if (hook) hook(hook_user, 1, 1, st);
-            if (side && ovl == 2) {  // C(u) behind B(u), beside A(u + 1)
+            if (split) {  // C(u) behind B(u), beside A(u + 1) on the other CUs
+                SKE_CK(hipEventRecord(ev[1], st));
+                SKE_CK(hipStreamWaitEvent(side, ev[1], 0));
+                SKE_CK(launch_c(A, ms, side));
+                SKE_CK(hipEventRecord(ev[2 + set], side));
+                have_prev = true;
+            } else if (side && ovl == 2) {  // C(u) behind B(u), beside A(u + 1)
                 SKE_CK(hipEventRecord(ev[set], st));
                 SKE_CK(hipStreamWaitEvent(side, ev[set], 0));
                 SKE_CK(launch_c(A, ms, side));
@@ -1943,7 +1973,9 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             SKE_CK(hipGetLastError());
         }
     }
-    if (side && ovl == 2 && have_prev) {  // join the last unit's pass C
+    if (split && have_prev) {  // join the last unit's pass C (and so every pass before it)
+        SKE_CK(hipStreamWaitEvent(st, ev[2 + int((u - 1) & 1)], 0));
+    } else if (side && ovl == 2 && have_prev) {  // join the last unit's pass C
         SKE_CK(hipStreamWaitEvent(st, ev[2 + int((u - 1) & 1)], 0));
     } else if (side && have_prev) {  // the last unit's pass C behind its pass B, then join
         const int set = int((u - 1) & 1);

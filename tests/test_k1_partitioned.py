@@ -279,12 +279,15 @@ def test_partitioned_hot_register_and_many_keys(engine, orc, hll_mode, pa_tile, 
     assert np.array_equal(engine.registers_all(40_001), regs)
 
 
-@pytest.mark.parametrize("mode,ovl,pre", [("direct", 1, 0), ("graph", 1, 0), ("direct", 2, 0), ("graph", 2, 1),
-                                          ("direct", 2, 1)])
-def test_many_pipelined_small_units(engine, orc, mode, ovl, pre):
+@pytest.mark.parametrize("mode,ovl,pre,ccus", [("direct", 1, 0, 0), ("graph", 1, 0, 0), ("direct", 2, 0, 0),
+                                               ("graph", 2, 1, 0), ("direct", 2, 1, 0), ("direct", 3, 0, 0),
+                                               ("graph", 3, 0, 0), ("direct", 3, 0, 32)])
+def test_many_pipelined_small_units(engine, orc, mode, ovl, pre, ccus):
     """ske_swipes_many_async through the partitioned K1 with pass C of every
     unit on a side stream beside the next unit's pass B (option part_overlap
-    1) or its pass A (2), with or without the pass-A register pre-check:
+    1) or its pass A (2; 3: on CU-masked streams, pass C on `part_ccus` CUs,
+    pass A on the rest, fail lists double-buffered), with or without the
+    pass-A register pre-check:
     sub-batches of
     64k swipes make ~25 units over 7 ragged batches (incl. 1 swipe and a
     partial tile), so the two scratch sets alternate many times; answers and
@@ -295,6 +298,8 @@ def test_many_pipelined_small_units(engine, orc, mode, ovl, pre):
     engine.set_option("part_sub", 65536)
     engine.set_option("part_overlap", ovl)
     engine.set_option("pa_precheck", pre)
+    if ccus:
+        engine.set_option("part_ccus", ccus)
     sizes = [300_000, 1, 70_001, 300_000, 250_000, 2048, 400_000]
     bs, start = [], 0
     for n in sizes:
