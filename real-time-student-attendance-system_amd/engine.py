@@ -177,13 +177,12 @@ class SketchEngine:
         self.ctx.call("ske_swipes_fixed_async", fid, C.c_void_p(b.slot.ptr),
                       C.c_void_p(b.bytes.ptr), b.width, b.n, C.c_void_p(out.ptr) if out else None)
 
-    def swipes_many_async(self, fid: int, batches, outs=None, branches: int = 0,
-                          fixed: bool = False):
-        """Enqueue K1 over several resident batches in one native call
-        (ske_swipes_many_async): batch j on branch j mod `branches` (0: 16),
-        forked from and joined back into the context stream; with several
-        branches two launches share the chip, half the CUs each.  `fixed`:
-        read the ids as fixed-width (as swipes_fixed_async)."""
+    @staticmethod
+    def many_args(batches, outs=None, fixed: bool = False):
+        """The ske_swipe_batch array of a many-batch call, built once: a
+        caller that replays the same batches (a serving loop over resident
+        buffers, the benchmark) passes it as `prepared` and skips the
+        per-call Python marshalling."""
         outs = outs if outs is not None else [None] * len(batches)
         arr = (SweBatch * len(batches))()
         for a, b, o in zip(arr, batches, outs):
@@ -192,8 +191,18 @@ class SketchEngine:
             a.width = b.width if fixed else 0
             a.n = b.n
             a.out_valid = o.ptr if o is not None else None
-        self.ctx.call("ske_swipes_many_async", fid, C.cast(arr, C.c_void_p), len(batches),
-                      branches)
+        return arr
+
+    def swipes_many_async(self, fid: int, batches, outs=None, branches: int = 0,
+                          fixed: bool = False, prepared=None):
+        """Enqueue K1 over several resident batches in one native call
+        (ske_swipes_many_async): batch j on branch j mod `branches` (0: 16),
+        forked from and joined back into the context stream; with several
+        branches two launches share the chip, half the CUs each.  `fixed`:
+        read the ids as fixed-width (as swipes_fixed_async).  `prepared`: the
+        many_args() array of these batches."""
+        arr = prepared if prepared is not None else self.many_args(batches, outs, fixed)
+        self.ctx.call("ske_swipes_many_async", fid, C.cast(arr, C.c_void_p), len(arr), branches)
 
     def swipes_stats(self, fid: int, b: DeviceBatch) -> tuple[int, int]:
         probes, nvalid = C.c_uint64(), C.c_uint64()
