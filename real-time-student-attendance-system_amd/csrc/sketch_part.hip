@@ -484,6 +484,7 @@ __global__ void __launch_bounds__(kA2Threads, kA2Threads == 1024 ? 1 : 2) k_part
 #ifndef SKE_A3_ABLATE
 #define SKE_A3_ABLATE 0
 #endif
+constexpr uint32_t kOORa = 0x80000000u;  // a buffer offset past every range: load 0, store dropped
 template <int KM, uint32_t kT = 512, uint32_t kCnt = kPMaxSlices + 1, int kMinBlocks = 2>
 __global__ void __launch_bounds__(kT, kMinBlocks * kT / 256) k_part_a3(const PartArgs A) {  // waves per SIMD
     // kCnt: counters per tile parity (slices + the past-the-batch sink); 512
@@ -500,11 +501,23 @@ __global__ void __launch_bounds__(kT, kMinBlocks * kT / 256) k_part_a3(const Par
     const uint32_t S = A.nslices;
     for (uint32_t c = tid; c < 2 * kCnt; c += kT) cnt[c] = c << 18;
     lds_barrier();
+    // Every global load and store below is issued by every wave the same
+    // number of times (buffer operations; a lane or a whole call with nothing
+    // to move gives an offset past the range): vmcnt counts in issue order and
+    // the compiler counts only what every path issues, so with a conditional
+    // store between a load and its use the wait for the load also waited for
+    // the stores (the copy-out's memory round trip, once per tile).
+    const __amdgpu_buffer_rsrc_t roffs = part_rsrc(A.offs, A.offs ? (A.n + 1) * 4 : 0u);
+    const __amdgpu_buffer_rsrc_t rhllw = part_rsrc(A.hllw, A.n * 4);
+    const __amdgpu_buffer_rsrc_t rfail0 = part_rsrc(A.fail, A.n);
+    const __amdgpu_buffer_rsrc_t roff = part_rsrc(A.off, (A.nslices + 1) * A.off_stride * 4);
     auto offsets = [&](uint32_t t, uint32_t u, uint32_t &b, uint32_t &e) {
         const uint32_t i = t * kTile + u * kT + tid;
         const uint32_t ic = i < A.n ? i : A.n - 1;
-        b = A.offs ? nt_ld<2>(A.offs + ic) : ic * A.fixed_w;
-        e = A.offs ? nt_ld<2>(A.offs + ic + 1) : b + A.fixed_w;
+        const uint32_t lb = __builtin_amdgcn_raw_buffer_load_b32(roffs, ic * 4, 0, nt_aux<2>());
+        const uint32_t le = __builtin_amdgcn_raw_buffer_load_b32(roffs, ic * 4 + 4, 0, nt_aux<2>());
+        b = A.offs ? lb : ic * A.fixed_w;
+        e = A.offs ? le : b + A.fixed_w;
     };
     uint32_t gt0, gt1;
     part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
@@ -538,11 +551,11 @@ __global__ void __launch_bounds__(kT, kMinBlocks * kT / 256) k_part_a3(const Par
             const bool act = i < A.n;
             uint64_t ha, hb, hh;
             part_hash3(A.bytes, it[u], ha, hb, hh);
-            if (act) {
+            {
                 uint32_t idx, rank;
                 hll_patlen(hh, idx, rank);
-                nt_st<8>(A.hllw + i, idx | (rank << 16));
-                nt_st<8>(A.fail + i, uint8_t(0));
+                __builtin_amdgcn_raw_buffer_store_b32(idx | (rank << 16), rhllw, act ? i * 4 : kOORa, 0, nt_aux<8>());
+                __builtin_amdgcn_raw_buffer_store_b8(uint8_t(0), rfail0, act ? i : kOORa, 0, nt_aux<8>());
             }
             const uint32_t lu20 = lu << 20;
             ProbeWalk32 wk;
@@ -598,7 +611,8 @@ __global__ void __launch_bounds__(kT, kMinBlocks * kT / 256) k_part_a3(const Par
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
             const uint32_t g = tid * kPer + j, c = cb + g;
-            if (g <= S) A.off[size_t(g) * A.off_stride + t] = run;  // run starts (pass B)
+            __builtin_amdgcn_raw_buffer_store_b32(run, roff, g <= S ? (g * A.off_stride + t) * 4 : kOORa, 0,
+                                                  0);  // run starts (pass B)
             if (g == S) stot = run;
             cnt[c] = 4 * run - (c << 18);
             run += v[j];
@@ -631,9 +645,19 @@ __global__ void __launch_bounds__(kT, kMinBlocks * kT / 256) k_part_a3(const Par
         for (uint32_t g = tid; g <= S; g += kT) cnt[nb + g] = (nb + g) << 18;
         lds_barrier();
         const uint32_t total = (SKE_A3_ABLATE & 3) ? 0u : (SKE_A3_ABLATE & 24) ? min(stot, kTile * KM) : stot;
-        part_u32x4 *dst = reinterpret_cast<part_u32x4 *>(A.rec + size_t(t) * A.stride);
+        // a fixed number of 16-B pieces per thread (the last ones past the
+        // tile's total go out of range); the LDS reads past the records stay
+        // inside the block's allocation (the counter table follows srec)
+        const __amdgpu_buffer_rsrc_t rdst = part_rsrc(A.rec + size_t(t) * A.stride, A.stride * 4);
         const part_u32x4 *src = reinterpret_cast<const part_u32x4 *>(srec);
-        for (uint32_t j = tid; j * 4 < total; j += kT) nt_st<4>(dst + j, src[j]);
+        constexpr uint32_t kCo = (kTile * KM / 4 + kT - 1) / kT;
+        static_assert(kCo * kT * 16 <= sizeof(srec) + sizeof(cnt), "copy-out reads stay in the block's LDS");
+#pragma unroll
+        for (uint32_t c = 0; c < kCo; c++) {
+            const uint32_t j = c * kT + tid;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, src[j]),
+                                                   rdst, j * 4 < total ? j * 16 : kOORa, 0, nt_aux<4>());
+        }
     }
 }
 
