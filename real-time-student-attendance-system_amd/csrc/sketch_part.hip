@@ -1136,6 +1136,13 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
 // the run's tiles -- the next tile's fail bytes (list overflows), slots and
 // HLL words in flight while a tile's CASes are, every CAS of a tile issued
 // before any is settled.  Marks carry the run's index: nothing is cleared.
+// SKE_PC_FIXED 1: pass C's loads and stores at a fixed count per tile (as pass
+// A's); measured equal at C3 (0.408 vs 0.409 ms, three alternations,
+// profiles/r03_ab_pass_a_vmcnt.txt): pass C is bound by the memory side's
+// random requests, not by its waves' waits.  Default 0.
+#ifndef SKE_PC_FIXED
+#define SKE_PC_FIXED 0
+#endif
 template <int U>
 __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
     static_assert(kPcBlock * U == 1024, "one 1024-swipe tile per sub-step");
@@ -1151,6 +1158,26 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
     struct In {
         uint32_t fb[U], sl[U], hv[U];
     };
+#if SKE_PC_FIXED
+    // every global load and store of a tile is issued a fixed number of times
+    // (buffer operations out of range for lanes with nothing to move; the
+    // pre-check load of a lane without a register reads the slab's first
+    // word), so the wait for the next tile's streams does not also wait for
+    // this tile's answer stores (see k_part_a3)
+    const __amdgpu_buffer_rsrc_t rfb = part_rsrc(A.fail, A.n), rsl = part_rsrc(A.slot, A.n * 4),
+                                 rhv = part_rsrc(A.hllw, A.n * 4), rout = part_rsrc(A.out, A.out ? A.n : 0u);
+    auto load = [&](uint32_t t, uint32_t tend, In &in) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
+            const uint32_t oor = uint32_t(!(t < tend && i < A.n)) << 31;
+            const uint32_t fb = __builtin_amdgcn_raw_buffer_load_b8(rfb, i | oor, 0, nt_aux<16>());
+            in.fb[u] = oor ? 1u : fb;
+            in.sl[u] = __builtin_amdgcn_raw_buffer_load_b32(rsl, (i * 4) | oor, 0, nt_aux<16>());
+            in.hv[u] = __builtin_amdgcn_raw_buffer_load_b32(rhv, (i * 4) | oor, 0, nt_aux<16>());
+        }
+    };
+#else
     auto load = [&](uint32_t t, uint32_t tend, In &in) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -1161,6 +1188,7 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
             in.hv[u] = act ? nt_ld<16>(A.hllw + i) : 0u;
         }
     };
+#endif
     lds_barrier();
     for (uint32_t r0 = gt0 + (blockIdx.x / kPGroups) * kRun; r0 < gt1; r0 += nblk * kRun) {
         const uint32_t r1 = r0 + kRun < gt1 ? r0 + kRun : gt1;
@@ -1215,8 +1243,16 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
                     }
                 }
             }
+#if SKE_PC_FIXED
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t x = nt_ld<32>(w[u] ? w[u] : reinterpret_cast<uint32_t *>(A.regs));
+                cw[u] = w[u] ? x : 0xffffffffu;
+            }
+#else
 #pragma unroll
             for (int u = 0; u < U; u++) cw[u] = w[u] ? nt_ld<32>(w[u]) : 0xffffffffu;
+#endif
             // every raising CAS of the tile in flight at once, then settled
             // (a lost race retries from the word the CAS returned)
 #pragma unroll
@@ -1225,6 +1261,13 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
                 if (w[u] && ((cw[u] >> sh[u]) & 0xffu) < rank[u])
                     seen[u] = atomicCAS(w[u], cw[u], (cw[u] & ~(0xffu << sh[u])) | (rank[u] << sh[u]));
             }
+#if SKE_PC_FIXED
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
+                __builtin_amdgcn_raw_buffer_store_b8(uint8_t(valid[u]), rout, i < A.n ? i : kOOR, 0, nt_aux<16>());
+            }
+#else
             if (A.out) {
 #pragma unroll
                 for (int u = 0; u < U; u++) {
@@ -1232,6 +1275,7 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
                     if (i < A.n) nt_st<16>(A.out + i, uint8_t(valid[u]));
                 }
             }
+#endif
 #pragma unroll
             for (int u = 0; u < U; u++)
                 if (w[u] && seen[u] != cw[u]) part_reg_max(w[u], sh[u], rank[u], seen[u]);
