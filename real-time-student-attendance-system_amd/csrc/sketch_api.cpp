@@ -1593,6 +1593,11 @@ int ske_diag_set_stamp_buffer(ske_ctx *c, void *dev_ptr) {
     HIPCHK(c, ske::set_stamp_buffer(dev_ptr));
     return SKE_OK;
 }
+int ske_diag_set_pb_stamp_buffer(ske_ctx *c, void *dev_ptr) {
+    if (!c) return SKE_EINVAL;
+    HIPCHK(c, ske::set_pb_stamp_buffer(dev_ptr));
+    return SKE_OK;
+}
 int ske_diag_set_k1_stamp_buffer(ske_ctx *c, void *dev_ptr) {
     if (!c) return SKE_EINVAL;
     HIPCHK(c, ske::set_k1_stamp_buffer(dev_ptr));

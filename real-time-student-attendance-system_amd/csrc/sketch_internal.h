@@ -94,6 +94,7 @@ bool k1_lds_plan(const ChainDev &ch, K1Args *A);
 hipError_t launch_swipes_lds(const K1Args &A, bool hll, int tile, int cus, hipStream_t st);
 hipError_t k1_lds_setup();
 hipError_t set_k1_stamp_buffer(void *p);  // -DSKE_STAMPS diagnostic build only
+hipError_t set_pb_stamp_buffer(void *p);  // -DSKE_STAMPS diagnostic build only
 
 // sketch_ingest.hip -- JSON event decode and key-slot resolution (device columns)
 struct IngestCols {

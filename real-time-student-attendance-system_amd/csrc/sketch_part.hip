@@ -852,8 +852,35 @@ constexpr uint32_t kPbQueue = 64;  // compacted fail stores per wave and group
 // failures past a list's kPbLanes entries (Poisson(3.7) at C3: ~2 % of the
 // lists overflow) and those of the rare long runs keep the byte store; pass C
 // (k_part_c_fl) folds the lists of a tile into LDS flags.
+// Diagnostic block stamps of pass B (tools/stamps/run_pb_stamps.py; built only
+// with -DSKE_STAMPS, the product library has none): thread 0 of every block
+// records s_memrealtime (100 MHz) at entry and exit and the block's XCD into a
+// side buffer no output depends on.
+#ifdef SKE_STAMPS
+__device__ unsigned long long *ske_pb_stamp_buf;
+hipError_t set_pb_stamp_buffer(void *p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(ske_pb_stamp_buf), &p, sizeof(void *));
+}
+#define PB_STAMP(k)                                                                                    \
+    do {                                                                                               \
+        if ((k) == 1) __syncthreads();                                                                 \
+        __builtin_amdgcn_sched_barrier(0);                                                             \
+        unsigned long long t_;                                                                         \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
+        __builtin_amdgcn_sched_barrier(0);                                                             \
+        if (threadIdx.x == 0 && ske_pb_stamp_buf) {                                                    \
+            ske_pb_stamp_buf[blockIdx.x * 4 + (k)] = t_;                                               \
+            ske_pb_stamp_buf[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_getreg((3 << 11) | 20);         \
+        }                                                                                              \
+    } while (0)
+#else
+#define PB_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
 template <int SP, int R = 2 * SP, bool FL = false>  // R: 16-byte pieces per lane and run (runs of SP slices)
 __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const PartArgs A) {
+    PB_STAMP(0);
     const uint32_t tmask = (1u << A.tile_log) - 1;
     __shared__ __attribute__((aligned(16))) uint8_t img[kPSliceBytes * SP];
     __shared__ uint32_t fq[kPbBlock / 64][kPbQueue];
@@ -1049,6 +1076,7 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
             ec = e1;
         }
     }
+    PB_STAMP(1);
 }
 
 // ---------------------------------------------------------------------------
