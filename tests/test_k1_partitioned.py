@@ -68,6 +68,42 @@ def test_partitioned_two_link_chain_ragged(engine, orc, hll_mode):
     assert np.array_equal(engine.registers_all(37), regs)
 
 
+@pytest.mark.parametrize("hll_mode", [0, 1])
+def test_c3_geometry_ragged_long_ids(engine, orc, hll_mode):
+    """The one-link k = 11 chain of C3's RESERVE 0.001 / 1e7 (the fail-list
+    pass A k_part_a3 with CAS PFADD, or the line-owned PFADD) on ids of 0..40
+    bytes: empty ids and ids longer than 8 bytes take pass A's generic
+    MurmurHash64A; a ragged last tile; answers and registers == the oracle."""
+    from rtsas_amd.engine import DeviceBatch, DeviceBuffer
+    import ctypes as C
+    rng = np.random.default_rng(77)
+    members = _rand_items(rng, 40000, 40, 1)
+    engine.reserve(0, 0.001, 10_000_000)
+    mb, mo = _pack(members)
+    dm = DeviceBatch.from_host(engine.ctx, mb, mo, np.zeros(len(members), np.uint32))
+    engine.ctx.call("ske_bf_madd", 0, C.c_void_p(dm.bytes.ptr), C.c_void_p(dm.offs.ptr), len(members), None, 1)
+    chain = orc.Chain(10_000_000, 0.001)
+    chain.madd_packed(mb, mo)
+    assert chain.nlinks == 1 and chain.link_info(0)["hashes"] == 11
+    engine.set_option("hll_mode", hll_mode)
+    assert engine.variant(0) == 3
+    items = [members[int(i)] for i in rng.integers(0, len(members), 90000)]
+    items += _rand_items(rng, 30000, 40) + [b""] * 50 + [b"12345678", b"123456789"]
+    order = rng.permutation(len(items))
+    items = [items[int(i)] for i in order]
+    keys = rng.integers(0, 37, len(items)).astype(np.uint32)
+    buf, offs = _pack(items)
+    engine.hll_reserve(37)
+    b = DeviceBatch.from_host(engine.ctx, buf, offs, keys)
+    out = DeviceBuffer(engine.ctx, b.n)
+    engine.swipes(0, b, out)
+    regs = np.zeros((37, 16384), np.uint8)
+    valid, _, _ = orc.process_swipes(chain, regs, keys, buf, offs)
+    assert np.array_equal(out.to_host(np.uint8, b.n), valid)
+    assert np.array_equal(engine.registers_all(37), regs)
+    assert valid.sum() > 80000
+
+
 def _c3_small(engine, n_members=200_000):
     from rtsas_amd import synthetic
     w = synthetic.WORKLOADS["c3"]
