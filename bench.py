@@ -122,6 +122,9 @@ def parse(argv=None):
     ap.add_argument("--pass-replay", type=int, default=1,
                     help="1 = per-kernel times from an instrumented replay of the same steps "
                          "after the timed region (the timed region itself is never instrumented)")
+    ap.add_argument("--sync-spin", type=int, default=1,
+                    help="1: the HIP runtime spins instead of yielding while the host waits for the "
+                         "device (hipDeviceScheduleSpin, set before the device is initialised)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N>1 (nccl = RCCL over xGMI; gloo only to rehearse "
                          "several ranks on a one-GPU box)")
@@ -666,6 +669,13 @@ def main():
     # one GPU per rank; the modulo only matters for a rehearsal of several
     # ranks on a one-GPU box (--dist-backend gloo), never on a full node
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    if args.sync_spin:
+        # torch's own HIP runtime (same soname): spin-wait host synchronisation,
+        # which the timed region's closing synchronize() pays once per call
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so.7")
+        if hip.hipSetDevice(local) == 0:
+            hip.hipSetDeviceFlags(1)  # hipDeviceScheduleSpin
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
