@@ -878,6 +878,12 @@ hipError_t set_pb_stamp_buffer(void *p) {
     do {            \
     } while (0)
 #endif
+// SKE_PB_DPP 1 (default): the fail-list pass B's 8-lane prefix by DPP row
+// shifts instead of three ds_bpermute rounds and a broadcast (pass B 0.1966 ->
+// 0.1946 ms, three alternations, profiles/r03_ab_pass_a_vmcnt.txt)
+#ifndef SKE_PB_DPP
+#define SKE_PB_DPP 1
+#endif
 template <int SP, int R = 2 * SP, bool FL = false>  // R: 16-byte pieces per lane and run (runs of SP slices)
 __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const PartArgs A) {
     PB_STAMP(0);
@@ -1010,12 +1016,27 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                 // this tile's failures (its kPbLanes lanes): positions by a
                 // segment prefix; the first kPbLanes go to the tile's list
                 uint32_t incl = cnt;
+#if SKE_PB_DPP
+                // 8-lane segment prefix by DPP row shifts (VALU, no LDS round
+                // trip); the list slots start as 0xffff and get the failures
+                q[lane] = 0xffffu;
+                __builtin_amdgcn_wave_barrier();
+                {
+                    uint32_t y = __builtin_amdgcn_update_dpp(0u, incl, 0x111, 0xf, 0xf, true);  // row_shr:1
+                    incl += qq >= 1 ? y : 0u;
+                    y = __builtin_amdgcn_update_dpp(0u, incl, 0x112, 0xf, 0xf, true);  // row_shr:2
+                    incl += qq >= 2 ? y : 0u;
+                    y = __builtin_amdgcn_update_dpp(0u, incl, 0x114, 0xf, 0xf, true);  // row_shr:4
+                    incl += qq >= 4 ? y : 0u;
+                }
+#else
 #pragma unroll
                 for (uint32_t o = 1; o < kPbLanes; o <<= 1) {
                     const uint32_t y = __shfl_up(incl, o, 64);
                     if (qq >= o) incl += y;
                 }
                 const uint32_t tot = __shfl(incl, k * kPbLanes + kPbLanes - 1, 64);
+#endif
                 uint32_t pos = incl - cnt;
                 while (fm) {
                     const uint32_t j = __builtin_ctz(fm);
@@ -1028,7 +1049,11 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                 __builtin_amdgcn_wave_barrier();
                 // lane (k, qq) writes entry qq of tile tg + k's list (tiles past
                 // this block's range belong to another wave: not written)
+#if SKE_PB_DPP
+                const uint32_t v = q[lane];
+#else
                 const uint32_t v = qq < tot ? q[lane] : 0xffffu;
+#endif
                 const uint32_t fo = ((unit * A.fl_stride + tg + k) * kPbLanes + qq) * 2;
                 __builtin_amdgcn_raw_buffer_store_b16(uint16_t(v), rfl, tg + k < tb ? fo : kOOR, 0, 0);
                 __builtin_amdgcn_wave_barrier();
