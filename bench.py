@@ -221,6 +221,18 @@ def cpu_baseline(orc, chain, w, b0, seconds, key_name):
                                            "(attendance_processor.py:100-137 without transport)"}}
 
 
+def checked(fn, *a, **k):
+    """A check that raises is reported in the line (ok false, the error), not
+    by losing the measured line: every rank runs the same checks on the same
+    shapes, so an error (an unsupported collective, a shape mismatch) is raised
+    on every rank alike before the next collective."""
+    try:
+        return fn(*a, **k)
+    except Exception as e:  # noqa: BLE001 - reported, not swallowed
+        print(f"CHECK ERROR {fn.__name__}: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
+        return {"ok": False, "error": f"{type(e).__name__}: {e}"[:400]}
+
+
 def verify(engine, orc, chain, w, km, rank, world, dist, dev, exchange, prefix="VERIFY", under=None):
     """The shipped multi-GPU classes on a verification stream, against the
     CPU oracle over the WHOLE stream (no collective on the expected side).
@@ -724,12 +736,13 @@ def main():
         orc = ge.load_oracle()
         chain = oracle_chain(run.engine, orc, run.w, run.p)
         if not args.no_check:
-            chk = verify(run.engine, orc, chain, run.w, run.km, rank, world, dist, dev, bool(args.exchange))
-            if world > 1 and not args.exchange:
+            chk = checked(verify, run.engine, orc, chain, run.w, run.km, rank, world, dist, dev,
+                          bool(args.exchange))
+            if world > 1 and not args.exchange and getattr(verify, "last_map", None) is not None:
                 # the unpartitioned-input path too (SwipeExchange: alltoallv over
                 # RCCL at N > 1) on a third key universe, then the same queries
-                x = verify(run.engine, orc, chain, run.w, run.km, rank, world, dist, dev, True,
-                           prefix="VERIFYX", under=verify.last_map)
+                x = checked(verify, run.engine, orc, chain, run.w, run.km, rank, world, dist, dev, True,
+                            prefix="VERIFYX", under=verify.last_map)
                 chk = {**chk, "ok": chk["ok"] and x["ok"], "exchange": x}
             line["check"] = chk
         if want_cpu:
