@@ -45,3 +45,17 @@ def test_sector_model_generic_k1():
     b = _bench()
     alg = b.pass_bytes(1000, 900, 7200, 7, True, [(1_102_784, 8)])
     assert alg["k1"] == 1000 * (7 + 0 + 4 + 1) + 64 * 7200 + 128 * 900
+
+
+def test_checked_reports_a_raising_check():
+    """A check that raises (an unsupported collective, a shape mismatch) is
+    reported in the bench line as ok false with the error, not by losing the
+    line; a passing check's dict comes through unchanged."""
+    b = _bench()
+
+    def boom(x):
+        raise RuntimeError("alltoall unsupported %d" % x)
+
+    r = b.checked(boom, 3)
+    assert r["ok"] is False and r["error"] == "RuntimeError: alltoall unsupported 3"
+    assert b.checked(lambda **k: {"ok": True, **k}, a=1) == {"ok": True, "a": 1}
