@@ -878,6 +878,12 @@ hipError_t set_pb_stamp_buffer(void *p) {
     do {            \
     } while (0)
 #endif
+#ifndef SKE_PB_ABLATE
+#define SKE_PB_ABLATE 0  // diagnostic builds only: 1 = one slice image per block
+#endif
+#ifndef SKE_PB_IMG_BATCH
+#define SKE_PB_IMG_BATCH 0  // pass B's slice-pair image copy as one batch of loads
+#endif
 // SKE_PB_DPP 1 (default): the fail-list pass B's 8-lane prefix by DPP row
 // shifts instead of three ds_bpermute rounds and a broadcast (pass B 0.1966 ->
 // 0.1946 ms, three alternations, profiles/r03_ab_pass_a_vmcnt.txt)
@@ -905,6 +911,9 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
     const __amdgpu_buffer_rsrc_t roff = part_rsrc(A.off, (A.nslices + 1) * A.off_stride * 4);
     const __amdgpu_buffer_rsrc_t rfl = part_rsrc(A.flist, FL ? A.nunits * A.fl_stride * kPbLanes * 2 : 0);
     uint32_t *q = fq[wave];
+#if SKE_PB_ABLATE & 1
+    bool pb_loaded = false;
+#endif
     while (w < wend) {
         // slices g .. g + SP - 1 (SP = 2: one link only, host-checked), so
         // one run per tile covers them all
@@ -917,10 +926,37 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
         const PartLink &L = A.link[l];
         const uint32_t b0 = (g - L.slice0) * kPSliceBytes;
         const uint32_t nb = L.nbytes16 - b0 < kPSliceBytes * SP ? L.nbytes16 - b0 : kPSliceBytes * SP;
+#if SKE_PB_ABLATE & 1
+        // diagnostic (answers wrong): the image of the block's first unit only
+        if (!pb_loaded) {
+            pb_loaded = true;
+#endif
         lds_barrier();  // every wave is done with the previous slice
+#if SKE_PB_IMG_BATCH
+        {
+            // the pair image in one batch of fixed-count buffer loads (past nb
+            // the range check returns zeros, which no record addresses): one
+            // memory round trip per unit instead of one per 16 KiB piece
+            constexpr uint32_t kCp = kPSliceBytes * SP / (kPbBlock * 16);
+            static_assert(kCp * kPbBlock * 16 == kPSliceBytes * SP, "image pieces");
+            const __amdgpu_buffer_rsrc_t rimg = part_rsrc(L.bf + b0, nb);
+            uint4 piece[kCp];
+#pragma unroll
+            for (uint32_t c = 0; c < kCp; c++)
+                piece[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                         rimg, (c * kPbBlock + threadIdx.x) * 16, 0, 0));
+#pragma unroll
+            for (uint32_t c = 0; c < kCp; c++)
+                *reinterpret_cast<uint4 *>(img + (c * kPbBlock + threadIdx.x) * 16) = piece[c];
+        }
+#else
         for (uint32_t o = threadIdx.x * 16; o < nb; o += kPbBlock * 16)
             *reinterpret_cast<uint4 *>(img + o) = *reinterpret_cast<const uint4 *>(L.bf + b0 + o);
+#endif
         lds_barrier();
+#if SKE_PB_ABLATE & 1
+        }
+#endif
         const __amdgpu_buffer_rsrc_t rfail = part_rsrc(A.fail + size_t(l) * A.fail_stride, A.fail_stride);
         const uint32_t orow = g * A.off_stride, erow = ge * A.off_stride;
         // run boundaries of 8 rounds at once: lane L holds those of tile
