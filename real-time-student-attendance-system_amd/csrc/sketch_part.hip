@@ -882,7 +882,7 @@ hipError_t set_pb_stamp_buffer(void *p) {
 #define SKE_PB_ABLATE 0  // diagnostic builds only: 1 = one slice image per block
 #endif
 #ifndef SKE_PB_IMG_BATCH
-#define SKE_PB_IMG_BATCH 0  // pass B's slice-pair image copy as one batch of loads
+#define SKE_PB_IMG_BATCH 1  // pass B's slice-pair image copy as one batch of loads (0.195 -> 0.190 ms, r03_ab_pass_a_vmcnt.txt)
 #endif
 // SKE_PB_DPP 1 (default): the fail-list pass B's 8-lane prefix by DPP row
 // shifts instead of three ds_bpermute rounds and a broadcast (pass B 0.1966 ->
