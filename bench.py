@@ -70,7 +70,9 @@ VERIFY_KEYS = 64
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without WORLD_SIZE in the environment and N > 1, "
+                         "bench.py launches the N ranks itself (torch.distributed.run)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3")
@@ -130,7 +132,54 @@ def parse(argv=None):
                          "several ranks on a one-GPU box)")
     ap.add_argument("--layout", default="offsets", choices=["offsets", "fixed"],
                     help="id batch layout: bytes + u32 offsets, or fixed-width ids")
+    ap.add_argument("--shares", default="mass", choices=["mass", "equal"],
+                    help="N > 1, input routed at ingest: mass = one global stream of N x the "
+                         "config's step swipes, each rank's batch the probability mass of the keys "
+                         "it owns (the fixed 1B-event stream of north_star, cut per step); "
+                         "equal = every rank the config's step swipes over its own keys")
     return ap.parse_args(argv)
+
+
+def free_port():
+    """A TCP port on 127.0.0.1 nothing listens on (the rendezvous port of a
+    self-launched multi-rank run)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(args, argv, env):
+    """How this invocation runs (the driver's contract: `bench.py --gpus N` is
+    N ranks, one per GPU).
+
+    - WORLD_SIZE set (an external torch.distributed.run): this process is one
+      rank; --gpus, when given, must equal WORLD_SIZE.  Returns None.
+    - WORLD_SIZE unset and --gpus N > 1: returns the command that launches the
+      N ranks (torch.distributed.run on 127.0.0.1, the same bench arguments);
+      the caller runs it as a child process BEFORE anything touches the GPU
+      and exits with its status.  Rank 0 prints the JSON line.
+    - otherwise one rank in this process (None)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if args.gpus is not None and int(ws) != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}")
+        return None
+    n = args.gpus or 1
+    if n <= 1:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+            os.path.abspath(__file__), *argv]
+
+
+def rank_swipes(step_swipes, mass, world, mode):
+    """Swipes this rank processes per step.  `mass`: the probability mass of
+    the keys it owns in the global stream.  mass mode: this rank's share of a
+    global step of world x step_swipes swipes; equal mode: step_swipes."""
+    if world <= 1 or mode == "equal":
+        return step_swipes
+    return max(1, int(round(world * step_swipes * mass)))
 
 
 def cpu_threads():
@@ -381,7 +430,10 @@ class Run:
                                           "zipf_lectures": 0, "zipf_days": 0})
             cdf = synthetic.cdf_from_probs(probs[mine]) if probs is not None else None
         self.w = w = synthetic.Workload(**{**w_all.__dict__, "n_keys": int(mine.size)})
-        self.n = n = args.batch or w.step_swipes
+        # the probability mass of this rank's keys in the global stream
+        self.mass = float(probs[mine].sum()) if probs is not None else mine.size / len(self.names)
+        self.shares = "equal" if args.exchange else args.shares
+        self.n = n = rank_swipes(args.batch or w.step_swipes, self.mass, world, self.shares)
         self.engine = engine = SketchEngine(local)
         self.stream = stream = torch.cuda.Stream()  # shared by libsketch and torch
         torch.cuda.set_stream(stream)
@@ -668,6 +720,14 @@ def secondary(args, cfg, local, dev, dist):
 
 def main():
     args = parse()
+    cmd = launch_plan(args, sys.argv[1:], os.environ)
+    if cmd is not None:
+        # N ranks as child processes, started before this process touches the
+        # GPU (no torch.cuda, no libsketch here); rank 0's JSON line goes
+        # straight to our stdout; a failing rank fails the run
+        import subprocess
+        print("bench.py: launching %d ranks: %s" % (args.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
+        sys.exit(subprocess.run(cmd).returncode)
     import numpy as np  # noqa: F401
     import torch
     import torch.distributed as dist
@@ -699,11 +759,27 @@ def main():
 
     run = Run(args, args.config, world, rank, local, dev, dist)
     elapsed, step_ms, host_enqueue = run.timed()
+    cdev = dev if args.dist_backend == "nccl" else "cpu"
+    my_elapsed = elapsed
+    total_swipes = run.n
+    shares = {"mode": run.shares, "swipes_per_step": [run.n], "key_mass": [run.mass],
+              "elapsed_s": [elapsed]}
     if world > 1:
-        t = torch.tensor([elapsed, step_ms], dtype=torch.float64,
-                         device=dev if args.dist_backend == "nccl" else "cpu")
+        t = torch.tensor([elapsed, step_ms], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, step_ms = float(t[0]), float(t[1])
+        # every rank's batch, key mass and wall time (the slowest bounds the job)
+        g = torch.zeros(3 * world, dtype=torch.float64, device=cdev)
+        g[3 * rank:3 * rank + 3] = torch.tensor([run.n, run.mass, my_elapsed], dtype=torch.float64)
+        dist.all_reduce(g, op=dist.ReduceOp.SUM)
+        g = g.view(world, 3).cpu().tolist()
+        total_swipes = int(sum(r[0] for r in g))
+        shares = {"mode": run.shares, "swipes_per_step": [int(r[0]) for r in g],
+                  "key_mass": [r[1] for r in g], "elapsed_s": [r[2] for r in g]}
+    mean_n = total_swipes / world
+    shares.update({"rank_share_max": max(shares["swipes_per_step"]) / mean_n,
+                   "rank_share_min": min(shares["swipes_per_step"]) / mean_n,
+                   "slowest_rank": int(max(range(world), key=lambda r: shares["elapsed_s"][r]))})
     pt = run.replay_instrumented() if args.pass_replay else None
     if world > 1 and pt is not None:
         t = torch.tensor([ms for ms, _ in pt], dtype=torch.float64,
@@ -712,7 +788,7 @@ def main():
         pt = [(float(t[i]), c) for i, (_, c) in enumerate(pt)]
 
     ms_per_step = elapsed * 1e3 / args.steps
-    value = world * run.n * args.steps / elapsed
+    value = total_swipes * args.steps / elapsed
     line = {
         "metric": METRIC,
         "value": value,
@@ -730,7 +806,9 @@ def main():
         "roofline": run.roofline(pt, step_ms),
         "preload_s": run.preload_s,
         "host_enqueue_us_per_step": host_enqueue * 1e6 / args.steps,
+        "rank_shares": shares,
     }
+    line["config"]["swipes_per_step_all_ranks"] = total_swipes
     want_cpu = rank == 0 and world == 1 and not args.no_cpu and args.cpu_seconds > 0
     if not args.no_check or want_cpu:
         orc = ge.load_oracle()
