@@ -87,33 +87,18 @@ def parse(argv=None):
     ap.add_argument("--variant", type=int, default=-1,
                     help="-1 auto, 0 global Bloom, 1 LDS Bloom, 2 XCD-partitioned, 3 partitioned")
     ap.add_argument("--max-batches", type=int, default=64)
-    ap.add_argument("--ablate", type=int, default=0, help="diagnostic: K1 parts removed (bits)")
     ap.add_argument("--part-sub", type=int, default=0,
                     help="partitioned K1: swipes per sub-batch of its three passes (0 = default)")
-    ap.add_argument("--hll-mode", type=int, default=-1,
-                    help="partitioned K1 PFADD: 0 = CAS on the slab, 1 = owned register lines "
-                         "(-1: library default)")
     ap.add_argument("--exchange", type=int, default=0,
                     help="1 = unpartitioned input: every rank's batches span ALL keys and a step "
                          "routes them to the key owners with all_to_all_single "
                          "(distributed.SwipeExchange), runs K1 there and returns the answers")
-    ap.add_argument("--pa-tile", type=int, default=-1,
-                    help="partitioned K1 tile: 10 = 1024 swipes, 11 = 2048 (one-link k = 11 "
-                         "chains; -1: library default)")
-    ap.add_argument("--pa-precheck", type=int, default=-1,
-                    help="partitioned K1: 1 = pass A pre-checks the HLL registers (pass C only "
-                         "raises), 0 = pass C loads them (-1: library default)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
-                    help="library option (ske_set_option), e.g. part_overlap=2; repeatable")
-    ap.add_argument("--pb-pairs", type=int, default=-1,
-                    help="partitioned K1 pass B: 1 = slice pairs (128 KiB images), 0 = single "
-                         "slices (-1: library default)")
+                    help="library option (ske_set_option), e.g. k1_grid=128; repeatable")
     ap.add_argument("--persistent", type=int, default=-1,
-                    help="1 = the K timed steps as ONE ske_swipes_many_async call (for the "
-                         "partitioned K1 with the part_overlap option: each step's pass C on a side "
-                         "stream beside the next step's pass B); for the LDS K1 one persistent "
-                         "LDS K1 launch over the K batches; default for the LDS K1); 0 = a K1 "
-                         "launch per step")
+                    help="1 = the K timed steps as ONE ske_swipes_many_async call (for the LDS "
+                         "K1 one persistent launch over the K batches; the default for the LDS K1); "
+                         "0 = a K1 launch per step")
     ap.add_argument("--streams", type=int, default=0,
                     help="HIP streams / graph branches the steps alternate over (0: 16 for the "
                          "LDS K1, 1 otherwise)")
@@ -282,7 +267,7 @@ def checked(fn, *a, **k):
         return {"ok": False, "error": f"{type(e).__name__}: {e}"[:400]}
 
 
-def verify(engine, orc, chain, w, km, rank, world, dist, dev, exchange, prefix="VERIFY", under=None):
+def verify(engine, orc, chain, w, km, rank, world, dist, dev, exchange, sinks, prefix="VERIFY", under=None):
     """The shipped multi-GPU classes on a verification stream, against the
     CPU oracle over the WHOLE stream (no collective on the expected side).
 
@@ -294,7 +279,8 @@ def verify(engine, orc, chain, w, km, rank, world, dist, dev, exchange, prefix="
     to distributed.SwipeExchange.  Then distributed.ShardedSketch, over a
     client that KeyMap.bind named, answers union PFCOUNT, PFCOUNT of every key
     and a rollup (RCCL at N > 1).  `under`: a KeyMap whose slots the
-    verification keys go above (default: the workload's)."""
+    verification keys go above (default: the workload's).  `sinks`: every
+    rank's spare slot for SwipeExchange.swipes_async's padding."""
     import numpy as np
     import torch
     import rtsas_amd
@@ -319,8 +305,11 @@ def verify(engine, orc, chain, w, km, rank, world, dist, dev, exchange, prefix="
     if exchange:
         lo, hi = rank * n // world, (rank + 1) * n // world
         ids = torch.as_tensor(buf[:n * width].reshape(n, width)[lo:hi].copy(), device=dev)
-        ex = SwipeExchange(rank, world, engine_k1(engine), vk, engine=engine)
-        got = ex.swipes(ids, torch.as_tensor(gkey[lo:hi].astype(np.int64), device=dev))
+        ex = SwipeExchange(rank, world, engine_k1(engine), vk, engine=engine, sink_slots=sinks)
+        # the host-free form (as the timed steps), every rank's slice <= n_max
+        got = ex.swipes_async(ids, torch.as_tensor(gkey[lo:hi].astype(np.int64), device=dev),
+                              n_max=-(-n // world))
+        ex.settle()
         torch.cuda.synchronize()
         ok_answers = bool(np.array_equal(got.cpu().numpy(), want[lo:hi]))
     else:
@@ -354,7 +343,7 @@ def verify(engine, orc, chain, w, km, rank, world, dist, dev, exchange, prefix="
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     verify.last_map = vk
     return {"ok": bool(ok.item()), "stream_swipes": n, "keys": VERIFY_KEYS, "keys_owned": int(mine.size),
-            "input": "SwipeExchange slice" if exchange else "owner-routed",
+            "input": "SwipeExchange.swipes_async slice" if exchange else "owner-routed",
             "answers": ok_answers, "owned_registers": ok_regs,
             "sharded_pfcount_union": bool(ok_union), "sharded_pfcount_each": bool(ok_each),
             "sharded_rollup": bool(ok_roll), "union_pfcount": int(union),
@@ -438,13 +427,11 @@ class Run:
         self.stream = stream = torch.cuda.Stream()  # shared by libsketch and torch
         torch.cuda.set_stream(stream)
         engine.set_stream(stream.cuda_stream)
-        for name, val in (("tile", args.tile), ("ablate", args.ablate), ("part_sub", args.part_sub)):
+        for name, val in (("tile", args.tile), ("part_sub", args.part_sub)):
             if val:
                 engine.set_option(name, val)
-        for name, val in (("variant", args.variant), ("hll_mode", args.hll_mode), ("pb_pairs", args.pb_pairs),
-                          ("pa_tile", args.pa_tile), ("pa_precheck", args.pa_precheck)):
-            if val >= 0:
-                engine.set_option(name, val)
+        if args.variant >= 0:
+            engine.set_option("variant", args.variant)
         for kv in args.opt:
             name, _, val = kv.partition("=")
             engine.set_option(name, int(val))
@@ -455,7 +442,11 @@ class Run:
         engine.preload(0, p, w.n_members)
         self.preload_s = time.perf_counter() - t0
         self.nslots = self.km.slots_end(rank)
-        engine.hll_reserve(self.nslots + VERIFY_KEYS)
+        # past the workload's keys: the verification universes (verify(), up
+        # to 2 x VERIFY_KEYS slots), then the exchange's sink slot (padding
+        # rows of SwipeExchange.swipes_async; no key lives there)
+        self.sinks = [self.km.slots_end(r) + 2 * VERIFY_KEYS for r in range(world)]
+        engine.hll_reserve(self.sinks[rank] + 1)
         self.variant = variant = engine.variant(0)
         self.lds_k1 = lds_k1 = variant == 1
         self.persistent = bool(args.persistent if args.persistent >= 0 else lds_k1) and not args.exchange
@@ -485,7 +476,7 @@ class Run:
                     __cuda_array_interface__ = {"shape": shape, "typestr": typestr, "data": (ptr, False),
                                                 "version": 3, "strides": None}
                 return torch.as_tensor(_V(), device=dev)
-            self.ex = SwipeExchange(rank, world, engine_k1(engine), self.km, engine=engine)
+            self.ex = SwipeExchange(rank, world, engine_k1(engine), self.km, engine=engine, sink_slots=self.sinks)
             self.xviews = [(tview(b.bytes.ptr, (n, self.width), "|u1"), tview(b.slot.ptr, (n,), "<i4"))
                            for b in self.batches]
 
@@ -493,7 +484,8 @@ class Run:
     def step(self, j):
         e = self.engine
         if self.ex is not None:
-            self.ex.swipes(*self.xviews[j % self.nb])
+            # host-free exchange: equal splits of a capacity, settled at the end
+            self.ex.swipes_async(*self.xviews[j % self.nb])
             return
         if len(self.streams) > 1:
             e.set_stream(self.streams[j % len(self.streams)].cuda_stream)
@@ -517,7 +509,14 @@ class Run:
                 self.step(j)
         e.set_stream(self.stream.cuda_stream)
         self.torch.cuda.synchronize()
+        self.finish()
         e.check_errors()
+
+    def finish(self):
+        """The end of a run of steps: the exchange's settle (capacity
+        overflows re-run with exact splits; a collective)."""
+        if self.ex is not None:
+            self.redone = getattr(self, "redone", 0) + self.ex.settle()
 
     def enqueue_steps(self, graph):
         a, e, torch = self.args, self.engine, self.torch
@@ -563,6 +562,7 @@ class Run:
         e1.record(self.stream)
         host_enqueue = time.perf_counter() - t0
         torch.cuda.synchronize()
+        self.finish()
         if barrier and self.world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
@@ -584,6 +584,7 @@ class Run:
         e.pass_times(reset=True)
         self.enqueue_steps(None)
         torch.cuda.synchronize()
+        self.finish()
         e.set_option("pass_timing", 0)
         e.check_errors()
         return e.pass_times(reset=True)
@@ -686,11 +687,12 @@ class Run:
                 "k1_variant": {0: "global-bloom", 1: "lds-bloom", 2: "xcd-regions",
                                3: "partitioned"}[self.variant],
                 "layout": a.layout, "streams": len(self.streams),
-                "input": ("unpartitioned: alltoallv to the key owners per step"
+                "input": ("unpartitioned: equal-split all_to_all to the key owners per step "
+                          "(SwipeExchange.swipes_async; capacity overflows re-run at settle)"
                           if a.exchange else "routed to the key owners at ingest"),
                 "launch": ("hip-graph" if self.graph is not None else
                            ("persistent (one K1 launch per 48 steps)" if self.lds_k1 else
-                            "one many-batch call (pass C of a step beside passes A/B of the next)")
+                            "one many-batch call")
                            if self.persistent else "host"),
                 "answers": "written (1 B per swipe)"}
 
@@ -809,18 +811,20 @@ def main():
         "rank_shares": shares,
     }
     line["config"]["swipes_per_step_all_ranks"] = total_swipes
+    if run.ex is not None:
+        line["exchange"] = {**run.ex.stats, "slack": run.ex.slack, "capacity_rows_per_peer": run.ex.capacity(run.n)}
     want_cpu = rank == 0 and world == 1 and not args.no_cpu and args.cpu_seconds > 0
     if not args.no_check or want_cpu:
         orc = ge.load_oracle()
         chain = oracle_chain(run.engine, orc, run.w, run.p)
         if not args.no_check:
             chk = checked(verify, run.engine, orc, chain, run.w, run.km, rank, world, dist, dev,
-                          bool(args.exchange))
+                          bool(args.exchange), run.sinks)
             if world > 1 and not args.exchange and getattr(verify, "last_map", None) is not None:
                 # the unpartitioned-input path too (SwipeExchange: alltoallv over
                 # RCCL at N > 1) on a third key universe, then the same queries
                 x = checked(verify, run.engine, orc, chain, run.w, run.km, rank, world, dist, dev, True,
-                            prefix="VERIFYX", under=verify.last_map)
+                            run.sinks, prefix="VERIFYX", under=verify.last_map)
                 chk = {**chk, "ok": chk["ok"] and x["ok"], "exchange": x}
             line["check"] = chk
         if want_cpu:

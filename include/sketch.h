@@ -113,8 +113,11 @@ int ske_get_stream(ske_ctx *ctx, void **hip_stream); /* the stream calls enqueue
  * named an HLL slot outside the slab since the last check.  The word is read
  * and cleared by device-side atomic exchanges (no flag set concurrently on
  * another stream is lost).  A synchronous K1 / PFADD / ingest call reports
- * only its OWN out-of-range slots; what earlier enqueue-only calls left is
- * kept for the next ske_sync / ske_check_errors. */
+ * the out-of-range slots flagged while it ran: its own, and those of any work
+ * that was running at the same time on other streams (enqueue-only calls
+ * still in flight may be attributed to it -- the flag is one device word);
+ * what finished before it began is kept for the next ske_sync /
+ * ske_check_errors. */
 int ske_sync(ske_ctx *ctx);
 int ske_check_errors(ske_ctx *ctx);  /* the same check: sync + report + clear */
 int ske_device_alloc(ske_ctx *ctx, uint64_t bytes, void **out); /* device scratch for callers */
@@ -214,7 +217,7 @@ int ske_swipes_fixed_async(ske_ctx *ctx, uint32_t fid, const uint32_t *slot,
  * pipelined in chunks: a chunk's ids and slots cross the host link while K1
  * runs on the previous one; the link carries width + 4 bytes per swipe in and
  * 1/8 byte out (the offsets-and-bytes form: width + 9).  Synchronous; reports
- * this call's own out-of-range slots (SKE_ERANGE).
+ * the out-of-range slots flagged while it ran (SKE_ERANGE; see ske_sync).
  *   replaces the per-event pair attendance_processor.py:109-113 + :127-129
  *   for a batch of fixed-digit student ids (every config's ids) */
 int ske_swipes_fixed_bits(ske_ctx *ctx, uint32_t fid, const uint32_t *slot, const uint8_t *bytes,
@@ -234,6 +237,21 @@ int ske_swipes_fixed_bits(ske_ctx *ctx, uint32_t fid, const uint32_t *slot, cons
 int ske_route_swipes(ske_ctx *ctx, const uint8_t *ids, uint32_t width, const uint32_t *gkey, uint64_t n,
                      uint32_t world, const uint32_t *key_owner, const uint32_t *key_local, uint32_t nkeys,
                      uint8_t *send_ids, uint32_t *send_slots, uint32_t *pos, uint64_t *counts);
+/* The same routing with no host synchronisation (enqueue only): owner o's
+ * swipes fill rows [o*cap, o*cap + counts[o]) of send_ids / send_slots (device,
+ * world*cap rows), so every peer pair exchanges exactly `cap` rows (an
+ * all_to_all of equal splits the host sizes without reading the device).
+ * Rows [counts[o], cap) get zero id bytes and slot sink_slots[o] (device,
+ * [world]: a slot owner o keeps for no key, so padding changes no key's
+ * registers).  counts (device, [world]) = swipes per owner; counts[o] > cap
+ * means the swipes ranked past cap were NOT sent (their answers are another
+ * row's): the caller re-runs the batch with ske_route_swipes, which is safe
+ * (PFADD is idempotent, answers are rewritten).  world*cap < 2^32.
+ * Replaces the per-event consumer loop's hand-off, attendance_processor.py:30-34. */
+int ske_route_swipes_cap_async(ske_ctx *ctx, const uint8_t *ids, uint32_t width, const uint32_t *gkey, uint64_t n,
+                               uint32_t world, const uint32_t *key_owner, const uint32_t *key_local, uint32_t nkeys,
+                               uint32_t cap, const uint32_t *sink_slots, uint8_t *send_ids, uint32_t *send_slots,
+                               uint32_t *pos, uint32_t *counts);
 /* out[i] = answers[pos[i]]: the owners' BF.EXISTS answers, received back in
  * send order, into input order (enqueue only). */
 int ske_route_return_async(ske_ctx *ctx, const uint8_t *answers, const uint32_t *pos, uint64_t n,
@@ -272,6 +290,11 @@ int ske_swipes_stats(ske_ctx *ctx, uint32_t fid, const uint8_t *bytes, const uin
  *   2 = XCD-partitioned K1 (sketch_xr.hip),
  *   3 = partitioned K1, passes A/B/C over LDS slices (sketch_part.hip; C3/C5) */
 int ske_swipes_variant(ske_ctx *ctx, uint32_t fid);
+/* Tuning options (no reference counterpart): "variant" (-1 auto, 0..3 as
+ * above), "tile" (LDS K1 swipes per thread: 1, 2, 4, 8), "k1_grid" (LDS K1
+ * blocks, 0 = one per CU), "k1_persistent" (0/1), "part_sub" (partitioned K1
+ * swipes per sub-batch, 0 = 16M), "pass_timing" (0/1).  Any other name or an
+ * out-of-range value: SKE_EINVAL.  None changes an answer or a register. */
 int ske_set_option(ske_ctx *ctx, const char *name, int64_t value);
 /* Kernel timing for the benchmark's roofline: with option "pass_timing" = 1
  * every K1 kernel launched outside a capture is bracketed by a HIP event pair

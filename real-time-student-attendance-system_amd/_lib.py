@@ -123,6 +123,8 @@ SIGNATURES = {
     "ske_swipes_fixed_bits": (C.c_int, [_CTX, C.c_uint32, _u32p, _u8p, C.c_uint32, C.c_uint64, _u8p, C.c_int]),
     "ske_route_swipes": (C.c_int, [_CTX, _u8p, C.c_uint32, _u32p, C.c_uint64, C.c_uint32, _u32p, _u32p,
                                    C.c_uint32, _u8p, _u32p, _u32p, _u64p]),
+    "ske_route_swipes_cap_async": (C.c_int, [_CTX, _u8p, C.c_uint32, _u32p, C.c_uint64, C.c_uint32, _u32p, _u32p,
+                                             C.c_uint32, C.c_uint32, _u32p, _u8p, _u32p, _u32p, _u32p]),
     "ske_route_return_async": (C.c_int, [_CTX, _u8p, _u32p, C.c_uint64, _u8p]),
     "ske_swipes_stats": (C.c_int, [_CTX, C.c_uint32, _u8p, _u32p, C.c_uint64,
                                    C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
@@ -168,6 +170,8 @@ def load() -> C.CDLL:
         pass
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
+        if os.environ.get("SKE_LIB") and not hasattr(lib, name):
+            continue  # an A/B build of an older revision: entry points it predates stay unbound
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

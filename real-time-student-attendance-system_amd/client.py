@@ -70,6 +70,30 @@ class KeySpace:
         self._next_slot = 0
         self._slot_key: dict[int, bytes] = {}
         self.slots_released = 0  # bumps whenever an HLL slot is freed (ingest key table)
+        # README day keys <stem>:YYYY-MM-DD by stem (the key minus its day),
+        # kept with the table: a lecture's day keys without a scan
+        self.day_keys: dict[bytes, set] = {}
+
+    @staticmethod
+    def _day_stem(key: bytes):
+        """The stem of a README-form day key <stem>:YYYY-MM-DD, else None."""
+        if len(key) > 11 and key[-11] == 0x3A and key[-3] == key[-6] == 0x2D and \
+                key[-10:-6].isdigit() and key[-5:-3].isdigit() and key[-2:].isdigit():
+            return key[:-11]
+        return None
+
+    def _index(self, key: bytes, add: bool) -> None:
+        stem = self._day_stem(key)
+        if stem is None:
+            return
+        if add:
+            self.day_keys.setdefault(stem, set()).add(key)
+        else:
+            ks = self.day_keys.get(stem)
+            if ks is not None:
+                ks.discard(key)
+                if not ks:
+                    del self.day_keys[stem]
 
     def type_of(self, key: bytes) -> str | None:
         return self.kind.get(key)
@@ -103,6 +127,7 @@ class KeySpace:
         self.kind[key] = "hll"
         self.slot[key] = s
         self._slot_key[s] = key
+        self._index(key, True)
         return s
 
     def bind(self, key: bytes, slot: int) -> None:
@@ -129,6 +154,7 @@ class KeySpace:
         self.kind[key] = "hll"
         self.slot[key] = slot
         self._slot_key[slot] = key
+        self._index(key, True)
 
     def drop(self, key: bytes) -> bool:
         k = self.kind.pop(key, None)
@@ -139,6 +165,7 @@ class KeySpace:
         elif k == "hll":
             s = self.slot.pop(key)
             self._slot_key.pop(s, None)
+            self._index(key, False)
             self.ctx.call("ske_hll_clear", s)  # a reused slot starts empty
             self._free_slots.append(s)
             self.slots_released += 1
@@ -149,9 +176,86 @@ class KeySpace:
         registers were never written)."""
         s = self.slot.pop(key)
         self._slot_key.pop(s, None)
+        self._index(key, False)
         del self.kind[key]
         self._free_slots.append(s)
         self.slots_released += 1
+
+
+def _sc(b: int) -> int:
+    """a byte as C's (signed) char, as Redis compares range bounds"""
+    return b - 256 if b >= 128 else b
+
+
+def redis_glob(pattern: bytes, string: bytes, _nest: int = 0) -> bool:
+    """Redis' SCAN / KEYS MATCH rule, restated from redis ``src/util.c``
+    ``stringmatchlen`` (case-sensitive; no Redis in this image, so parity is
+    unpinned -- tests/test_encoding.py holds the cases): ``*`` any run, ``?``
+    one byte, ``[...]`` a class with ``^`` negation, ``a-z`` ranges (bounds
+    swapped when reversed) and ``\\`` escapes, ``\\`` escaping the next
+    pattern byte outside a class.  Python's fnmatch differs (``[!...]``, no
+    escapes)."""
+    p, s = pattern, string
+    pi, si = 0, 0
+    if _nest > 1000:
+        return False
+    while pi < len(p) and si < len(s):
+        c = p[pi]
+        if c == 0x2A:  # '*'
+            while pi + 1 < len(p) and p[pi + 1] == 0x2A:
+                pi += 1
+            if pi + 1 == len(p):
+                return True
+            while si < len(s):
+                if redis_glob(p[pi + 1:], s[si:], _nest + 1):
+                    return True
+                si += 1
+            return False
+        elif c == 0x3F:  # '?'
+            si += 1
+        elif c == 0x5B:  # '['
+            pi += 1
+            neg = pi < len(p) and p[pi] == 0x5E  # '^'
+            if neg:
+                pi += 1
+            match = False
+            while True:
+                if pi < len(p) and p[pi] == 0x5C and len(p) - pi >= 2:  # '\\'
+                    pi += 1
+                    if p[pi] == s[si]:
+                        match = True
+                elif pi < len(p) and p[pi] == 0x5D:  # ']'
+                    break
+                elif pi >= len(p):
+                    pi -= 1
+                    break
+                elif len(p) - pi >= 3 and p[pi + 1] == 0x2D:  # 'a-z'
+                    lo, hi, ch = _sc(p[pi]), _sc(p[pi + 2]), _sc(s[si])
+                    if lo > hi:
+                        lo, hi = hi, lo
+                    pi += 2
+                    if lo <= ch <= hi:
+                        match = True
+                elif p[pi] == s[si]:
+                    match = True
+                pi += 1
+            if neg:
+                match = not match
+            if not match:
+                return False
+            si += 1
+        else:
+            if c == 0x5C and len(p) - pi >= 2:  # an escaped byte
+                pi += 1
+            if p[pi] != s[si]:
+                return False
+            si += 1
+        pi += 1
+        if si == len(s):
+            while pi < len(p) and p[pi] == 0x2A:
+                pi += 1
+            break
+    return pi == len(p) and si == len(s)
 
 
 class SketchClient:
@@ -189,16 +293,20 @@ class SketchClient:
 
     def scan_iter(self, match=None, count=None, _type=None):
         """SCAN over the key table, redis-py's iterator form (one pass, sorted;
-        MATCH in Redis' glob syntax: *, ?, [..]).  (redis-py's ``keys()`` is
-        not offered: ``self.keys`` is the key table.)"""
-        import fnmatch
-        import re
+        MATCH in Redis' own glob dialect, ``redis_glob``).  (redis-py's
+        ``keys()`` is not offered: ``self.keys`` is the key table.)"""
         pat = encode(match if match is not None else "*")
-        rx = re.compile(fnmatch.translate(pat.decode("latin-1")).encode("latin-1"), re.S)
+        every = pat == b"*"  # SCAN's own bypass (the glob rule alone would skip an empty key name)
         for k in sorted(self.keys.kind):
-            if rx.match(k) and (_type is None or self.keys.kind[k] == {"string": "hll", "MBbloom--": "bf"}.get(
+            if (every or redis_glob(pat, k)) and (_type is None or self.keys.kind[k] == {"string": "hll", "MBbloom--": "bf"}.get(
                     _type, _type)):
                 yield k.decode() if self.decode_responses else k
+
+    def day_keys(self, stem) -> list:
+        """The README-form day keys <stem>:YYYY-MM-DD that exist (sorted),
+        from the key table's index -- no scan over every key."""
+        ks = sorted(self.keys.day_keys.get(encode(stem), ()))
+        return [k.decode() for k in ks] if self.decode_responses else ks
 
     def type(self, name):
         k = self.keys.type_of(encode(name))

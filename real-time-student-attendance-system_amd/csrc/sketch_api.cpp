@@ -77,26 +77,10 @@ struct ske_ctx {
     bool err_pending = false;     // taken from the device, not yet reported by ske_sync
     unsigned long long *stats = nullptr;
     int pb = 2;           // K1 tile: swipes per thread in flight (1, 2, 4, 8)
-    int variant = -1;     // -1 auto, 0 global, 1 LDS
-    uint32_t ablate = 0;  // diagnostic only (kAblate* bits)
-    int xr_region_u = 2;  // XCD-partitioned K1: swipes per lane in the slice passes
-    int xr_finish_u = 1;  //   and in the finish pass
+    int variant = -1;     // -1 auto, 0 global, 1 LDS, 2 XCD-partitioned, 3 partitioned
     uint32_t part_sub = 0;  // partitioned K1: swipes per sub-batch (0: default)
-    int hll_mode = 0;       // partitioned K1's PFADD: 1 owned register lines, 0 CAS
-    int pb_pairs = 2;       // partitioned K1 pass B: 2 slice pairs + fail lists, 1 + fail bytes, 0 slices
-    int pa_tile = 10;       // partitioned K1 tile: 10 = 1024 swipes, 11 = 2048 (one-link k = 11 only)
-    int pa_pre = 0;         // partitioned K1: pass A pre-checks the registers (measured slower: A +0.20, C -0.04 ms)
-    int pa_grid = 0;        // partitioned K1 pass A blocks per CU (one-link k = 11; 0 = 2)
-    int pa_threads = 512;   // fail-list pass A (k_part_a3) threads per 1024-swipe tile: 512 or 1024
-    int part_overlap = 0;   // many-batch calls: partitioned K1 pass C on a side stream (measured slower)
-    hipEvent_t part_ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    // part_overlap 3: CU-masked streams, [0] pass A on the CUs pass C does not
-    // use, [1] pass C on part_ccus CUs (every (cus / part_ccus)-th CU)
-    hipStream_t cu_st[2] = {nullptr, nullptr};
-    int part_ccus = 64, cu_st_ccus = 0;
     bool lds_ok = false;
     bool k1_ok = false;       // short-id LDS K1 (sketch_k1.hip) usable
-    int k1_legacy = 0;        // 1: always the generic LDS kernel (A/B diagnostics)
     int k1_grid = 0;          // blocks of the short-id LDS K1 (0: one per CU)
     int k1_persistent = 1;    // ske_swipes_many_async: one LDS K1 launch over all batches
     uint8_t *zero16 = nullptr;  // 16 zero bytes on the device
@@ -537,7 +521,7 @@ int check_err_flag(ske_ctx *c, int code_if_set) {
 // options allow it; false: use the generic kernels.
 bool k1_fast_args(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32_t *offs,
                   uint32_t fixed_w, const uint32_t *slot, uint64_t n, uint8_t *out, K1Args *A) {
-    if (!c->k1_ok || c->k1_legacy || c->ablate || !use_lds(c, ch)) return false;
+    if (!c->k1_ok || !use_lds(c, ch)) return false;
     if (n >= (uint64_t(1) << 31)) return false;
     if (!offs && uint64_t(fixed_w) * n >= (uint64_t(1) << 32)) return false;
     if (!k1_lds_plan(ch, A)) return false;
@@ -554,44 +538,13 @@ bool k1_fast_args(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const ui
     return true;
 }
 
-// The partitioned K1 over nb batches; `pipelined`: pass C of each unit on a
-// side stream, overlapping the next unit's passes A / B (launch_swipes_part).
-int launch_part(ske_ctx *c, const ChainDev &ch, const PartBatch *bt, uint32_t nb, bool pipelined) {
+// The partitioned K1 over nb batches, every pass on the context stream.
+int launch_part(ske_ctx *c, const ChainDev &ch, const PartBatch *bt, uint32_t nb) {
     uint64_t nmax = 0;
     for (uint32_t j = 0; j < nb; j++) nmax = bt[j].n > nmax ? bt[j].n : nmax;
     if (nmax == 0) return SKE_OK;
     hipError_t e = part_reserve(ch, nmax, c->part_sub, c->scratch);
     if (e != hipSuccess) return scratch_error(c, e);
-    hipStream_t side = nullptr, side_a = nullptr;
-    const bool cu_split = pipelined && c->part_overlap == 3;
-    if (cu_split && (!c->cu_st[0] || c->cu_st_ccus != c->part_ccus)) {
-        for (hipStream_t &x : c->cu_st)
-            if (x) {
-                (void)hipStreamDestroy(x);
-                x = nullptr;
-            }
-        const int step = c->cus / c->part_ccus;
-        const uint32_t nw = uint32_t((c->cus + 31) / 32);
-        std::vector<uint32_t> ma(nw, 0), mc(nw, 0);
-        for (int i = 0; i < c->cus; i++) ((i % step == 0) ? mc : ma)[i / 32] |= 1u << (i % 32);
-        HIPCHK(c, hipExtStreamCreateWithCUMask(&c->cu_st[0], nw, ma.data()));
-        HIPCHK(c, hipExtStreamCreateWithCUMask(&c->cu_st[1], nw, mc.data()));
-        c->cu_st_ccus = c->part_ccus;
-    }
-    if (pipelined) {
-        if (c->many_n < 1) {
-            HIPCHK(c, hipStreamCreateWithFlags(&c->many_st[0], hipStreamNonBlocking));
-            HIPCHK(c, hipEventCreateWithFlags(&c->many_join[0], hipEventDisableTiming));
-            c->many_n = 1;
-        }
-        for (int i = 0; i < 4; i++)
-            if (!c->part_ev[i]) HIPCHK(c, hipEventCreateWithFlags(&c->part_ev[i], hipEventDisableTiming));
-        side = c->many_st[0];
-        if (cu_split) {
-            side_a = c->cu_st[0];
-            side = c->cu_st[1];
-        }
-    }
     unsigned long long cid = 0;
     int rc = scratch_user_begin(c, &cid);
     if (rc) return rc;
@@ -614,9 +567,8 @@ int launch_part(ske_ctx *c, const ChainDev &ch, const PartBatch *bt, uint32_t nb
         }
     };
     c->hook_arg = &hs;
-    e = launch_swipes_part(ch, bt, nb, c->regs, c->nslots, c->scratch, c->err, c->cus, c->part_sub, c->hll_mode,
-                           c->pb_pairs, c->pa_tile, c->pa_pre, pipelined ? c->part_overlap : 0, c->pa_grid, c->st, side, c->part_ev, c->timing && !c->capturing ? +hook : nullptr, c, c->pa_threads,
-                           side_a, cu_split ? c->cus / (c->cus / c->part_ccus) : 0);
+    e = launch_swipes_part(ch, bt, nb, c->regs, c->nslots, c->scratch, c->err, c->cus, c->part_sub, c->st,
+                           c->timing && !c->capturing ? +hook : nullptr, c);
     if (e != hipSuccess) {
         c->last_hip = std::string("launch_swipes_part: ") + hipGetErrorString(e);
         scratch_user_end(c, cid);
@@ -636,10 +588,10 @@ int launch_k1(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32
         mark_end(c, m);
         return SKE_OK;
     }
-    const int var = c->ablate ? 0 : k1_variant(c, ch);
+    const int var = k1_variant(c, ch);
     if (var == 3) {
         const PartBatch pb{bytes, offs, fixed_w, slot, n, out};
-        return launch_part(c, ch, &pb, 1, false);
+        return launch_part(c, ch, &pb, 1);
     }
     if (var == 2) {
         hipError_t e = hipSuccess;
@@ -650,17 +602,9 @@ int launch_k1(ske_ctx *c, const ChainDev &ch, const uint8_t *bytes, const uint32
         if (rc) return rc;
         const PassMark m = mark_begin(c, 0);
         HIPCHK(c, launch_swipes_xr(ch, bytes, offs, fixed_w, slot, n, c->regs, c->nslots, out,
-                                   scr, c->err, c->cus, c->xr_region_u, c->xr_finish_u, c->st));
+                                   scr, c->err, c->cus, 2, 1, c->st));
         mark_end(c, m);
         return scratch_user_end(c, cid);
-    }
-    if (c->ablate) {
-        ChainDev cha = ch;
-        cha.ablate = c->ablate;
-        HIPCHK(c, launch_swipes(0, cha, use_lds(c, ch), c->pb, bytes, offs, fixed_w, slot, n,
-                                c->regs, c->nslots, out, (unsigned long long *)c->err, c->cus,
-                                c->st));
-        return SKE_OK;
     }
     const PassMark m = mark_begin(c, 0);
     HIPCHK(c, launch_swipes(0, ch, use_lds(c, ch), c->pb, bytes, offs, fixed_w, slot, n, c->regs,
@@ -754,10 +698,6 @@ int ske_close(ske_ctx *c) {
         (void)hipEventDestroy(c->many_join[i]);
     }
     if (c->many_fork) (void)hipEventDestroy(c->many_fork);
-    for (hipStream_t x : c->cu_st)
-        if (x) (void)hipStreamDestroy(x);
-    for (hipEvent_t e : c->part_ev)
-        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->chunk_ev) (void)hipEventDestroy(e);
     if (c->copy_st) (void)hipStreamDestroy(c->copy_st);
     if (c->kt_key) (void)hipFree(c->kt_key);
@@ -859,72 +799,14 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
         c->pb = int(value);
         return SKE_OK;
     }
-    if (!strcmp(name, "xr_region_u") || !strcmp(name, "xr_finish_u")) {
-        // xr_region_u < 0: the per-step slice loop instead of the batched one
-        const int64_t a = (name[3] == 'r' && value < 0) ? -value : value;
-        if (a != 1 && a != 2 && a != 4 && a != 8) return SKE_EINVAL;
-        (name[3] == 'r' ? c->xr_region_u : c->xr_finish_u) = int(value);
-        return SKE_OK;
-    }
     if (!strcmp(name, "pass_timing")) {  // 1: bracket every K1 kernel with HIP events
         if (value < 0 || value > 1) return SKE_EINVAL;
         c->timing = value != 0;
         return SKE_OK;
     }
-    if (!strcmp(name, "hll_mode")) {  // partitioned K1's PFADD: 1 owned lines, 0 CAS
-        if (value < 0 || value > 1) return SKE_EINVAL;
-        c->hll_mode = int(value);
-        return SKE_OK;
-    }
-    if (!strcmp(name, "part_overlap")) {  // many-batch calls: pass C beside the next B (1) or A (2),
-                                          // or beside the next A on CU-partitioned streams (3)
-        if (value < 0 || value > 3) return SKE_EINVAL;
-        c->part_overlap = int(value);
-        return SKE_OK;
-    }
-    if (!strcmp(name, "part_ccus")) {  // part_overlap 3: CUs given to pass C (a divisor of the CU count)
-        if (value < 8 || value > c->cus / 2 || c->cus % value) return SKE_EINVAL;
-        c->part_ccus = int(value);
-        return SKE_OK;
-    }
-    if (!strcmp(name, "pa_tile")) {  // partitioned K1 tile: log2 swipes, 10 or 11
-        if (value != 10 && value != 11) return SKE_EINVAL;
-        c->pa_tile = int(value);
-        return SKE_OK;
-    }
-    if (!strcmp(name, "pa_precheck")) {  // partitioned K1: register pre-check in pass A (1) or pass C
-        if (value < 0 || value > 1) return SKE_EINVAL;
-        c->pa_pre = int(value);
-        return SKE_OK;
-    }
-    if (!strcmp(name, "pa_threads")) {  // fail-list pass A: threads per 1024-swipe tile
-        if (value != 512 && value != 1024) return SKE_EINVAL;
-        c->pa_threads = int(value);
-        return SKE_OK;
-    }
-    if (!strcmp(name, "pa_grid")) {  // partitioned K1: pass A blocks per CU (0 = default); fail-list
-                                     // pass A of <= 511 slices: 0 / 4 a 512-entry counter table at
-                                     // two blocks per CU, 3 that table at three blocks per CU, 2 the
-                                     // 2048-entry table; < 320 slices: 5 the counters in 16 copies
-                                     // (k_part_a4); A/B in DESIGN.md §3
-        if (value < 0 || value > 5) return SKE_EINVAL;
-        c->pa_grid = int(value);
-        return SKE_OK;
-    }
-    if (!strcmp(name, "pb_pairs")) {  // partitioned K1 pass B: 0 slices, 1 slice pairs + fail bytes,
-                                      // 2 slice pairs + fail lists (sketch_part.hip k_part_c_fl)
-        if (value < 0 || value > 2) return SKE_EINVAL;
-        c->pb_pairs = int(value);
-        return SKE_OK;
-    }
     if (!strcmp(name, "part_sub")) {  // partitioned K1 sub-batch (swipes; 0 = default)
         if (value < 0 || value > (int64_t(1) << 24)) return SKE_EINVAL;
         c->part_sub = uint32_t(value);
-        return SKE_OK;
-    }
-    if (!strcmp(name, "ablate")) {
-        if (value < 0 || value > 7) return SKE_EINVAL;
-        c->ablate = uint32_t(value);
         return SKE_OK;
     }
     if (!strcmp(name, "k1_grid")) {
@@ -935,11 +817,6 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
     if (!strcmp(name, "k1_persistent")) {  // 0: many-batch calls launch K1 per batch
         if (value < 0 || value > 1) return SKE_EINVAL;
         c->k1_persistent = int(value);
-        return SKE_OK;
-    }
-    if (!strcmp(name, "k1_legacy")) {
-        if (value < 0 || value > 1) return SKE_EINVAL;
-        c->k1_legacy = int(value);
         return SKE_OK;
     }
     if (!strcmp(name, "variant")) {
@@ -1411,16 +1288,16 @@ int ske_swipes_many_async(ske_ctx *c, uint32_t fid, const ske_swipe_batch *b, ui
                               b[j].n, b[j].out_valid, &A);
         if (ok) return swipes_many_persistent(c, A, b, nb);
     }
-    // the partitioned K1: one call over every batch (pass C beside the next
-    // A / B when pipelined), before any branch streams are made (it uses
-    // none; creating them lazily here cost ms of host time per new count)
-    const int var = (nb && !c->ablate) ? k1_variant(c, ch) : 0;
+    // the partitioned K1: one call over every batch, before any branch
+    // streams are made (it uses none; creating them lazily here cost ms of
+    // host time per new count)
+    const int var = nb ? k1_variant(c, ch) : 0;
     if (var == 3) {
         std::vector<PartBatch> pb(nb);
         for (uint32_t j = 0; j < nb; j++)
             pb[j] = PartBatch{b[j].bytes, b[j].width ? nullptr : b[j].offs, b[j].width, b[j].slot, b[j].n,
                               b[j].out_valid};
-        return launch_part(c, ch, pb.data(), nb, c->part_overlap != 0 && nb > 1);
+        return launch_part(c, ch, pb.data(), nb);
     }
     uint32_t br = branches ? branches : SKE_MANY_DEFAULT_BRANCHES;
     if (nb && br > nb) br = nb;
@@ -1476,6 +1353,23 @@ int ske_route_swipes(ske_ctx *c, const uint8_t *ids, uint32_t width, const uint3
     HIPCHK(c, hipMemcpyAsync(h, tot, size_t(world) * 4, hipMemcpyDeviceToHost, c->st));
     HIPCHK(c, hipStreamSynchronize(c->st));
     for (uint32_t o = 0; o < world; o++) counts[o] = h[o];
+    return SKE_OK;
+}
+
+int ske_route_swipes_cap_async(ske_ctx *c, const uint8_t *ids, uint32_t width, const uint32_t *gkey, uint64_t n,
+                               uint32_t world, const uint32_t *key_owner, const uint32_t *key_local, uint32_t nkeys,
+                               uint32_t cap, const uint32_t *sink_slots, uint8_t *send_ids, uint32_t *send_slots,
+                               uint32_t *pos, uint32_t *counts) {
+    if (!c || !counts || !sink_slots || world == 0 || world > 64 || width == 0 || width > 4096 ||
+        n >= (uint64_t(1) << 32) || cap == 0 || uint64_t(cap) * world >= (uint64_t(1) << 32))
+        return SKE_EINVAL;
+    if (!send_ids || !send_slots || (n && (!ids || !gkey || !pos))) return SKE_EINVAL;
+    if (nkeys && (!key_owner || !key_local)) return SKE_EINVAL;
+    hipError_t e = hipSuccess;
+    uint32_t *hist = (uint32_t *)scratch_get(c->scratch, 40, route_hist_words(n, world) * 4 + 4, &e);
+    if (e != hipSuccess) return scratch_error(c, e);
+    HIPCHK(c, launch_route_cap(ids, width, gkey, n, world, key_owner, key_local, nkeys, cap, sink_slots, send_ids,
+                               send_slots, pos, hist, counts, c->cus, c->st));
     return SKE_OK;
 }
 
@@ -1566,23 +1460,28 @@ int ske_swipes_fixed_bits(ske_ctx *c, uint32_t fid, const uint32_t *slot, const 
     // (earlier users of the staging buffers)
     HIPCHK(c, hipEventRecord(c->chunk_ev[0], c->st));
     HIPCHK(c, hipStreamWaitEvent(c->copy_st, c->chunk_ev[0], 0));
-    for (uint64_t j = 0; j < nchunks; j++) {
-        const uint64_t s0 = j * kFeedChunk, m = n - s0 < kFeedChunk ? n - s0 : kFeedChunk;
-        HIPCHK(c, stage_h2d(c->hs, db + s0 * width, bytes + s0 * width, m * width, c->copy_st, false, nullptr));
-        HIPCHK(c, stage_h2d(c->hs, ds + s0, slot + s0, m * 4, c->copy_st, false, nullptr));
-        HIPCHK(c, hipEventRecord(c->chunk_ev[j], c->copy_st));
-        HIPCHK(c, hipStreamWaitEvent(c->st, c->chunk_ev[j], 0));
-        rc = ske_swipes_fixed_async(c, fid, ds + s0, db + s0 * width, width, m, dans + s0);
-        if (rc) {
-            (void)hipStreamSynchronize(c->copy_st);  // the copies may still read the caller's buffers
-            return rc;
+    // once a copy is queued, every exit waits for the copy stream first: the
+    // DMA may still read the caller's (pinned) buffers
+    auto chunks = [&]() -> int {
+        for (uint64_t j = 0; j < nchunks; j++) {
+            const uint64_t s0 = j * kFeedChunk, m = n - s0 < kFeedChunk ? n - s0 : kFeedChunk;
+            HIPCHK(c, stage_h2d(c->hs, db + s0 * width, bytes + s0 * width, m * width, c->copy_st, false, nullptr));
+            HIPCHK(c, stage_h2d(c->hs, ds + s0, slot + s0, m * 4, c->copy_st, false, nullptr));
+            HIPCHK(c, hipEventRecord(c->chunk_ev[j], c->copy_st));
+            HIPCHK(c, hipStreamWaitEvent(c->st, c->chunk_ev[j], 0));
+            const int r = ske_swipes_fixed_async(c, fid, ds + s0, db + s0 * width, width, m, dans + s0);
+            if (r) return r;
+            if (out_bits) {
+                HIPCHK(c, launch_pack_bits(dans + s0, m, dbits + s0 / 8, c->cus, c->st));
+                HIPCHK(c, hipMemcpyAsync(out_bits + s0 / 8, dbits + s0 / 8, (m + 7) / 8, hipMemcpyDeviceToHost, c->st));
+            }
         }
-        if (out_bits) {
-            HIPCHK(c, launch_pack_bits(dans + s0, m, dbits + s0 / 8, c->cus, c->st));
-            HIPCHK(c, hipMemcpyAsync(out_bits + s0 / 8, dbits + s0 / 8, (m + 7) / 8, hipMemcpyDeviceToHost, c->st));
-        }
-    }
-    HIPCHK(c, hipStreamSynchronize(c->copy_st));
+        return SKE_OK;
+    };
+    rc = chunks();
+    const hipError_t se = hipStreamSynchronize(c->copy_st);
+    if (rc) return rc;
+    HIPCHK(c, se);
     return check_call_err(c);
 }
 

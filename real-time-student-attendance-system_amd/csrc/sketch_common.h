@@ -234,17 +234,10 @@ struct LinkDev {
 
 constexpr int kRegions = 8;  // one slice of every link per XCD
 
-// Diagnostic ablation bits (ske_set_option "ablate"; never set in production):
-// the timing of K1 with a part removed says what bounds it.
-constexpr uint32_t kAblateHll = 1;     // skip the HLL half (hash + register max)
-constexpr uint32_t kAblateProbe = 2;   // skip the Bloom probes (every swipe valid)
-constexpr uint32_t kAblateCas = 4;     // HLL hash + pre-check load, no CAS
-
 struct ChainDev {
     int32_t nlinks;
     uint32_t lds_bytes;  // sum of link bytes, 16-B aligned per link
-    uint32_t ablate;
-    uint32_t pad_;
+    uint32_t pad_[2];
     LinkDev link[kMaxLinks];
 };
 

@@ -86,6 +86,10 @@ hipError_t launch_route(const uint8_t *ids, uint32_t width, const uint32_t *slot
 uint64_t route_hist_words(uint64_t n, uint32_t world);
 // out (device) = answers in[0..n) packed 1 bit per swipe, LSB first; in must be 8-B aligned
 hipError_t launch_pack_bits(const uint8_t *in, uint64_t n, uint8_t *out, int cus, hipStream_t st);
+hipError_t launch_route_cap(const uint8_t *ids, uint32_t width, const uint32_t *slot, uint64_t n, uint32_t world,
+                            const uint32_t *kown, const uint32_t *kloc, uint32_t nkeys, uint32_t cap,
+                            const uint32_t *sink, uint8_t *sids, uint32_t *sslot, uint32_t *pos, uint32_t *hist,
+                            uint32_t *tot, int cus, hipStream_t st);
 hipError_t launch_route_return(const uint8_t *ans, const uint32_t *pos, uint64_t n, uint8_t *out, int cus,
                                hipStream_t st);
 
@@ -137,8 +141,6 @@ struct Scratch;
 bool part_supported(const ChainDev &ch);
 // sizes the context scratch for batches of up to n swipes (no launch)
 // sub: swipes per sub-batch of the three passes (0: the default, 16M)
-// hll_mode: 1 = PFADD by owned register lines (partitioned, no atomics),
-//           0 = per-swipe pre-check + CAS
 hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub, Scratch *scr);
 // hook (may be null): called as hook(user, pass, 0) right before and
 // hook(user, pass, 1) right after each pass's launch (pass 0..2 = A, B, C)
@@ -151,15 +153,10 @@ struct PartBatch {
     uint64_t n;
     uint8_t *out;          // may be nullptr
 };
-// side == nullptr: every pass on st; else pass C on `side` (ev: 4 events);
-// ovl 3: pass A on `side_a`, B on st, C on `side` (CU-masked streams: C on
-// c_cus CUs, A on the others)
+// every pass of every (batch, sub-batch) unit on st, in order
 hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t nb, uint8_t *regs,
                               uint32_t nslots, Scratch *scr, unsigned int *err, int cus, uint32_t sub,
-                              int hll_mode, int pb_pairs, int tile_opt, int pre_opt, int ovl, int a_grid, hipStream_t st, hipStream_t side,
-                              hipEvent_t *ev,
-                              PassHook hook = nullptr, void *hook_user = nullptr, int a3_threads = 512,
-                              hipStream_t side_a = nullptr, int c_cus = 0);
+                              hipStream_t st, PassHook hook = nullptr, void *hook_user = nullptr);
 
 
 // sketch_order.hip -- order-exact paths (replies that depend on item order)

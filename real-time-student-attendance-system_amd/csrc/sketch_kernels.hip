@@ -181,8 +181,6 @@ __global__ void __launch_bounds__(kLds ? 1024 : 256)
     const uint64_t c1 = c0 + per_block < n ? c0 + per_block : n;
     bool staged = !kLds;
     uint32_t probes = 0, nvalid = 0;
-    const bool ablate_probe = kMode == kModeSwipes && (ch.ablate & kAblateProbe);
-    const bool do_hll = kMode == kModeSwipes && !(ch.ablate & kAblateHll);
     // a block with no work still joins the staging barrier below
     int tile_no = 0;
     SKE_STAMP(0, 0);
@@ -201,7 +199,7 @@ __global__ void __launch_bounds__(kLds ? 1024 : 256)
                 const uint64_t b = fixed_w ? i * fixed_w : offs[i];
                 const uint64_t e = fixed_w ? b + fixed_w : offs[i + 1];
                 it[u] = load_item(bytes, b, e);
-                if (do_hll) sl[u] = slot[i];
+                if (kMode == kModeSwipes) sl[u] = slot[i];
             }
         }
         if (!staged) {
@@ -243,7 +241,7 @@ __global__ void __launch_bounds__(kLds ? 1024 : 256)
                 reg[u] = nullptr;
                 rank[u] = 0;
                 cur[u] = 0xffu;
-                if (do_hll && act[u] && sl[u] < nslots) {
+                if (act[u] && sl[u] < nslots) {
                     uint32_t idx;
                     hll_patlen(hh[u], idx, rank[u]);
                     reg[u] = regs + size_t(sl[u]) * kHllRegs + idx;
@@ -255,34 +253,25 @@ __global__ void __launch_bounds__(kLds ? 1024 : 256)
         SKE_STAMP(tile_no, 3);
         bool valid[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) valid[u] = ablate_probe && act[u];
-        if (!ablate_probe) {
-            for (int l = ch.nlinks - 1; l >= 0; --l) {
-                const LinkDev &L = ch.link[l];
-                if (kLds && L.div.d <= (uint64_t(1) << 31))
-                    link_probe_lds32<U>(L, lds_img, ha, hb, act, valid, probes);
-                else if (L.div.d <= (uint64_t(1) << 31))
-                    link_probe<kLds, U, ProbeCursor32>(L, lds_img, ha, hb, act, valid, probes);
-                else
-                    link_probe<kLds, U, ProbeCursor>(L, lds_img, ha, hb, act, valid, probes);
-            }
+        for (int u = 0; u < U; u++) valid[u] = false;
+        for (int l = ch.nlinks - 1; l >= 0; --l) {
+            const LinkDev &L = ch.link[l];
+            if (kLds && L.div.d <= (uint64_t(1) << 31))
+                link_probe_lds32<U>(L, lds_img, ha, hb, act, valid, probes);
+            else if (L.div.d <= (uint64_t(1) << 31))
+                link_probe<kLds, U, ProbeCursor32>(L, lds_img, ha, hb, act, valid, probes);
+            else
+                link_probe<kLds, U, ProbeCursor>(L, lds_img, ha, hb, act, valid, probes);
         }
         SKE_STAMP(tile_no, 4);
         if constexpr (kMode == kModeSwipes) {
-            if (do_hll) {
 #pragma unroll
-                for (int u = 0; u < U; u++) {
-                    if (!valid[u]) continue;
-                    if (sl[u] >= nslots) {
-                        atomicOr(reinterpret_cast<unsigned int *>(stats), 1u);
-                    } else if (cur[u] < rank[u]) {
-                        // the pre-check may be stale but is never too high
-                        if (ch.ablate & kAblateCas) {
-                            if (out) out[base + uint64_t(u) * T + tid] = 2;
-                        } else {
-                            reg_max(reg[u], rank[u]);
-                        }
-                    }
+            for (int u = 0; u < U; u++) {
+                if (!valid[u]) continue;
+                if (sl[u] >= nslots) {
+                    atomicOr(reinterpret_cast<unsigned int *>(stats), 1u);
+                } else if (cur[u] < rank[u]) {
+                    reg_max(reg[u], rank[u]);  // the pre-check may be stale but is never too high
                 }
             }
             SKE_STAMP(tile_no, 5);

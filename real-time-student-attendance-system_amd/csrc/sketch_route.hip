@@ -136,6 +136,81 @@ __global__ void __launch_bounds__(kRtBlock) k_route_scatter(const RouteArgs R) {
     }
 }
 
+// Capacity-padded layout (the host-free exchange): owner o's swipes go to
+// rows [o * cap, o * cap + tot[o]) of the send buffers, so every rank sends
+// and receives exactly `cap` rows per peer (an all_to_all of equal splits,
+// whose sizes the host knows without reading the device).  A swipe ranked
+// past cap in its owner is not sent (pos = its row modulo cap: a row of the
+// same owner, answered for another swipe) -- tot[o] > cap tells the host,
+// which then re-runs the batch with exact splits (PFADD is idempotent and
+// the answers are rewritten).
+__global__ void __launch_bounds__(kRtBlock) k_route_scatter_cap(const RouteArgs R, uint32_t cap) {
+    __shared__ uint32_t c[kRtMaxWorld], base[kRtMaxWorld];
+    const uint32_t tid = threadIdx.x;
+    if (tid < R.world) {
+        c[tid] = 0;
+        // this block's first rank within its owner (the scan is owner major)
+        base[tid] = R.hist[size_t(tid) * R.nblocks + blockIdx.x] - R.hist[size_t(tid) * R.nblocks];
+    }
+    __syncthreads();
+    const uint64_t b0 = uint64_t(blockIdx.x) * kRtTile;
+#pragma unroll 4
+    for (uint32_t j = 0; j < kRtItems; j++) {
+        const uint64_t i = b0 + j * kRtBlock + tid;
+        if (i >= R.n) continue;
+        const uint32_t g = R.slot[i];
+        const uint32_t o = route_owner(R, g);
+        const uint32_t r = base[o] + atomicAdd(&c[o], 1u);
+        const uint32_t p = o * cap + (r < cap ? r : r % cap);
+        R.pos[i] = p;
+        if (r >= cap) continue;  // overflow: tot[o] > cap reports it
+        R.sslot[p] = route_known(R, g) ? R.kloc[g] : kNoSlot;
+        const uint8_t *src = R.ids + i * R.width;
+        uint8_t *dst = R.sids + uint64_t(p) * R.width;
+        if (R.width == 8) {
+            *reinterpret_cast<uint64_t *>(dst) = *reinterpret_cast<const uint64_t *>(src);
+        } else {
+            for (uint32_t k = 0; k < R.width; k++) dst[k] = src[k];
+        }
+    }
+}
+
+// rows [tot[o], cap) of owner o: id bytes zero, slot sink[o] (a slot the
+// owner keeps for nothing else, so the padding's PFADDs change no key)
+__global__ void __launch_bounds__(256) k_route_pad(const RouteArgs R, uint32_t cap, const uint32_t *sink) {
+    const uint64_t rows = uint64_t(R.world) * cap;
+    for (uint64_t j = uint64_t(blockIdx.x) * 256 + threadIdx.x; j < rows; j += uint64_t(gridDim.x) * 256) {
+        const uint32_t o = uint32_t(j / cap), r = uint32_t(j % cap);
+        if (r < R.tot[o]) continue;
+        R.sslot[j] = sink[o];
+        uint8_t *dst = R.sids + j * R.width;
+        for (uint32_t k = 0; k < R.width; k++) dst[k] = 0;
+    }
+}
+
+hipError_t launch_route_cap(const uint8_t *ids, uint32_t width, const uint32_t *slot, uint64_t n, uint32_t world,
+                            const uint32_t *kown, const uint32_t *kloc, uint32_t nkeys, uint32_t cap,
+                            const uint32_t *sink, uint8_t *sids, uint32_t *sslot, uint32_t *pos, uint32_t *hist,
+                            uint32_t *tot, int cus, hipStream_t st) {
+    if (world == 0 || world > kRtMaxWorld || width == 0 || n >= (uint64_t(1) << 32) || cap == 0 ||
+        uint64_t(cap) * world >= (uint64_t(1) << 32))
+        return hipErrorInvalidValue;
+    RouteArgs R{ids, slot, kown, kloc, sids, sslot, pos, hist, tot, n, width, world,
+                uint32_t((n + kRtTile - 1) / kRtTile), nkeys};
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(tot, 0, size_t(world) * 4, st);
+        if (e != hipSuccess) return e;
+    } else {
+        hipLaunchKernelGGL(k_route_count, dim3(R.nblocks), dim3(kRtBlock), 0, st, R);
+        hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(1024), 0, st, R);
+        hipLaunchKernelGGL(k_route_scatter_cap, dim3(R.nblocks), dim3(kRtBlock), 0, st, R, cap);
+    }
+    const uint64_t g = (uint64_t(world) * cap + 255) / 256;
+    hipLaunchKernelGGL(k_route_pad, dim3(unsigned(g < uint64_t(cus) * 8 ? g : uint64_t(cus) * 8)), dim3(256), 0, st,
+                       R, cap, sink);
+    return hipGetLastError();
+}
+
 __global__ void __launch_bounds__(256) k_route_return(const uint8_t *ans, const uint32_t *pos, uint64_t n,
                                                       uint8_t *out) {
     for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256)

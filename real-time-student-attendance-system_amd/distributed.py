@@ -42,6 +42,7 @@ logic runs unchanged with ``gloo`` on CPU tensors in the tests.
 from __future__ import annotations
 
 import ctypes as C
+import math
 from typing import Sequence
 
 import numpy as np
@@ -265,7 +266,8 @@ class SwipeExchange:
     on host copies.
     """
 
-    def __init__(self, rank: int, world: int, k1, keymap: KeyMap, group=None, engine=None):
+    def __init__(self, rank: int, world: int, k1, keymap: KeyMap, group=None, engine=None,
+                 sink_slots=None, slack: float = 0.15):
         import torch
         import torch.distributed as dist
         assert keymap.world == world, "the key map was built for another world size"
@@ -278,6 +280,23 @@ class SwipeExchange:
         self.engine = engine
         backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
         self.device_collectives = backend == "nccl"
+        # swipes_async: sink_slots[r] = a local slot rank r keeps for no key
+        # (it absorbs the padding rows' PFADDs); slack = capacity over an
+        # even share, adapted by settle() to the largest share it has seen
+        self.sink = None if sink_slots is None else np.asarray(sink_slots, np.int64).astype(np.uint32)
+        assert self.sink is None or self.sink.size == world
+        self.slack = float(slack)
+        self.pending = []
+        self._free_pinned = []
+        self.stats = {"batches": 0, "redone": 0, "max_share": 0.0}
+
+    def capacity(self, n_max: int) -> int:
+        """Rows per peer of the equal-split exchange for batches of at most
+        n_max swipes (the same on every rank: a function of n_max, the world
+        size and the slack every rank derives alike)."""
+        if self.world == 1:
+            return max(1, int(n_max))
+        return min(int(n_max), math.ceil(int(n_max) * (1.0 + self.slack) / self.world)) + 256
 
     def owner_local(self, gkeys):
         """(owner, local slot) of global key indices (torch tensors)."""
@@ -329,6 +348,156 @@ class SwipeExchange:
         ans = torch.empty_like(back)
         ans[order] = back
         return ans
+
+    # ---- host-free form: equal splits of `cap` rows per peer
+    def swipes_async(self, ids, gkeys, n_max: int | None = None):
+        """``swipes`` with no host synchronisation (enqueue only on a device).
+
+        Every peer pair exchanges exactly ``cap = capacity(n_max)`` rows
+        (n_max: the largest batch any rank passes in this call; default this
+        batch's size, so ranks must then pass equal sizes), so the splits are
+        known without reading the routing counts: owner o's swipes fill rows
+        [o*cap, o*cap + count_o), the rest are padding (zero ids into the
+        owner's sink slot).  The answers tensor is returned at once and is
+        final after ``settle()``, which every rank calls at the same point:
+        a batch in which some owner got more than cap swipes on any rank is
+        then run again through ``swipes`` (exact splits; PFADD is idempotent
+        and its answers are rewritten)."""
+        torch = self.torch
+        if self.sink is None:
+            raise ValueError("swipes_async needs sink_slots (one spare local slot per rank)")
+        n, w = ids.shape
+        cap = self.capacity(n if n_max is None else n_max)
+        assert n <= (n if n_max is None else n_max)
+        dev = ids.device
+        if self.engine is not None and ids.is_cuda:
+            send_ids, send_slots, pos, counts = self._route_cap_native(ids, gkeys, cap)
+        else:
+            send_ids, send_slots, pos, counts = self._route_cap_torch(ids, gkeys, cap)
+        rows = self.world * cap
+        r_flat = torch.zeros(rows * w + 16, dtype=torch.uint8, device=dev)
+        self._a2a(r_flat[:rows * w], send_ids.reshape(-1), None, None)
+        r_slots = torch.empty(rows, dtype=torch.int32, device=dev)
+        self._a2a(r_slots, send_slots, None, None)
+        r_ans = self.k1(r_flat[:rows * w].view(rows, w), r_slots)
+        back = torch.empty(rows, dtype=torch.uint8, device=dev)
+        self._a2a(back, r_ans.to(torch.uint8), None, None)
+        ans = self._gather(back, pos, n)
+        if counts.is_cuda:
+            # pinned landing rows for the counts, reused once settled
+            host = self._free_pinned.pop() if self._free_pinned else \
+                torch.empty(self.world, dtype=torch.int32, pin_memory=True)
+            host.copy_(counts, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host, ev = counts.to(torch.int32), None
+        self.pending.append({"ids": ids, "gkeys": gkeys, "ans": ans, "counts": host, "ev": ev, "cap": cap,
+                             "n": n})
+        return ans
+
+    def settle(self) -> int:
+        """Finish every swipes_async batch since the last settle (collective:
+        every rank calls it at the same point).  Returns the batches re-run
+        because some owner overflowed its capacity on some rank; adapts the
+        slack to the largest owner share seen (the same on every rank)."""
+        torch = self.torch
+        pend, self.pending = self.pending, []
+        if not pend:
+            return 0
+        flags, share = [], 0.0
+        for p in pend:
+            if p["ev"] is not None:
+                p["ev"].synchronize()
+            c = p["counts"].numpy().astype(np.int64)
+            if p["ev"] is not None:
+                self._free_pinned.append(p["counts"])
+            flags.append(int(c.max(initial=0) > p["cap"]))
+            if p["n"]:
+                share = max(share, float(c.max(initial=0)) * self.world / p["n"])
+        v = torch.tensor(flags + [int(share * 1e6)], dtype=torch.int64)
+        if self.world > 1:
+            if self.device_collectives:
+                v = v.to(pend[0]["ans"].device)
+            self.dist.all_reduce(v, op=self.dist.ReduceOp.MAX, group=self.group)
+            v = v.cpu()
+        v = v.tolist()
+        redo = 0
+        for p, f in zip(pend, v[:-1]):
+            if f:
+                p["ans"].copy_(self.swipes(p["ids"], p["gkeys"]))
+                redo += 1
+        gshare = v[-1] / 1e6
+        self.stats["batches"] += len(pend)
+        self.stats["redone"] += redo
+        self.stats["max_share"] = max(self.stats["max_share"], gshare)
+        if gshare > 0:
+            self.slack = max(0.02, gshare - 1.0 + 0.03)
+        return redo
+
+    def _route_cap_torch(self, ids, gkeys, cap):
+        torch = self.torch
+        n, w = ids.shape
+        dest, local = self.owner_local(gkeys)
+        order = torch.argsort(dest, stable=True)
+        counts = torch.bincount(dest, minlength=self.world)
+        starts = torch.cumsum(counts, 0) - counts
+        ds = dest[order]
+        r = torch.arange(n, device=ids.device) - starts[ds]
+        keep = r < cap
+        row = ds * cap + torch.where(keep, r, r % cap)
+        rows = self.world * cap
+        send_ids = torch.zeros((rows, w), dtype=torch.uint8, device=ids.device)
+        sink = torch.from_numpy(self.sink.astype(np.int64)).to(torch.int32).to(ids.device)
+        send_slots = sink[torch.arange(rows, device=ids.device) // cap]
+        send_ids[row[keep]] = ids[order][keep]
+        send_slots[row[keep]] = local[order][keep].to(torch.int32)
+        pos = torch.empty(n, dtype=torch.int64, device=ids.device)
+        pos[order] = row
+        return send_ids, send_slots, pos, counts
+
+    def _route_cap_native(self, ids, gkeys, cap):
+        torch = self.torch
+        n, w = ids.shape
+        dev = ids.device
+        ids = ids.contiguous()
+        g32 = gkeys.to(torch.int32).contiguous()
+        own, loc = self.keymap.tables(dev)
+        rows = self.world * cap
+        send_ids = torch.empty(rows * w, dtype=torch.uint8, device=dev)
+        send_slots = torch.empty(rows, dtype=torch.int32, device=dev)
+        pos = torch.empty(max(1, n), dtype=torch.int32, device=dev)
+        counts = torch.empty(self.world, dtype=torch.int32, device=dev)
+        if not hasattr(self, "_sink_dev"):
+            self._sink_dev = torch.from_numpy(self.sink.view(np.int32)).to(dev)
+        eng = self.engine
+        prev = eng.get_stream()
+        try:
+            eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+            eng.ctx.call("ske_route_swipes_cap_async", C.c_void_p(ids.data_ptr()), w, C.c_void_p(g32.data_ptr()), n,
+                         self.world, C.c_void_p(own.data_ptr()), C.c_void_p(loc.data_ptr()), len(self.keymap),
+                         cap, C.c_void_p(self._sink_dev.data_ptr()), C.c_void_p(send_ids.data_ptr()),
+                         C.c_void_p(send_slots.data_ptr()), C.c_void_p(pos.data_ptr()),
+                         C.c_void_p(counts.data_ptr()))
+        finally:
+            eng.set_stream(prev)
+        return send_ids.view(rows, w), send_slots, pos, counts
+
+    def _gather(self, back, pos, n):
+        """answers of the send rows back into input order"""
+        torch = self.torch
+        if self.engine is not None and back.is_cuda:
+            ans = torch.empty(n, dtype=torch.uint8, device=back.device)
+            eng = self.engine
+            prev = eng.get_stream()
+            try:
+                eng.set_stream(torch.cuda.current_stream(back.device).cuda_stream)
+                eng.ctx.call("ske_route_return_async", C.c_void_p(back.data_ptr()), C.c_void_p(pos.data_ptr()), n,
+                             C.c_void_p(ans.data_ptr()))
+            finally:
+                eng.set_stream(prev)
+            return ans
+        return back[pos[:n].to(torch.int64)]
 
     def _swipes_native(self, ids, gkeys):
         torch = self.torch

@@ -131,17 +131,26 @@ class AttendanceProcessor:
     def get_attendance_stats(self, lecture_id: str, day: str | None = None) -> dict:
         """PFCOUNT of the lecture's key (:151-152).  In the README key form a
         lecture is counted per day: with a day, that day's key; without one
-        (the reference's signature), the union of every day key of the
-        lecture in the store (SCAN MATCH prefix+lecture:*, so a fresh
-        processor on the same store answers the same) -- PFCOUNT k1 k2 ..."""
+        (the reference's signature), the union of every day key
+        prefix+lecture:YYYY-MM-DD in the store -- PFCOUNT k1 k2 ...  The day
+        keys come from the key table's stem index (KeySpace.day_keys, kept
+        by every key creation / DEL, so a fresh processor on the same store
+        answers the same without scanning every key; a lecture id that is a
+        prefix of another, e.g. 'A' and 'A:B', keeps its own keys)."""
         prefix = self.config.hll_key_prefix
         if self.config.hll_key_form == "code":
             key = f"{prefix}{lecture_id}" + (f":{day}" if day else "")
             return {"unique_attendees": self.redis_client.pfcount(key)}
         if day is not None:
             return {"unique_attendees": self.redis_client.pfcount(f"{prefix}{lecture_id}:{day}")}
-        pat = "".join("[" + ch + "]" if ch in "*?[]\\" else ch for ch in f"{prefix}{lecture_id}:")
-        keys = [k for k in self.redis_client.scan_iter(match=pat + "*", _type="string")]
+        stem = f"{prefix}{lecture_id}"
+        index = getattr(self.redis_client, "day_keys", None)
+        if callable(index):  # SketchClient: the key table's stem index
+            keys = index(stem)
+        else:  # any redis-py-like client: SCAN for exactly <stem>:YYYY-MM-DD
+            pat = "".join("[" + ch + "]" if ch in "*?[]\\^" else ch for ch in stem)
+            keys = list(self.redis_client.scan_iter(match=pat + ":" + "[0-9]" * 4 + "-" + "[0-9]" * 2 + "-" +
+                                                     "[0-9]" * 2, _type="string"))
         return {"unique_attendees": self.redis_client.pfcount(*keys) if keys else 0}
 
 

@@ -31,7 +31,7 @@ def groups(nm):
     return [nm[i::5] for i in range(5)] + [nm, []]
 
 
-def main(out_dir):
+def main(out_dir, mode="exact"):
     import torch
     import torch.distributed as dist
     import __graft_entry__ as ge
@@ -52,7 +52,8 @@ def main(out_dir):
     client = pkg.SketchClient(context=eng.ctx)
     km.bind(client, rank)
     nlocal = km.slots_end(rank)
-    eng.hll_reserve(max(1, nlocal))
+    sinks = [km.slots_end(r) for r in range(world)]  # one spare slot past the universe per rank
+    eng.hll_reserve(nlocal + 1)
     n = N - 1000 * rank                      # uneven slices
     b = eng.swipe_batch(p, rank * N, n)
     buf, offs, slot = b.to_host()
@@ -60,8 +61,31 @@ def main(out_dir):
     assert (np.diff(offs.astype(np.int64)) == width).all()
     ids = torch.from_numpy(buf[:n * width].reshape(n, width).copy()).cuda()
     slots = torch.from_numpy(slot.astype(np.int64)).cuda()
-    ex = SwipeExchange(rank, world, engine_k1(eng), km, engine=eng)
-    ans = ex.swipes(ids, slots)
+    k1 = engine_k1(eng)
+    if os.environ.get("EXCH_DEBUG"):
+        # every K1 call: its slots must all be local slots of this rank
+        k1_plain = k1
+
+        def k1(ids_, slots_):  # noqa: F811
+            torch.cuda.synchronize()
+            sl = slots_.cpu().numpy().view(np.uint32)
+            print(f"rank {rank} k1 rows {sl.size} max slot {sl.max() if sl.size else -1} nslots {nlocal + 1}",
+                  file=sys.stderr, flush=True)
+            r = k1_plain(ids_, slots_)
+            torch.cuda.synchronize()
+            eng.sync()
+            return r
+    ex = SwipeExchange(rank, world, k1, km, engine=eng, sink_slots=sinks,
+                       slack=-0.6 if mode == "async_overflow" else world - 1.0)
+    if mode == "exact":
+        ans = ex.swipes(ids, slots)
+    else:
+        h = N // 2  # n_max: no rank's half-slice is longer
+        a0 = ex.swipes_async(ids[:h], slots[:h], n_max=h)
+        a1 = ex.swipes_async(ids[h:], slots[h:], n_max=h)
+        redone = ex.settle()
+        assert (redone == 2) == (mode == "async_overflow"), (mode, redone, ex.stats)
+        ans = torch.cat([a0, a1])
     torch.cuda.synchronize()
     eng.sync()
     sk = ShardedSketch(client, rank, world)
@@ -76,4 +100,4 @@ def main(out_dir):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "exact")

@@ -49,3 +49,20 @@ def test_keyhash_matches_oracle(orc):
         d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
         for seed in (0, 0xADC83B19, 2**64 - 1):
             assert murmur64a(d, seed) == orc.murmur64a(d, seed)
+
+
+def test_redis_glob_dialect(pkg):
+    """SCAN MATCH follows Redis' stringmatchlen (redis src/util.c, restated in
+    client.redis_glob), not Python's fnmatch: '^' negates a class, backslash
+    escapes, reversed ranges are swapped.  No Redis in this image: the cases
+    are the rule read from the source -- parity unpinned."""
+    from rtsas_amd.client import redis_glob as g
+    assert g(b"[^a]*", b"bcd") and not g(b"[^a]*", b"abc")
+    assert g(b"h[!e]llo", b"h!llo") and g(b"h[!e]llo", b"hello") and not g(b"h[!e]llo", b"hallo")  # "!" is a member
+    assert g(b"foo\\*", b"foo*") and not g(b"foo\\*", b"foox")
+    assert g(b"h[e-a]llo", b"hallo") and g(b"h[a-e]llo", b"hello") and not g(b"h[^e]llo", b"hello")
+    assert g(b"h[\\]]llo", b"h]llo")
+    assert g(b"a*c", b"abbbc") and g(b"**b", b"ab") and g(b"a?c", b"abc") and not g(b"a?c", b"ac")
+    assert g(b"hll:unique:L1:????-??-??", b"hll:unique:L1:2025-03-19")
+    assert not g(b"hll:unique:L1:????-??-??", b"hll:unique:L1:x:2025-03-19")
+    assert not g(b"*", b"")  # stringmatchlen itself; SCAN / KEYS bypass a bare '*'

@@ -100,7 +100,7 @@ class _StoreOps:
                         np.uint64)
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, mode="exact"):
     import sys
     sys.path.insert(0, ROOT)
     import __graft_entry__ as ge
@@ -113,7 +113,8 @@ def _worker(rank, world, port, out_dir):
     names = _names()
     km = KeyMap(names, world)
     chain = _chain(orc)
-    regs = np.zeros((km.slots_end(rank), 16384), np.uint8)
+    # one spare slot past the universe: the sink of swipes_async's padding rows
+    regs = np.zeros((km.slots_end(rank) + 1, 16384), np.uint8)
     slot_of = {km.names[g]: int(km.local[g]) for g in km.keys_of(rank)}
 
     def k1(ids, local_slots):   # the oracle as this rank's K1
@@ -123,9 +124,23 @@ def _worker(rank, world, port, out_dir):
         v, _, _ = orc.process_swipes(chain, regs, local_slots.numpy().astype(np.uint32), buf, offs)
         return torch.from_numpy(v.astype(np.uint8))
 
-    ex = SwipeExchange(rank, world, k1, km)
+    sinks = [km.slots_end(r) for r in range(world)]
+    # async: a capacity of a whole batch per peer (never overflows);
+    # async_overflow: 0.4 of an even share (always overflows)
+    slack = {"exact": 0.1, "async": world - 1.0, "async_overflow": -0.6}[mode]
+    ex = SwipeExchange(rank, world, k1, km, sink_slots=sinks, slack=slack)
     buf, gkey = _stream(rank)
-    ans = ex.swipes(torch.from_numpy(buf), torch.from_numpy(gkey))
+    if mode == "exact":
+        ans = ex.swipes(torch.from_numpy(buf), torch.from_numpy(gkey))
+    else:
+        # two batches of this rank's slice, host-free form, then settle
+        h = N // 2  # n_max: no rank's batch is longer (rank r's slice is N - 113 r)
+        a0 = ex.swipes_async(torch.from_numpy(buf[:h]), torch.from_numpy(gkey[:h]), n_max=h)
+        a1 = ex.swipes_async(torch.from_numpy(buf[h:]), torch.from_numpy(gkey[h:]), n_max=h)
+        redone = ex.settle()
+        assert (redone == 2) == (mode == "async_overflow"), (mode, redone, ex.stats)
+        assert ex.stats["max_share"] > 1.0
+        ans = torch.cat([a0, a1])
     sk = ShardedSketch(None, rank, world, ops=_StoreOps(orc, regs, slot_of))
     union = sk.pfcount_union(names)
     each = sk.pfcount_each(names)
@@ -136,9 +151,15 @@ def _worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_exchange_then_sharded_queries_equal_one_shard(orc, tmp_path, world):
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+@pytest.mark.parametrize("world,mode", [(2, "exact"), (3, "exact"), (2, "async"), (3, "async"),
+                                        (2, "async_overflow")])
+def test_exchange_then_sharded_queries_equal_one_shard(orc, tmp_path, world, mode):
+    """mode exact: SwipeExchange.swipes (alltoallv of exact splits, the host
+    reads the routing counts); async: swipes_async (equal splits of a
+    capacity, padding into a sink slot, no host read) over two batches, then
+    settle(); async_overflow: a capacity below the owners' shares, so
+    settle() re-runs both batches with exact splits."""
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world, join=True)
     names = _names()
     chain = _chain(orc)
     regs = np.zeros((len(names), 16384), np.uint8)

@@ -796,3 +796,19 @@ def test_host_staged_large_offsets_checked_on_the_pinned_copy(engine, pkg, orc, 
     e2.swipes(0, b, dout)
     assert np.array_equal(out, dout.to_host(np.uint8, n))
     assert np.array_equal(regs_host, e2.registers_all(16))
+
+
+def test_product_options_only(engine):
+    """The shipped library takes only the six tuning options; the diagnostic
+    and measured-slower knobs of earlier rounds (ablate, hll_mode,
+    part_overlap, ...) are gone and refused: no option can
+    make an answer or a register wrong."""
+    from rtsas_amd._lib import SKE_EINVAL
+    lib, ptr = engine.ctx.lib, engine.ctx.ptr
+    for name in [b"ablate", b"hll_mode", b"part_overlap", b"part_ccus", b"pa_tile", b"pa_precheck",
+                 b"pa_grid", b"pa_threads", b"pb_pairs", b"k1_legacy", b"xr_region_u", b"xr_finish_u"]:
+        assert lib.ske_set_option(ptr, name, 1) == SKE_EINVAL, name
+    for name, val in [(b"variant", -1), (b"tile", 2), (b"k1_grid", 0), (b"k1_persistent", 1),
+                      (b"part_sub", 0), (b"pass_timing", 0)]:
+        assert lib.ske_set_option(ptr, name, val) == 0, name
+    assert lib.ske_set_option(ptr, b"tile", 3) == SKE_EINVAL

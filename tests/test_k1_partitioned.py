@@ -33,11 +33,11 @@ def _pack(items):
     return buf, offs
 
 
-@pytest.mark.parametrize("hll_mode", [1, 0])
-def test_partitioned_two_link_chain_ragged(engine, orc, hll_mode):
+def test_partitioned_two_link_chain_ragged(engine, orc):
     """RESERVE 0.01 / 20000 grown to two links (k = 8, 9: 17 probes per swipe,
-    tiles of 1024 swipes), ragged ids; the partitioned kernel forced, its
-    PFADD by owned register lines (1) or by CAS (0)."""
+    tiles of 1024 swipes), ragged ids; the partitioned kernel forced (the
+    general instantiation: k_part_a<22>, single-slice k_part_b<1>, fail
+    bytes, k_part_c)."""
     from rtsas_amd.engine import DeviceBatch, DeviceBuffer
     rng = np.random.default_rng(21)
     members = _rand_items(rng, 30000, 40, 1)
@@ -51,7 +51,6 @@ def test_partitioned_two_link_chain_ragged(engine, orc, hll_mode):
     chain.madd_packed(mb, mo)
     assert chain.nlinks == 2
     engine.set_option("variant", 3)
-    engine.set_option("hll_mode", hll_mode)
     assert engine.variant(0) == 3
     items = [members[int(i)] for i in rng.integers(0, len(members), 60000)]
     items += _rand_items(rng, 20000, 40)
@@ -68,10 +67,9 @@ def test_partitioned_two_link_chain_ragged(engine, orc, hll_mode):
     assert np.array_equal(engine.registers_all(37), regs)
 
 
-@pytest.mark.parametrize("hll_mode", [0, 1])
-def test_c3_geometry_ragged_long_ids(engine, orc, hll_mode):
+def test_c3_geometry_ragged_long_ids(engine, orc):
     """The one-link k = 11 chain of C3's RESERVE 0.001 / 1e7 (the fail-list
-    pass A k_part_a3 with CAS PFADD, or the line-owned PFADD) on ids of 0..40
+    path: k_part_a3, k_part_b<2, 4, true>, k_part_c_fl) on ids of 0..40
     bytes: empty ids and ids longer than 8 bytes take pass A's generic
     MurmurHash64A; a ragged last tile; answers and registers == the oracle."""
     from rtsas_amd.engine import DeviceBatch, DeviceBuffer
@@ -85,7 +83,6 @@ def test_c3_geometry_ragged_long_ids(engine, orc, hll_mode):
     chain = orc.Chain(10_000_000, 0.001)
     chain.madd_packed(mb, mo)
     assert chain.nlinks == 1 and chain.link_info(0)["hashes"] == 11
-    engine.set_option("hll_mode", hll_mode)
     assert engine.variant(0) == 3
     items = [members[int(i)] for i in rng.integers(0, len(members), 90000)]
     items += _rand_items(rng, 30000, 40) + [b""] * 50 + [b"12345678", b"123456789"]
@@ -199,18 +196,19 @@ def test_graph_replay_then_direct_launch_other_stream(engine, orc):
 
 
 @pytest.mark.parametrize("invalid", [0.1, 0.5, 1.0])
-@pytest.mark.parametrize("pb_mode", [2, 1])
-def test_fail_lists_and_overflow_vs_oracle(engine, orc, invalid, pb_mode):
-    """Pass B -> C through fail lists (pb_pairs 2, the default) or fail bytes
-    (1) on the C3 filter: at 100 % invalid every (slice pair, tile) list
-    overflows into the fail bytes many times over, at 10 % a few do; a
-    ragged last tile; answers and registers == the oracle."""
+@pytest.mark.parametrize("error", [0.001, 0.0001])
+def test_fail_lists_and_overflow_vs_oracle(engine, orc, invalid, error):
+    """error 0.001 (C3's filter, one link of k = 11): pass B -> C through fail
+    lists; at 100 % invalid every (slice pair, tile) list overflows into the
+    fail bytes many times over, at 10 % a few do.  error 0.0001 (one link of
+    k = 15, 394 slices): the general instantiation on slice pairs (k_part_a<22>,
+    k_part_b<2>, fail bytes, k_part_c).  A ragged last tile; answers and
+    registers == the oracle."""
     from rtsas_amd import synthetic
     from rtsas_amd.engine import DeviceBuffer
     w = synthetic.WORKLOADS["c3"]
     w = synthetic.Workload(**{**w.__dict__, "n_members": 300_000, "n_keys": 97, "zipf_lectures": 0,
-                              "zipf_days": 0, "invalid_frac": invalid})
-    engine.set_option("pb_pairs", pb_mode)
+                              "zipf_days": 0, "invalid_frac": invalid, "bf_error": error})
     engine.reserve(0, w.bf_error, w.bf_capacity)
     p = engine.gen_params(w, seed=4242)
     engine.preload(0, p, w.n_members)
@@ -232,18 +230,17 @@ def test_fail_lists_and_overflow_vs_oracle(engine, orc, invalid, pb_mode):
 
 
 @pytest.mark.parametrize("invalid", [0.1, 1.0])
-@pytest.mark.parametrize("pa_grid", [3, 4, 5])
-def test_pass_a_counter_layouts_vs_oracle(engine, orc, invalid, pa_grid):
-    """The fail-list pass A's counter-table forms on the C3 filter (303
-    slices): a 512-entry table at three (3) or two (4) blocks per CU, and the
-    slice counters spread over 16 copies (5, k_part_a4); a ragged last tile;
-    answers and registers == the oracle."""
+@pytest.mark.parametrize("capacity", [10_000_000, 20_000_000])
+def test_pass_a_counter_layouts_vs_oracle(engine, orc, invalid, capacity):
+    """The fail-list pass A's two counter tables: the 512-entry table of
+    chains under 512 slices (C3's 1e7 filter: 303) and the 2048-entry table
+    (2e7: 604 slices); a ragged last tile; answers and registers == the
+    oracle."""
     from rtsas_amd import synthetic
     from rtsas_amd.engine import DeviceBuffer
     w = synthetic.WORKLOADS["c3"]
     w = synthetic.Workload(**{**w.__dict__, "n_members": 300_000, "n_keys": 97, "zipf_lectures": 0,
-                              "zipf_days": 0, "invalid_frac": invalid})
-    engine.set_option("pa_grid", pa_grid)
+                              "zipf_days": 0, "invalid_frac": invalid, "bf_capacity": capacity})
     engine.reserve(0, w.bf_error, w.bf_capacity)
     p = engine.gen_params(w, seed=4243)
     engine.preload(0, p, w.n_members)
@@ -280,18 +277,12 @@ def test_hll_reserve_refused_while_graph_alive(engine):
     engine.hll_reserve(cap + 100)  # no graph holds the slab any more
 
 
-@pytest.mark.parametrize("hll_mode,pa_tile,pre", [(1, 10, 0), (0, 10, 0), (0, 11, 0), (0, 10, 1)])
-def test_partitioned_hot_register_and_many_keys(engine, orc, hll_mode, pa_tile, pre):
-    """Adversarial PFADD shapes for the line-owned apply: 2M swipes where half
-    repeat ONE id into ONE key (one register line takes a million updates) and
-    the rest spread over 40k keys (many lines per sub-bucket); registers ==
-    the oracle.  pre = 1: pass A pre-checks the registers and pass C only
-    raises (option pa_precheck)."""
+def test_partitioned_hot_register_and_many_keys(engine, orc):
+    """Adversarial PFADD shapes for pass C's CAS: 2M swipes where half repeat
+    ONE id into ONE key (one register word takes a million racing updates)
+    and the rest spread over 40k keys; registers == the oracle."""
     from rtsas_amd.engine import DeviceBatch, DeviceBuffer
     w, p = _c3_small(engine)
-    engine.set_option("hll_mode", hll_mode)
-    engine.set_option("pa_tile", pa_tile)   # 11: 2048-swipe tiles (k_part_a2<11, 1024>, pass B R = 6)
-    engine.set_option("pa_precheck", pre)
     engine.hll_reserve(40_001)
     b = engine.swipe_batch(p, 0, 2_000_000)
     buf, offs, slot = b.to_host()
@@ -315,27 +306,17 @@ def test_partitioned_hot_register_and_many_keys(engine, orc, hll_mode, pa_tile, 
     assert np.array_equal(engine.registers_all(40_001), regs)
 
 
-@pytest.mark.parametrize("mode,ovl,pre,ccus", [("direct", 1, 0, 0), ("graph", 1, 0, 0), ("direct", 2, 0, 0),
-                                               ("graph", 2, 1, 0), ("direct", 2, 1, 0), ("direct", 3, 0, 0),
-                                               ("graph", 3, 0, 0), ("direct", 3, 0, 32)])
-def test_many_pipelined_small_units(engine, orc, mode, ovl, pre, ccus):
-    """ske_swipes_many_async through the partitioned K1 with pass C of every
-    unit on a side stream beside the next unit's pass B (option part_overlap
-    1) or its pass A (2; 3: on CU-masked streams, pass C on `part_ccus` CUs,
-    pass A on the rest, fail lists double-buffered), with or without the
-    pass-A register pre-check:
-    sub-batches of
-    64k swipes make ~25 units over 7 ragged batches (incl. 1 swipe and a
-    partial tile), so the two scratch sets alternate many times; answers and
-    registers == the oracle over the batches in order."""
+@pytest.mark.parametrize("mode", ["direct", "graph"])
+def test_many_small_units(engine, orc, mode):
+    """ske_swipes_many_async through the partitioned K1 with sub-batches of
+    64k swipes: ~25 units over 7 ragged batches (incl. 1 swipe and a partial
+    tile) reuse one scratch set in stream order, launched directly or
+    replayed from a graph; answers and registers == the oracle over the
+    batches in order."""
     import torch
     from rtsas_amd.engine import DeviceBuffer
     w, p = _c3_small(engine)
     engine.set_option("part_sub", 65536)
-    engine.set_option("part_overlap", ovl)
-    engine.set_option("pa_precheck", pre)
-    if ccus:
-        engine.set_option("part_ccus", ccus)
     sizes = [300_000, 1, 70_001, 300_000, 250_000, 2048, 400_000]
     bs, start = [], 0
     for n in sizes:
@@ -348,11 +329,11 @@ def test_many_pipelined_small_units(engine, orc, mode, ovl, pre, ccus):
         if mode == "direct":
             engine.swipes_many_async(0, bs, outs)
         else:
-            engine.swipes_many_async(0, bs[:2], outs[:2])  # side stream, scratch sets
+            engine.swipes_many_async(0, bs[:2], outs[:2])  # scratch sized before the capture
             torch.cuda.synchronize()
             g = engine.capture(lambda: engine.swipes_many_async(0, bs, outs))
             g.launch()
-        engine.sync()  # the context stream alone: the side stream was joined into it
+        engine.sync()
         if mode == "graph":
             g.free()
     finally:

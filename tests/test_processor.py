@@ -320,3 +320,26 @@ def test_c1_readme_default_exact(pkg, orc):
     assert p.get_attendance_stats("CS101-L1", "2025-03-19")["unique_attendees"] == hlls[key].count()
     assert p.get_attendance_stats("CS101-L1")["unique_attendees"] == hlls[key].count()
     client.flushall()
+
+
+@pytest.mark.gpu
+def test_sketch_client_day_key_index(pkg):
+    """get_attendance_stats(lecture) without a day reads the key table's day
+    index (KeySpace.day_keys), not a scan of every key: only README day keys
+    <prefix><lecture>:YYYY-MM-DD count, a lecture id that prefixes another
+    ('A' vs 'A:B') keeps its own keys, and DEL / FLUSHALL keep the index
+    (ADVICE r3)."""
+    c = pkg.SketchClient(decode_responses=True)
+    for k, v in [("hll:unique:A:2025-03-01", 1), ("hll:unique:A:2025-03-02", 2),
+                 ("hll:unique:A:B:2025-03-01", 3), ("hll:unique:A:notes", 4), ("hll:unique:AB:2025-03-01", 5)]:
+        c.pfadd(k, v)
+    assert c.day_keys("hll:unique:A") == ["hll:unique:A:2025-03-01", "hll:unique:A:2025-03-02"]
+    assert c.day_keys("hll:unique:A:B") == ["hll:unique:A:B:2025-03-01"]
+    p = pkg.AttendanceProcessor(client=c)
+    assert p.get_attendance_stats("A")["unique_attendees"] == c.pfcount("hll:unique:A:2025-03-01",
+                                                                        "hll:unique:A:2025-03-02") == 2
+    c.delete("hll:unique:A:2025-03-01")
+    assert c.day_keys("hll:unique:A") == ["hll:unique:A:2025-03-02"]
+    assert p.get_attendance_stats("A")["unique_attendees"] == 1
+    c.flushall()
+    assert c.day_keys("hll:unique:A") == [] and p.get_attendance_stats("A")["unique_attendees"] == 0

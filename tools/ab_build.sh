@@ -5,7 +5,8 @@
 set -e
 rev=$1; name=$2
 root=$(git rev-parse --show-toplevel)
-tmp=$(mktemp -d)
+tmp="$root/tools/ab/src_$name"
+rm -rf "$tmp"; mkdir -p "$tmp"
 git -C "$root" archive "$rev" real-time-student-attendance-system_amd/csrc include | tar -x -C "$tmp"
 make -s -C "$tmp/real-time-student-attendance-system_amd/csrc" -j8 libsketch.so
 mkdir -p "$root/tools/ab"

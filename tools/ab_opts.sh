@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of library options on one box with the partitioned K1's per-pass times:
 # ROUNDS alternations of bench.py over the ';'-separated option sets in OPTS
-# (each a list of bench.py arguments, e.g. "--opt pa_grid=3"; an empty set is
+# (each a list of bench.py arguments, e.g. "--opt k1_grid=128"; an empty set is
 # the default), extra bench args in ARGS, the library in SKE_LIB (default in-tree).
 mkdir -p gpurun_out
 IFS=';' read -ra SETS <<< "${OPTS:-}"
