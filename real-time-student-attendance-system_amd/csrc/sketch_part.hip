@@ -350,6 +350,9 @@ __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const Par
 // lanes past the batch count into the first pair past the chain (the sink),
 // whose records land past the copy-out.
 constexpr uint32_t kOORa = 0x80000000u;  // a buffer offset past every range: load 0, store dropped
+#ifndef SKE_PA_UNROLL
+#define SKE_PA_UNROLL 1
+#endif
 #ifndef SKE_ALIGN_BIG
 #define SKE_ALIGN_BIG 32
 #endif
@@ -379,7 +382,6 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
                   "whole pairs per thread; a rank * 4 below bit 16; starts fit 16 bits");
     __shared__ __attribute__((aligned(16))) uint32_t srec[kRecWords];
     __shared__ uint32_t cnt[2 * kCnt];
-    static_assert(kCo * kT * 16 <= sizeof(srec) + sizeof(cnt), "copy-out reads stay in the block's LDS");
     __shared__ uint32_t swsum[kT / 64];
     __shared__ uint32_t stot;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -423,7 +425,7 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
     const uint8_t *cntb = reinterpret_cast<const uint8_t *>(cnt);
     uint8_t *srecb = reinterpret_cast<uint8_t *>(srec);
     auto tile = [&](const uint32_t t, auto parc) {
-        constexpr uint32_t cb = decltype(parc)::value * kCnt;
+        const uint32_t cb = uint32_t(parc) * kCnt;
         uint32_t *cp = cnt + cb;
         uint32_t rv[kU][KM], rp[kU][KM];
         const uint32_t tn = t + tstep < gt1 ? t + tstep : t;
@@ -506,25 +508,35 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
                 *reinterpret_cast<uint32_t *>(srecb + (r + *reinterpret_cast<const uint32_t *>(cntb + (r >> 16)))) =
                     rv[u][q];
             }
-        constexpr uint32_t nb = (cb ^ kCnt);
+        const uint32_t nb = (cb ^ kCnt);
         for (uint32_t g = tid; g <= sink + 1; g += kT) cnt[nb + g] = (nb + g) << 18;
         lds_barrier();
         const uint32_t total = stot;
         // a fixed number of 16-B pieces per thread (those past the tile's
         // total go out of range; the gaps between runs are copied as they are)
         const __amdgpu_buffer_rsrc_t rdst = part_rsrc(A.rec + size_t(t) * A.stride, A.stride * 4);
+        // (a piece past the records reads the last piece instead: an LDS read
+        // past srec would be undefined behaviour, from which the compiler may
+        // infer a bound on tid for the rest of the kernel)
         const part_u32x4 *src = reinterpret_cast<const part_u32x4 *>(srec);
+        constexpr uint32_t kLast = kRecWords / 4 - 1;
 #pragma unroll
         for (uint32_t c = 0; c < kCo; c++) {
             const uint32_t j = c * kT + tid;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, src[j]),
+            const uint32_t jr = (c + 1) * kT <= kLast + 1 ? j : (j < kLast ? j : kLast);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, src[jr]),
                                                    rdst, j * 4 < total ? j * 16 : kOORa, 0, nt_aux<4>());
         }
     };
+#if SKE_PA_UNROLL
     for (uint32_t t = gt0 + blockIdx.x / kPGroups; t < gt1; t += 2 * tstep) {
         tile(t, std::integral_constant<uint32_t, 0>{});
         if (t + tstep < gt1) tile(t + tstep, std::integral_constant<uint32_t, 1>{});
     }
+#else
+    uint32_t par = 0;
+    for (uint32_t t = gt0 + blockIdx.x / kPGroups; t < gt1; t += tstep, par ^= 1) tile(t, par);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -906,7 +918,11 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
 // (Its loads and stores at a fixed count per tile, as pass A's, measured
 // equal, 0.408 vs 0.409 ms: pass C is bound by the memory side's random
 // requests, not by its waves' waits.)
-template <int U>
+// kPhase (SKE_PC_PHASES 2): 1 = the answers and the rank-1 updates only
+// (a register still 0 gets a plain byte store of 1: every writer of this
+// phase writes 1, so no update can be lost), 2 = the rank >= 2 updates by
+// CAS, after phase 1 has finished; 0 = both in one pass (CAS for all).
+template <int U, int kPhase = 0>
 __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
     static_assert(kPcBlock * U == 1024, "one 1024-swipe tile per sub-step");
     constexpr uint32_t kRun = kPbGroup;  // tiles per block iteration
@@ -975,18 +991,34 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
                 w[u] = nullptr;
                 rank[u] = sh[u] = 0;
                 if (valid[u]) {
+                    const uint32_t rk = cur.hv[u] >> 16;
                     if (cur.sl[u] >= A.nslots) {
-                        atomicOr(A.err, 1u);
-                    } else {
+                        if (kPhase != 2) atomicOr(A.err, 1u);
+                    } else if (kPhase == 0 || (kPhase == 1) == (rk == 1)) {
                         const uint32_t ridx = cur.hv[u] & 0xffffu;
                         w[u] = reinterpret_cast<uint32_t *>(A.regs + (uint64_t(cur.sl[u]) << kHllP) + (ridx & ~3u));
                         sh[u] = (ridx & 3) * 8;
-                        rank[u] = cur.hv[u] >> 16;
+                        rank[u] = rk;
                     }
                 }
             }
 #pragma unroll
             for (int u = 0; u < U; u++) cw[u] = w[u] ? nt_ld<32>(w[u]) : 0xffffffffu;
+            if constexpr (kPhase == 1) {
+#pragma unroll
+                for (int u = 0; u < U; u++)
+                    if (w[u] && ((cw[u] >> sh[u]) & 0xffu) == 0)
+                        reinterpret_cast<uint8_t *>(w[u])[sh[u] / 8] = 1;
+                if (A.out) {
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
+                        if (i < A.n) nt_st<16>(A.out + i, uint8_t(valid[u]));
+                    }
+                }
+                cur = nxt;
+                continue;
+            }
             // every raising CAS of the tile in flight at once, then settled
             // (a lost race retries from the word the CAS returned)
 #pragma unroll
@@ -995,7 +1027,7 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
                 if (w[u] && ((cw[u] >> sh[u]) & 0xffu) < rank[u])
                     seen[u] = atomicCAS(w[u], cw[u], (cw[u] & ~(0xffu << sh[u])) | (rank[u] << sh[u]));
             }
-            if (A.out) {
+            if (kPhase == 0 && A.out) {
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
@@ -1106,6 +1138,9 @@ hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratc
     return part_scratch(&A, n ? n : 1, part_sub(sub_opt), scr);
 }
 
+#ifndef SKE_PC_PHASES
+#define SKE_PC_PHASES 1
+#endif
 #ifndef SKE_PA_CNT_AL
 #define SKE_PA_CNT_AL 1024
 #endif
@@ -1177,7 +1212,12 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             if (flist) {
                 const unsigned gc =
                     (part_grid(ms, 1024 * kPbGroup, unsigned(cus) * 8) + kPGroups - 1) / kPGroups * kPGroups;
+#if SKE_PC_PHASES == 2
+                hipLaunchKernelGGL((k_part_c_fl<4, 1>), dim3(gc), dim3(kPcBlock), 0, st, A);
+                hipLaunchKernelGGL((k_part_c_fl<4, 2>), dim3(gc), dim3(kPcBlock), 0, st, A);
+#else
                 hipLaunchKernelGGL(k_part_c_fl<4>, dim3(gc), dim3(kPcBlock), 0, st, A);
+#endif
             } else {
                 const unsigned gc = (part_grid(ms, kPcBlock * 2, unsigned(cus) * 8) + kPGroups - 1) / kPGroups * kPGroups;
                 hipLaunchKernelGGL(k_part_c<2>, dim3(gc), dim3(kPcBlock), 0, st, A);

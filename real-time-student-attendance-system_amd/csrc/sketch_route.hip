@@ -175,16 +175,19 @@ __global__ void __launch_bounds__(kRtBlock) k_route_scatter_cap(const RouteArgs 
     }
 }
 
-// rows [tot[o], cap) of owner o: id bytes zero, slot sink[o] (a slot the
-// owner keeps for nothing else, so the padding's PFADDs change no key)
+// rows [tot[o], cap) of owner o (blockIdx.y): id bytes zero, slot sink[o]
+// (a slot the owner keeps for nothing else, so the padding's PFADDs change no
+// key); only the padding rows are visited
 __global__ void __launch_bounds__(256) k_route_pad(const RouteArgs R, uint32_t cap, const uint32_t *sink) {
-    const uint64_t rows = uint64_t(R.world) * cap;
-    for (uint64_t j = uint64_t(blockIdx.x) * 256 + threadIdx.x; j < rows; j += uint64_t(gridDim.x) * 256) {
-        const uint32_t o = uint32_t(j / cap), r = uint32_t(j % cap);
-        if (r < R.tot[o]) continue;
-        R.sslot[j] = sink[o];
+    const uint32_t o = blockIdx.y, t = R.tot[o], s = sink[o];
+    for (uint32_t r = t + blockIdx.x * 256 + threadIdx.x; r < cap; r += gridDim.x * 256) {
+        const uint64_t j = uint64_t(o) * cap + r;
+        R.sslot[j] = s;
         uint8_t *dst = R.sids + j * R.width;
-        for (uint32_t k = 0; k < R.width; k++) dst[k] = 0;
+        if (R.width == 8)
+            *reinterpret_cast<uint64_t *>(dst) = 0;
+        else
+            for (uint32_t k = 0; k < R.width; k++) dst[k] = 0;
     }
 }
 
@@ -205,9 +208,9 @@ hipError_t launch_route_cap(const uint8_t *ids, uint32_t width, const uint32_t *
         hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(1024), 0, st, R);
         hipLaunchKernelGGL(k_route_scatter_cap, dim3(R.nblocks), dim3(kRtBlock), 0, st, R, cap);
     }
-    const uint64_t g = (uint64_t(world) * cap + 255) / 256;
-    hipLaunchKernelGGL(k_route_pad, dim3(unsigned(g < uint64_t(cus) * 8 ? g : uint64_t(cus) * 8)), dim3(256), 0, st,
-                       R, cap, sink);
+    const uint64_t g = (uint64_t(cap) + 255) / 256;
+    const unsigned gx = unsigned(g < uint64_t(cus) * 4 / world + 1 ? g : uint64_t(cus) * 4 / world + 1);
+    hipLaunchKernelGGL(k_route_pad, dim3(gx, world), dim3(256), 0, st, R, cap, sink);
     return hipGetLastError();
 }
 

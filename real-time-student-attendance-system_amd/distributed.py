@@ -375,13 +375,22 @@ class SwipeExchange:
         else:
             send_ids, send_slots, pos, counts = self._route_cap_torch(ids, gkeys, cap)
         rows = self.world * cap
-        r_flat = torch.zeros(rows * w + 16, dtype=torch.uint8, device=dev)
-        self._a2a(r_flat[:rows * w], send_ids.reshape(-1), None, None)
-        r_slots = torch.empty(rows, dtype=torch.int32, device=dev)
-        self._a2a(r_slots, send_slots, None, None)
-        r_ans = self.k1(r_flat[:rows * w].view(rows, w), r_slots)
-        back = torch.empty(rows, dtype=torch.uint8, device=dev)
-        self._a2a(back, r_ans.to(torch.uint8), None, None)
+        if self.world == 1:
+            # one rank: the exchange is the identity, K1 reads the send rows
+            # in place (their storage has the 16 readable bytes K1 wants)
+            r_ids, r_slots = send_ids, send_slots
+        else:
+            r_flat = torch.zeros(rows * w + 16, dtype=torch.uint8, device=dev)
+            self._a2a(r_flat[:rows * w], send_ids.reshape(-1), None, None)
+            r_ids = r_flat[:rows * w].view(rows, w)
+            r_slots = torch.empty(rows, dtype=torch.int32, device=dev)
+            self._a2a(r_slots, send_slots, None, None)
+        r_ans = self.k1(r_ids, r_slots).to(torch.uint8)
+        if self.world == 1:
+            back = r_ans
+        else:
+            back = torch.empty(rows, dtype=torch.uint8, device=dev)
+            self._a2a(back, r_ans, None, None)
         ans = self._gather(back, pos, n)
         if counts.is_cuda:
             # pinned landing rows for the counts, reused once settled
@@ -447,7 +456,7 @@ class SwipeExchange:
         keep = r < cap
         row = ds * cap + torch.where(keep, r, r % cap)
         rows = self.world * cap
-        send_ids = torch.zeros((rows, w), dtype=torch.uint8, device=ids.device)
+        send_ids = torch.zeros(rows * w + 16, dtype=torch.uint8, device=ids.device)[:rows * w].view(rows, w)
         sink = torch.from_numpy(self.sink.astype(np.int64)).to(torch.int32).to(ids.device)
         send_slots = sink[torch.arange(rows, device=ids.device) // cap]
         send_ids[row[keep]] = ids[order][keep]
@@ -464,7 +473,7 @@ class SwipeExchange:
         g32 = gkeys.to(torch.int32).contiguous()
         own, loc = self.keymap.tables(dev)
         rows = self.world * cap
-        send_ids = torch.empty(rows * w, dtype=torch.uint8, device=dev)
+        send_ids = torch.empty(rows * w + 16, dtype=torch.uint8, device=dev)  # + K1's readable tail
         send_slots = torch.empty(rows, dtype=torch.int32, device=dev)
         pos = torch.empty(max(1, n), dtype=torch.int32, device=dev)
         counts = torch.empty(self.world, dtype=torch.int32, device=dev)
@@ -481,7 +490,7 @@ class SwipeExchange:
                          C.c_void_p(counts.data_ptr()))
         finally:
             eng.set_stream(prev)
-        return send_ids.view(rows, w), send_slots, pos, counts
+        return send_ids[:rows * w].view(rows, w), send_slots, pos, counts
 
     def _gather(self, back, pos, n):
         """answers of the send rows back into input order"""

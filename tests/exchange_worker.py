@@ -77,6 +77,20 @@ def main(out_dir, mode="exact"):
             return r
     ex = SwipeExchange(rank, world, k1, km, engine=eng, sink_slots=sinks,
                        slack=-0.6 if mode == "async_overflow" else world - 1.0)
+    if os.environ.get("EXCH_DEBUG"):
+        route_plain = ex._route_cap_native
+
+        def route_dbg(ids_, g_, cap):
+            r = route_plain(ids_, g_, cap)
+            torch.cuda.synchronize()
+            ssl = r[1].cpu().numpy().view(np.uint32)
+            ct = r[3].cpu().numpy()
+            for o in range(world):
+                ch = ssl[o * cap:(o + 1) * cap]
+                print(f"rank {rank} route n {ids_.shape[0]} cap {cap} owner {o} count {ct[o]} chunk max slot "
+                      f"{ch.max()} (owner {o} slots < {km.slots_end(o) + 1})", file=sys.stderr, flush=True)
+            return r
+        ex._route_cap_native = route_dbg
     if mode == "exact":
         ans = ex.swipes(ids, slots)
     else:

@@ -202,3 +202,39 @@ def test_key_map_is_one_rule(pkg):
     assert sum(km.count(r) for r in range(5)) == len(names)
     enc = [n.encode() for n in names]
     assert murmur64a_many(enc, 0x1234).tolist() == [murmur64a(b, 0x1234) for b in enc]
+
+
+def test_exchange_one_rank_no_group(orc):
+    """world 1 (no process group): both forms reduce to K1 on the caller's
+    slice -- the async form reads its send rows in place, no copy -- and
+    answer / count as the one-shard oracle."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as ge
+    ge.load_package()
+    from rtsas_amd.distributed import KeyMap, SwipeExchange
+    names = _names()
+    km = KeyMap(names, 1)
+    chain = _chain(orc)
+    buf, gkey = _stream(0)
+    for mode in ("exact", "async"):
+        regs = np.zeros((km.slots_end(0) + 1, 16384), np.uint8)
+
+        def k1(ids, local_slots):
+            m = ids.shape[0]
+            flat = np.concatenate([ids.numpy().reshape(-1), np.zeros(16, np.uint8)])
+            offs = np.arange(0, W * m + 1, W, dtype=np.uint32)
+            v, _, _ = orc.process_swipes(chain, regs, local_slots.numpy().astype(np.uint32), flat, offs)
+            return torch.from_numpy(v.astype(np.uint8))
+        ex = SwipeExchange(0, 1, k1, km, sink_slots=[km.slots_end(0)])
+        if mode == "exact":
+            ans = ex.swipes(torch.from_numpy(buf), torch.from_numpy(gkey))
+        else:
+            ans = ex.swipes_async(torch.from_numpy(buf), torch.from_numpy(gkey))
+            assert ex.settle() == 0
+        want_regs = np.zeros((len(names), 16384), np.uint8)
+        flat = np.concatenate([buf.reshape(-1), np.zeros(16, np.uint8)])
+        offs = np.arange(0, W * len(gkey) + 1, W, dtype=np.uint32)
+        want, _, _ = orc.process_swipes(chain, want_regs, gkey.astype(np.uint32), flat, offs)
+        assert np.array_equal(ans.numpy(), want.astype(np.uint8)), mode
+        assert np.array_equal(regs[km.local[np.arange(len(names))]], want_regs), mode

@@ -58,3 +58,48 @@ def test_exchange_on_device_equals_oracle(orc, engine, tmp_path, world, mode):
         assert d["roll"].tolist() == [orc.hll_count_regs(regs[[idx[n] for n in g]].max(axis=0)) if g else 0
                                       for g in groups(nm)]
     assert seen == NK
+
+
+
+@pytest.mark.parametrize("slack,world", [(0.2, 2), (-0.6, 2), (0.1, 3), (-0.5, 5)])
+def test_route_cap_layout(engine, slack, world):
+    """ske_route_swipes_cap_async alone (one process, no collective): owner
+    o's swipes fill rows [o*cap, o*cap + min(count_o, cap)) with their ids
+    and local slots, owner o's other rows are padding (zero ids, sink[o]),
+    pos[i] is a row of swipe i's owner holding swipe i (or, past cap, another
+    swipe of that owner), counts are the owners' counts -- also with
+    capacities below the owners' shares (slack < 0)."""
+    import torch
+    from rtsas_amd.distributed import KeyMap, SwipeExchange
+    names = [f"hll:unique:L{k:03d}:2025-01-01" for k in range(37)]
+    km = KeyMap(names, world)
+    sinks = [km.slots_end(r) for r in range(world)]
+    ex = SwipeExchange(0, world, None, km, engine=engine, sink_slots=sinks, slack=slack)
+    rng = np.random.default_rng(3)
+    cap = ex.capacity(200_000)
+    for n in (200_000, 199_000, 1):
+        idn = rng.integers(48, 58, (n, 8), dtype=np.uint8)
+        gk = rng.integers(0, 37, n)
+        send_ids, send_slots, pos, counts = ex._route_cap_native(torch.from_numpy(idn).cuda(),
+                                                                 torch.from_numpy(gk).cuda(), cap)
+        torch.cuda.synchronize()
+        sid, ssl = send_ids.cpu().numpy(), send_slots.cpu().numpy().view(np.uint32)
+        ps, ct = pos.cpu().numpy()[:n].astype(np.int64), counts.cpu().numpy()
+        own = km.owner[gk].astype(np.int64)
+        assert ct.tolist() == np.bincount(own, minlength=world).tolist()
+        assert ((ps // cap) == own).all()
+        for o in range(world):
+            k = min(int(ct[o]), cap)
+            rows = o * cap + np.arange(cap)
+            hit = np.zeros(cap, bool)
+            hit[ps[own == o] - o * cap] = True
+            assert hit[:k].all() and not hit[k:].any()
+            assert (ssl[rows[k:]] == sinks[o]).all() and not sid[rows[k:]].any()
+        # every real row holds (the id, the local slot) of one of the swipes that name it
+        def key(row, slot, id64):
+            return (row.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)) ^ (slot.astype(np.uint64) << np.uint64(40)) \
+                ^ id64
+        want = key(ps, km.local[gk], idn.view(np.uint64).ravel())
+        rr = np.unique(ps)
+        have = key(rr, ssl[rr], sid.view(np.uint64).ravel()[rr])
+        assert np.isin(have, want).all()

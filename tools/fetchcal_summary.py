@@ -21,6 +21,14 @@ import sys
 KINDS = {"k_stream16": ["stream16"], "k_strided4": ["line4", "sector4"], "k_runs": ["runs", "runs_al"]}
 
 
+def read_bytes(m: dict) -> float:
+    """Memory-side read bytes from the TCC/EA request counters by size: 128-B
+    requests at 128, 64-B at 64, 32-B at 32 (TCC_EA0_RDREQ counts them all)."""
+    r128, r64 = m["TCC_EA0_RDREQ_128B_sum"], m["TCC_EA0_RDREQ_64B_sum"]
+    r32 = m.get("TCC_EA0_RDREQ_32B_sum", 0.0)
+    return 128 * r128 + 64 * r64 + 32 * r32
+
+
 def main(root: str) -> dict:
     times = json.load(open(os.path.join(root, "times.json")))
     per = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -51,9 +59,14 @@ def main(root: str) -> dict:
         if "FETCH_SIZE" in m:
             fpl = m["FETCH_SIZE"] * 1024 / lines
             e.update({"fetch_per_line_B": fpl, "factor": 128.0 / fpl if fpl else None})
-        for c in ("TCC_MISS_sum", "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_REQ_sum"):
+        for c in ("TCC_MISS_sum", "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum",
+                  "TCC_EA0_RDREQ_128B_sum", "TCC_REQ_sum"):
             if c in m:
                 e[c.replace("_sum", "") + "_per_line"] = m[c] / lines
+        if "TCC_EA0_RDREQ_128B_sum" in m and "TCC_EA0_RDREQ_64B_sum" in m:
+            # bytes by request size
+            e["read_bytes_by_size"] = read_bytes(m)
+            e["read_bytes_per_line"] = e["read_bytes_by_size"] / lines
         e["line_GBps"] = lines * 128 / (t["ms"] * 1e-3) / 1e9
         if "record_bytes" in t:
             e["record_bytes"] = t["record_bytes"]

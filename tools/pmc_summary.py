@@ -59,6 +59,15 @@ def summarise(root: str, kernel: str, skip: int = 3, wide: float = 0.0) -> dict:
         out["lds_bank_conflict_rate"] = m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"]
     if "TCC_HIT_sum" in m and "TCC_MISS_sum" in m:
         out["l2_hit_rate"] = m["TCC_HIT_sum"] / max(1.0, m["TCC_HIT_sum"] + m["TCC_MISS_sum"])
+    if "TCC_EA0_RDREQ_128B_sum" in m and "TCC_EA0_RDREQ_64B_sum" in m:
+        # calibrated read bytes (tools/fetchcal.hip, profiles/r04_fetchcal.json): the
+        # memory-side read requests by size, 128 / 64 / 32 B -- FETCH_SIZE counts every
+        # request at 64 B, half of a 128-B line whatever the loads' width
+        rd = (128 * m["TCC_EA0_RDREQ_128B_sum"] + 64 * m["TCC_EA0_RDREQ_64B_sum"]
+              + 32 * m.get("TCC_EA0_RDREQ_32B_sum", 0.0))
+        out["read_bytes_by_request_size"] = rd
+        if "WRITE_SIZE" in m:
+            out["hbm_bytes_calibrated"] = rd + m["WRITE_SIZE"] * 1024
     return out
 
 
