@@ -322,9 +322,39 @@ class SwipeExchange:
         out.copy_(o)
         return out
 
+    def _on_stream(self, t):
+        """libsketch follows torch's current stream, but a NULL handle (torch's
+        default stream) means the library's own non-blocking stream, which
+        does not order with torch's copies: on the default stream the
+        exchange runs on a stream of its own, behind the caller's work, and
+        the caller's stream waits for it at the end."""
+        import contextlib
+        torch = self.torch
+        if not t.is_cuda or torch.cuda.current_stream(t.device).cuda_stream != 0:
+            return contextlib.nullcontext(None)
+
+        @contextlib.contextmanager
+        def cm():
+            caller = torch.cuda.current_stream(t.device)
+            if not hasattr(self, "_own_stream"):
+                self._own_stream = torch.cuda.Stream(t.device)
+            s = self._own_stream
+            s.wait_stream(caller)
+            with torch.cuda.stream(s):
+                yield caller
+            caller.wait_stream(s)
+        return cm()
+
     def swipes(self, ids, gkeys):
         """ids: uint8 [n, w] tensor, gkeys: integer [n] tensor of global key
         indices (same device).  Returns uint8 [n] answers in the input order."""
+        with self._on_stream(ids) as caller:
+            ans = self._swipes(ids, gkeys)
+            if caller is not None:
+                ans.record_stream(caller)
+        return ans
+
+    def _swipes(self, ids, gkeys):
         if self.engine is not None and ids.is_cuda:
             return self._swipes_native(ids, gkeys)
         torch = self.torch
@@ -363,6 +393,13 @@ class SwipeExchange:
         a batch in which some owner got more than cap swipes on any rank is
         then run again through ``swipes`` (exact splits; PFADD is idempotent
         and its answers are rewritten)."""
+        with self._on_stream(ids) as caller:
+            ans = self._swipes_async(ids, gkeys, n_max)
+            if caller is not None:
+                ans.record_stream(caller)
+        return ans
+
+    def _swipes_async(self, ids, gkeys, n_max):
         torch = self.torch
         if self.sink is None:
             raise ValueError("swipes_async needs sink_slots (one spare local slot per rank)")

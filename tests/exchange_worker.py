@@ -62,35 +62,8 @@ def main(out_dir, mode="exact"):
     ids = torch.from_numpy(buf[:n * width].reshape(n, width).copy()).cuda()
     slots = torch.from_numpy(slot.astype(np.int64)).cuda()
     k1 = engine_k1(eng)
-    if os.environ.get("EXCH_DEBUG"):
-        # every K1 call: its slots must all be local slots of this rank
-        k1_plain = k1
-
-        def k1(ids_, slots_):  # noqa: F811
-            torch.cuda.synchronize()
-            sl = slots_.cpu().numpy().view(np.uint32)
-            print(f"rank {rank} k1 rows {sl.size} max slot {sl.max() if sl.size else -1} nslots {nlocal + 1}",
-                  file=sys.stderr, flush=True)
-            r = k1_plain(ids_, slots_)
-            torch.cuda.synchronize()
-            eng.sync()
-            return r
     ex = SwipeExchange(rank, world, k1, km, engine=eng, sink_slots=sinks,
                        slack=-0.6 if mode == "async_overflow" else world - 1.0)
-    if os.environ.get("EXCH_DEBUG"):
-        route_plain = ex._route_cap_native
-
-        def route_dbg(ids_, g_, cap):
-            r = route_plain(ids_, g_, cap)
-            torch.cuda.synchronize()
-            ssl = r[1].cpu().numpy().view(np.uint32)
-            ct = r[3].cpu().numpy()
-            for o in range(world):
-                ch = ssl[o * cap:(o + 1) * cap]
-                print(f"rank {rank} route n {ids_.shape[0]} cap {cap} owner {o} count {ct[o]} chunk max slot "
-                      f"{ch.max()} (owner {o} slots < {km.slots_end(o) + 1})", file=sys.stderr, flush=True)
-            return r
-        ex._route_cap_native = route_dbg
     if mode == "exact":
         ans = ex.swipes(ids, slots)
     else:
