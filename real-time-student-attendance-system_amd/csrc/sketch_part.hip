@@ -115,6 +115,19 @@ __device__ __forceinline__ void part_group(uint32_t ntiles, uint32_t x, uint32_t
     t1 = uint32_t(uint64_t(ntiles) * (x + 1) / kPGroups);
 }
 
+// Inclusive prefix sum over a wave's 64 lanes on DPP: row shifts 1, 2, 4, 8
+// inside 16-lane rows, then row_bcast:15 / row_bcast:31 across rows (gfx9);
+// a lane whose source is outside its row adds the identity.  VALU only.
+__device__ __forceinline__ uint32_t part_wave_scan(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 into rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 into rows 2, 3
+    return v;
+}
+
 // ---------------------------------------------------------------------------
 // ids of at most 8 bytes (every config's student ids), read and hashed the way
 // the LDS K1 does (sketch_k1.hip): the one or two aligned 64-bit words holding
@@ -351,13 +364,16 @@ __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const Par
 // whose records land past the copy-out.
 constexpr uint32_t kOORa = 0x80000000u;  // a buffer offset past every range: load 0, store dropped
 #ifndef SKE_PA_UNROLL
-#define SKE_PA_UNROLL 1
+#define SKE_PA_UNROLL 0
 #endif
 #ifndef SKE_ALIGN_BIG
 #define SKE_ALIGN_BIG 32
 #endif
 #ifndef SKE_A4_MAX_UNITS
 #define SKE_A4_MAX_UNITS (kCnt / 2 - 1)
+#endif
+#ifndef SKE_ALIGN_SMALL
+#define SKE_ALIGN_SMALL 1
 #endif
 // The line-aligned instantiation (kAlign 32, runs on 128-B lines) gives
 // wrong answers on MI355X once a pass-A block takes two or more tiles
@@ -368,24 +384,36 @@ constexpr uint32_t kOORa = 0x80000000u;  // a buffer offset past every range: lo
 #define SKE_ALIGN_MAX_UNITS 0
 #endif
 constexpr uint32_t kAlignMaxUnits = SKE_ALIGN_MAX_UNITS;  // pairs of the line-aligned instantiation (C3/C5: 152)
+#ifndef SKE_PA_WPE
+#define SKE_PA_WPE 4  // waves per SIMD: two 512-thread blocks per CU
+#endif
 template <int KM, uint32_t kCnt, uint32_t kAlign>
-__global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two blocks per CU
+__global__ void __launch_bounds__(512, SKE_PA_WPE) k_part_a3(const PartArgs A) {
     constexpr uint32_t kT = 512;
     constexpr uint32_t kU = 1024 / kT, kTile = 1024;
     constexpr uint32_t kPer = kCnt / kT;  // counters per thread: kPer / 2 whole pairs
     constexpr uint32_t kMaxUnits = kAlign >= SKE_ALIGN_BIG ? kAlignMaxUnits : SKE_A4_MAX_UNITS;
     // records, plus the largest padding, rounded so the fixed-count copy-out's
     // LDS reads stay inside the block (the counters follow the records)
-    constexpr uint32_t kRecWords = kTile * KM + kAlign * (kMaxUnits + 1);
+    constexpr uint32_t kRecWords = kTile * KM + (kAlign > 1 ? kAlign * (kMaxUnits + 1) : 0);
     constexpr uint32_t kCo = (kRecWords / 4 + kT - 1) / kT;
     static_assert(kCnt % (2 * kT) == 0 && kRecWords < 65536u && 4u * kTile * KM < 65536u,
                   "whole pairs per thread; a rank * 4 below bit 16; starts fit 16 bits");
-    __shared__ __attribute__((aligned(16))) uint32_t srec[kRecWords];
-    __shared__ uint32_t cnt[2 * kCnt];
-    __shared__ uint32_t swsum[kT / 64];
-    __shared__ uint32_t stot;
+    // one LDS object, counters first: it sits at LDS address 0, so a probe's
+    // counter address is its slice field shifted and added to the parity's
+    // base (v_bfe + v_lshl_add: two VALU per probe)
+    struct __attribute__((aligned(16))) Lds {
+        uint32_t cnt[2 * kCnt];
+        uint32_t srec[kRecWords];
+        uint32_t swsum[kT / 64];
+        uint32_t stot;
+    };
+    __shared__ Lds lds;
+    uint32_t *const cnt = lds.cnt, *const srec = lds.srec, *const swsum = lds.swsum;
+    uint32_t &stot = lds.stot;
+    static_assert((kCnt & (kCnt - 1)) == 0, "parity base above the counter index bits");
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t S = A.nslices, nunits = A.nunits;
+    const uint32_t nunits = A.nunits;
     const uint32_t sink = 2 * nunits;  // the sink pair's first slice
     for (uint32_t c = tid; c < 2 * kCnt; c += kT) cnt[c] = c << 18;
     lds_barrier();
@@ -424,9 +452,18 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
     }
     const uint8_t *cntb = reinterpret_cast<const uint8_t *>(cnt);
     uint8_t *srecb = reinterpret_cast<uint8_t *>(srec);
+    uint8_t *const cntw = reinterpret_cast<uint8_t *>(cnt);
+    // a probe's slice (kCnt - 1 masks it: slices < kCnt), as one v_bfe the
+    // compiler cannot fold into a shift and mask of the address
+    auto part_slice = [](uint32_t x) {
+        constexpr uint32_t kW = __builtin_ctz(kCnt);
+        uint32_t r;
+        asm("v_bfe_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "i"(kPSliceLog), "i"(kW));
+        return r;
+    };
     auto tile = [&](const uint32_t t, auto parc) {
         const uint32_t cb = uint32_t(parc) * kCnt;
-        uint32_t *cp = cnt + cb;
+        const uint32_t pb = cb * 4;  // the parity's byte base, above (kCnt - 1) * 4
         uint32_t rv[kU][KM], rp[kU][KM];
         const uint32_t tn = t + tstep < gt1 ? t + tstep : t;
 #pragma unroll
@@ -453,7 +490,7 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
                 for (int q = 0; q < KM; q++) {
                     const uint32_t x = wk.x;
                     rv[u][q] = (x & 0xfffffu) | lu20;
-                    rp[u][q] = atomicAdd(&cp[__builtin_amdgcn_ubfe(x, kPSliceLog, 12)], 4u);
+                    rp[u][q] = atomicAdd(reinterpret_cast<uint32_t *>(cntw + part_slice(x) * 4 + pb), 4u);
                     if (q + 1 < KM) wk.step(L.d);
                 }
             } else {
@@ -461,7 +498,7 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
                 for (int q = 0; q < KM; q++) {
                     const uint32_t x = wk.x;
                     rv[u][q] = (x & 0xfffffu) | lu20;
-                    rp[u][q] = atomicAdd(&cp[act ? __builtin_amdgcn_ubfe(x, kPSliceLog, 12) : sink], 4u);
+                    rp[u][q] = atomicAdd(reinterpret_cast<uint32_t *>(cntw + (act ? part_slice(x) : sink) * 4 + pb), 4u);
                     if (q + 1 < KM) wk.step(L.d);
                 }
             }
@@ -479,12 +516,7 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
         }
 #pragma unroll
         for (uint32_t j = 0; j < kPer; j += 2) s += (v[j] + v[j + 1] + kAlign - 1) & ~(kAlign - 1);
-        uint32_t incl = s;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o, 64);
-            if (lane >= uint32_t(o)) incl += y;
-        }
+        const uint32_t incl = part_wave_scan(s);
         if (lane == 63) swsum[wave] = incl;
         lds_barrier();
         uint32_t run = incl - s;
@@ -608,7 +640,7 @@ hipError_t set_pb_stamp_buffer(void *p) {
 // ds_bpermute rounds and a broadcast (0.1966 -> 0.1946 ms, round 3); the
 // slice-pair image is copied as one batch of buffer loads (0.195 -> 0.190 ms).
 #ifndef SKE_PB_SPLIT
-#define SKE_PB_SPLIT 0
+#define SKE_PB_SPLIT 1
 #endif
 template <int SP, int R = 2 * SP, bool FL = false>  // R: 16-byte pieces per lane and run (runs of SP slices)
 __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const PartArgs A) {
@@ -1068,7 +1100,7 @@ static uint32_t part_stride(uint32_t ksum) { return ((ksum << kPTileLog) + 31) &
 // pairs, pair runs aligned to part_align() records (the sink pair must fit
 // k_part_a3<11, 2048>'s counters)
 static bool part_flist(const PartArgs &A) { return A.nlinks == 1 && A.ksum == 11 && A.nslices <= 2046; }
-static uint32_t part_align(const PartArgs &A) { return A.nunits <= kAlignMaxUnits ? SKE_ALIGN_BIG : 4u; }
+static uint32_t part_align(const PartArgs &A) { return A.nunits <= kAlignMaxUnits ? SKE_ALIGN_BIG : SKE_ALIGN_SMALL; }
 
 static bool part_plan(const ChainDev &ch, PartArgs *A) {
     if (ch.nlinks < 1 || ch.nlinks > kPMaxLinks) return false;
@@ -1169,7 +1201,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
     const bool aligned = part_align(A) == SKE_ALIGN_BIG;
     const bool pairs = A.nlinks == 1;  // a one-link chain is probed in slice pairs (128 KiB images)
     const unsigned ga = unsigned(cus) * (km <= 11 ? 2u : 1u) / kPGroups * kPGroups;  // blocks past a group's tiles exit
-    const unsigned g2 = unsigned(cus) * 2 / kPGroups * kPGroups;
+    const unsigned g2 = unsigned(cus) * (SKE_PA_WPE / 2) / kPGroups * kPGroups;  // pass A: resident blocks
     const unsigned gb = unsigned(cus) * (pairs ? 1 : 2) / kPGroups * kPGroups;  // all resident
     for (uint32_t j = 0; j < nb; j++) {
         const PartBatch &B = bt[j];
@@ -1191,8 +1223,10 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             if (hook) hook(hook_user, 0, 0, st);
             if (flist && aligned)  // runs on 128-B lines (C3/C5: 152 pairs)
                 hipLaunchKernelGGL((k_part_a3<11, SKE_PA_CNT_AL, SKE_ALIGN_BIG>), dim3(g2), dim3(512), 0, st, A);
+            else if (flist && A.nunits < 512)  // C3/C5: 152 pairs, two counters per thread
+                hipLaunchKernelGGL((k_part_a3<11, 1024, SKE_ALIGN_SMALL>), dim3(g2), dim3(512), 0, st, A);
             else if (flist)
-                hipLaunchKernelGGL((k_part_a3<11, 2048, 4>), dim3(g2), dim3(512), 0, st, A);
+                hipLaunchKernelGGL((k_part_a3<11, 2048, SKE_ALIGN_SMALL>), dim3(g2), dim3(512), 0, st, A);
             else if (km <= 11)
                 hipLaunchKernelGGL(k_part_a<11>, dim3(ga), dim3(kPaBlock), 0, st, A);
             else

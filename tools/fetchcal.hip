@@ -22,6 +22,9 @@
 //   runs_al    the same runs with each start rounded up to a 128-B line
 //              (pass A writing sentinel-padded runs)
 //
+//   wstream16 / wbytes / wline4   stores: 16 B per lane over every line, 1 B
+//              per lane contiguous, one 4-B word per line (WRITE_SIZE)
+//
 // tools/fetchcal_summary.py divides the PMC per kernel by these counts.
 #include <hip/hip_runtime.h>
 
@@ -93,6 +96,26 @@ __global__ void __launch_bounds__(1024) k_runs(const uint32_t *p, uint32_t nbyte
         }
     }
     if (acc == 0x1234567u) sink[0] = acc;
+}
+
+// writes (WRITE_SIZE calibration): 16 B per lane over every line (pass A's
+// record copy-out), 1 B per lane contiguous (pass C's answers), one 4-B word
+// per 128-B line (a scattered partial-line store)
+__global__ void __launch_bounds__(1024) k_wstream16(uint32_t *p, uint32_t n16) {
+    const __amdgpu_buffer_rsrc_t r = rs(p, n16 * 16);
+    for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < n16; i += gridDim.x * 1024)
+        __builtin_amdgcn_raw_buffer_store_b128(__attribute__((ext_vector_type(4))) unsigned int{i, i, i, i}, r, i * 16, 0, 2);
+}
+__global__ void __launch_bounds__(1024) k_wbytes(uint32_t *p, uint32_t n) {
+    const __amdgpu_buffer_rsrc_t r = rs(p, n);
+    for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < n; i += gridDim.x * 1024)
+        __builtin_amdgcn_raw_buffer_store_b8(uint8_t(i), r, i, 0, 0);
+}
+__global__ void __launch_bounds__(1024) k_wstrided4(uint32_t *p, uint32_t nwords, uint32_t step_words) {
+    const __amdgpu_buffer_rsrc_t r = rs(p, nwords * 4);
+    const uint32_t n = nwords / step_words;
+    for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < n; i += gridDim.x * 1024)
+        __builtin_amdgcn_raw_buffer_store_b32(i, r, i * step_words * 4, 0, 0);
 }
 
 template <typename F>
@@ -177,6 +200,14 @@ int main() {
                lines, recs * 4);
         if (q != p) CK(hipFree(q));
     }
+    const size_t wb = bytes / 4;  // 176 MB of bytes: the answers' shape
+    printf(", \"wstream16\": {\"ms\": %.4f, \"lines\": %.0f, \"bytes\": %zu}", median_ms([&] {
+        hipLaunchKernelGGL(k_wstream16, dim3(grid), dim3(1024), 0, 0, p, uint32_t(bytes / 16)); }), lines_all, bytes);
+    printf(", \"wbytes\": {\"ms\": %.4f, \"lines\": %.0f, \"bytes\": %zu}", median_ms([&] {
+        hipLaunchKernelGGL(k_wbytes, dim3(grid), dim3(1024), 0, 0, p, uint32_t(wb)); }), double(wb) / 128, wb);
+    printf(", \"wline4\": {\"ms\": %.4f, \"lines\": %.0f, \"bytes\": %.0f}", median_ms([&] {
+        hipLaunchKernelGGL(k_wstrided4, dim3(grid), dim3(1024), 0, 0, p, uint32_t(bytes / 4), 32u); }), lines_all,
+        lines_all * 4);
     printf("}\n");
     CK(hipFree(p));
     CK(hipFree(st));

@@ -18,7 +18,8 @@ import json
 import os
 import sys
 
-KINDS = {"k_stream16": ["stream16"], "k_strided4": ["line4", "sector4"], "k_runs": ["runs", "runs_al"]}
+KINDS = {"k_stream16": ["stream16"], "k_strided4": ["line4", "sector4"], "k_runs": ["runs", "runs_al"],
+         "k_wstream16": ["wstream16"], "k_wbytes": ["wbytes"], "k_wstrided4": ["wline4"]}
 
 
 def read_bytes(m: dict) -> float:
@@ -67,6 +68,13 @@ def main(root: str) -> dict:
             # bytes by request size
             e["read_bytes_by_size"] = read_bytes(m)
             e["read_bytes_per_line"] = e["read_bytes_by_size"] / lines
+        if "WRITE_SIZE" in m and "bytes" in t:
+            # WRITE_SIZE (KB) against the bytes the kernel stores
+            e["write_size_B"] = m["WRITE_SIZE"] * 1024
+            e["write_size_per_stored_byte"] = m["WRITE_SIZE"] * 1024 / t["bytes"]
+        for c in ("TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum", "TCC_WRITE_SECTORS_sum"):
+            if c in m:
+                e[c.replace("_sum", "") + "_per_line"] = m[c] / lines
         e["line_GBps"] = lines * 128 / (t["ms"] * 1e-3) / 1e9
         if "record_bytes" in t:
             e["record_bytes"] = t["record_bytes"]

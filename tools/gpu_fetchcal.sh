@@ -9,7 +9,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -s KILL 60 rocprofv3 -L > $OUT/avail.txt 2>&1 || true
 timeout -k 10 120 ./tools/fetchcal > $OUT/times.json || exit $?
-GROUPS_=("FETCH_SIZE" "TCC_MISS_sum TCC_HIT_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_REQ_sum")
+GROUPS_=("FETCH_SIZE" "TCC_MISS_sum TCC_HIT_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_REQ_sum" "WRITE_SIZE" "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_WRITE_SECTORS_sum")
 for c in "${GROUPS_[@]}"; do
   ok=1
   for x in $c; do grep -q "${x%_sum}" $OUT/avail.txt || { echo "skip [$c]: $x not offered"; ok=0; }; done
