@@ -64,7 +64,7 @@ RANDOM_CAS_GPS = 21.1
 MALL_BYTES = 256 << 20  # Infinity Cache: a slab this small stays on chip
 METRIC = "swipes/sec (fused BF.EXISTS+PFADD) at 1/2/4/8 GPUs; % of HBM peak"
 PASS_NAMES = ["k1", "k_part_a", "k_part_b", "k_part_c"]
-PMC_ROUNDS = ["r03", "r02"]  # newest committed PMC summaries first
+PMC_ROUNDS = ["r04", "r03", "r02"]  # newest committed PMC summaries first
 VERIFY_KEYS = 64
 
 
@@ -630,15 +630,32 @@ class Run:
         pmc, pmc_src = load_pmc(self.cfg, dom)
         traffic = None
         if pmc is not None:
-            traffic = pmc.get("hbm_bytes_corrected", pmc.get("hbm_bytes_per_dispatch"))
+            # request-size-calibrated bytes where the summary has them (round 4:
+            # every read request by its size, tools/fetchcal.hip), else FETCH+WRITE
+            traffic = pmc.get("hbm_bytes_calibrated",
+                              pmc.get("hbm_bytes_corrected", pmc.get("hbm_bytes_per_dispatch")))
             if traffic is not None and self.persistent and dom == "k1":
-                traffic *= a.steps / passes["k1"]["launches"] / pmc.get("steps_per_dispatch", a.steps)
+                # per launch of this run (one persistent launch per 48 steps
+                # when the timed steps were not replayed per pass)
+                launches = passes["k1"]["launches"] if "k1" in passes else -(-a.steps // 48)
+                traffic *= a.steps / launches / pmc.get("steps_per_dispatch", a.steps)
         r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": pmc_src,
              "kernel": dom, "kernel_ms": kern_ms, "alg_bytes_per_launch": dom_bytes,
              "kernel_times": "instrumented replay of the timed steps" if passes else "timed region events",
              "device_ms_per_step": step_ms, "probes_per_swipe": self.probes / n,
              "valid_frac": self.nvalid / n, "passes": passes}
+        if dom.startswith("k_part"):
+            # SURVEY §8(d)'s whole-path model prices every probe as a random
+            # 64-B HBM sector; the partitioned K1 answers probes from LDS slices
+            whole = alg["k1"]
+            r["whole_path_model"] = {
+                "what": "SURVEY §8(d) bytes for the whole path (every probe a random 64-B sector): not an HBM "
+                        "roofline for the partitioned K1, whose probes are served from LDS-resident filter "
+                        "slices after a radix partition; its rooflines are the per-pass algorithmic bytes "
+                        "(passes[*].alg_bytes), the dominant pass's taken above",
+                "bytes_per_step": whole, "would_need_GBps": whole / (step_ms * 1e-3) / 1e9,
+                "of_peak": whole / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
         if dom == "k_part_c":
             sectors = self.nvalid / (kern_ms * 1e-3) / 1e9
             r["random_sector_bound"] = {

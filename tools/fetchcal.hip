@@ -46,6 +46,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rs(const void *p, uint32_t nby
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, int(nbytes), 0x00020000);
 }
 constexpr uint32_t kOOR = 0x80000000u;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 __global__ void __launch_bounds__(1024) k_stream16(const uint32_t *p, uint32_t n16, uint32_t *sink) {
     const __amdgpu_buffer_rsrc_t r = rs(p, n16 * 16);
@@ -104,7 +105,7 @@ __global__ void __launch_bounds__(1024) k_runs(const uint32_t *p, uint32_t nbyte
 __global__ void __launch_bounds__(1024) k_wstream16(uint32_t *p, uint32_t n16) {
     const __amdgpu_buffer_rsrc_t r = rs(p, n16 * 16);
     for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < n16; i += gridDim.x * 1024)
-        __builtin_amdgcn_raw_buffer_store_b128(__attribute__((ext_vector_type(4))) unsigned int{i, i, i, i}, r, i * 16, 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{i, i, i, i}, r, i * 16, 0, 2);
 }
 __global__ void __launch_bounds__(1024) k_wbytes(uint32_t *p, uint32_t n) {
     const __amdgpu_buffer_rsrc_t r = rs(p, n);
