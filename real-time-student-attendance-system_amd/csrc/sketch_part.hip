@@ -639,8 +639,16 @@ hipError_t set_pb_stamp_buffer(void *p) {
 // The fail-list pass B's 8-lane prefix runs on DPP row shifts instead of three
 // ds_bpermute rounds and a broadcast (0.1966 -> 0.1946 ms, round 3); the
 // slice-pair image is copied as one batch of buffer loads (0.195 -> 0.190 ms).
+// SKE_PB_SPLIT: how pass B's blocks share the (slice unit, tile) space.
+// 0: per XCD tile group, unit major (round 3); 1: all tiles, unit major (a
+// block restages its image once or twice: pass B 0.189 -> 0.183 ms);
+// 2 (default): XCD x takes tile group x and its 32 blocks take units round
+// robin, so adjacent units' runs, which share their boundary lines, are read
+// by neighbouring CUs of one XCD at about the same time (round 4, A/B of
+// three alternations on one box: 0.211 -> 0.200 ms; 128-B read requests
+// 8.34 -> 8.06 M, L2 hits 0.65 -> 1.84 M per dispatch)
 #ifndef SKE_PB_SPLIT
-#define SKE_PB_SPLIT 1
+#define SKE_PB_SPLIT 2
 #endif
 template <int SP, int R = 2 * SP, bool FL = false>  // R: 16-byte pieces per lane and run (runs of SP slices)
 __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const PartArgs A) {
@@ -651,8 +659,13 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
     // this block's share of the (slice unit, tile) space, unit major: of its
     // XCD group's tiles (SKE_PB_SPLIT 0), or of all tiles (1: every block
     // restages its images once or twice instead of ~6 times)
+    // SKE_PB_SPLIT 2: XCD x (blocks b % 8 == x) takes tile group x, and its
+    // blocks take whole units round robin (block j: units j, j + 32, ...),
+    // so the 32 CUs of an XCD sweep the same tiles of 32 ADJACENT units at
+    // about the same pace: a line two neighbouring runs share is read while
+    // the other block's read of it is still in the XCD's L2
     uint32_t gt0 = 0, gt1 = A.ntiles, nblk = gridDim.x, bi = blockIdx.x;
-    if (SKE_PB_SPLIT == 0) {
+    if (SKE_PB_SPLIT != 1) {
         part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
         nblk = gridDim.x / kPGroups;
         bi = blockIdx.x / kPGroups;
@@ -661,7 +674,12 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
     const uint32_t nunits = (A.nslices + SP - 1) / SP;
     const uint32_t total = nunits * gn;
     uint32_t w = uint32_t(uint64_t(total) * bi / nblk);
-    const uint32_t wend = uint32_t(uint64_t(total) * (bi + 1) / nblk);
+    uint32_t wend = uint32_t(uint64_t(total) * (bi + 1) / nblk);
+    uint32_t su = bi;  // SKE_PB_SPLIT 2: this block's current unit
+    if (SKE_PB_SPLIT == 2) {
+        w = su < nunits ? su * gn : total;
+        wend = su < nunits ? w + gn : total;
+    }
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t k = lane / kPbLanes, qq = lane % kPbLanes;
     constexpr uint32_t kWaves = kPbBlock / 64, kStep = kWaves * kPbGroup;
@@ -669,7 +687,14 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
     const __amdgpu_buffer_rsrc_t roff = part_rsrc(A.off, (A.nslices + 1) * A.off_stride * 4);
     const __amdgpu_buffer_rsrc_t rfl = part_rsrc(A.flist, FL ? A.nunits * A.fl_stride * kPbLanes * 2 : 0);
     uint32_t *q = fq[wave];
-    while (w < wend) {
+    while (true) {
+        if (w >= wend) {
+            if (SKE_PB_SPLIT != 2) break;
+            su += nblk;  // block-uniform
+            if (su >= nunits) break;
+            w = su * gn;
+            wend = w + gn;
+        }
         // slices g .. g + SP - 1 (SP = 2: one link only, host-checked), so
         // one run per tile covers them all
         const uint32_t unit = w / gn, g = unit * SP, ta = gt0 + w % gn;

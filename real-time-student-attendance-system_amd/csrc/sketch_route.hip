@@ -59,16 +59,60 @@ __device__ __forceinline__ uint32_t route_owner(const RouteArgs &R, uint32_t g) 
     return route_known(R, g) ? R.kown[g] : 0u;
 }
 
+// Ranks within a wave by owner: one LDS atomic per distinct owner of the
+// wave's active lanes (a lane-per-atomic form serialises all 64 lanes on one
+// counter when one owner takes most swipes -- every swipe at world 1: 230 us
+// per 16M-swipe batch for the scatter).  Returns this lane's slot from c[o].
+__device__ __forceinline__ uint32_t route_wave_rank(uint32_t o, bool act, uint32_t *c) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t below = (uint64_t(1) << lane) - 1;
+    uint64_t rem = __ballot(act);
+    uint32_t r = 0;
+    while (rem) {  // wave-uniform: one round per distinct owner
+        const uint32_t leader = uint32_t(__builtin_ctzll(rem));
+        const uint32_t ol = __builtin_amdgcn_readlane(o, leader);
+        const bool mine = act && o == ol;
+        const uint64_t m = __ballot(mine);
+        uint32_t b = 0;
+        if (lane == leader) b = atomicAdd(&c[ol], uint32_t(__popcll(m)));
+        b = __builtin_amdgcn_readlane(b, leader);
+        if (mine) r = b + uint32_t(__popcll(m & below));
+        rem &= ~m;
+    }
+    return r;
+}
+
+// the owner (or kRtMaxWorld: a key past the table or naming no rank) and
+// local slot of global key g
+__device__ __forceinline__ uint32_t route_own_raw(const RouteArgs &R, uint32_t g) {
+    return g < R.nkeys ? R.kown[g] : kRtMaxWorld;
+}
+
+// Items in batches of kRtBatch per thread: every global load of a batch is
+// issued before the first wave rank, so a thread's loads are in flight
+// together instead of one dependent chain (slot -> owner -> rank) per item.
+constexpr uint32_t kRtBatch = 8;
+
 __global__ void __launch_bounds__(kRtBlock) k_route_count(const RouteArgs R) {
     __shared__ uint32_t c[kRtMaxWorld];
     const uint32_t tid = threadIdx.x;
     if (tid < R.world) c[tid] = 0;
     __syncthreads();
     const uint64_t b0 = uint64_t(blockIdx.x) * kRtTile;
+    for (uint32_t j0 = 0; j0 < kRtItems; j0 += kRtBatch) {
+        uint32_t g[kRtBatch], o[kRtBatch];
 #pragma unroll
-    for (uint32_t j = 0; j < kRtItems; j++) {
-        const uint64_t i = b0 + j * kRtBlock + tid;
-        if (i < R.n) atomicAdd(&c[route_owner(R, R.slot[i])], 1u);
+        for (uint32_t b = 0; b < kRtBatch; b++) {
+            const uint64_t i = b0 + (j0 + b) * kRtBlock + tid;
+            g[b] = i < R.n ? R.slot[i] : 0xffffffffu;
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kRtBatch; b++) o[b] = route_own_raw(R, g[b]);
+#pragma unroll
+        for (uint32_t b = 0; b < kRtBatch; b++) {
+            const bool act = b0 + (j0 + b) * kRtBlock + tid < R.n;
+            route_wave_rank(o[b] < R.world ? o[b] : 0u, act, c);
+        }
     }
     __syncthreads();
     if (tid < R.world) R.hist[size_t(tid) * R.nblocks + blockIdx.x] = c[tid];
@@ -120,10 +164,11 @@ __global__ void __launch_bounds__(kRtBlock) k_route_scatter(const RouteArgs R) {
 #pragma unroll 4
     for (uint32_t j = 0; j < kRtItems; j++) {
         const uint64_t i = b0 + j * kRtBlock + tid;
-        if (i >= R.n) continue;
-        const uint32_t g = R.slot[i];
-        const uint32_t o = route_owner(R, g);
-        const uint32_t p = base[o] + atomicAdd(&c[o], 1u);
+        const bool act = i < R.n;
+        const uint32_t g = act ? R.slot[i] : 0u;
+        const uint32_t o = act ? route_owner(R, g) : 0u;
+        const uint32_t p = base[o] + route_wave_rank(o, act, c);
+        if (!act) continue;
         R.pos[i] = p;
         R.sslot[p] = route_known(R, g) ? R.kloc[g] : kNoSlot;
         const uint8_t *src = R.ids + i * R.width;
@@ -154,23 +199,40 @@ __global__ void __launch_bounds__(kRtBlock) k_route_scatter_cap(const RouteArgs 
     }
     __syncthreads();
     const uint64_t b0 = uint64_t(blockIdx.x) * kRtTile;
-#pragma unroll 4
-    for (uint32_t j = 0; j < kRtItems; j++) {
-        const uint64_t i = b0 + j * kRtBlock + tid;
-        if (i >= R.n) continue;
-        const uint32_t g = R.slot[i];
-        const uint32_t o = route_owner(R, g);
-        const uint32_t r = base[o] + atomicAdd(&c[o], 1u);
-        const uint32_t p = o * cap + (r < cap ? r : r % cap);
-        R.pos[i] = p;
-        if (r >= cap) continue;  // overflow: tot[o] > cap reports it
-        R.sslot[p] = route_known(R, g) ? R.kloc[g] : kNoSlot;
-        const uint8_t *src = R.ids + i * R.width;
-        uint8_t *dst = R.sids + uint64_t(p) * R.width;
-        if (R.width == 8) {
-            *reinterpret_cast<uint64_t *>(dst) = *reinterpret_cast<const uint64_t *>(src);
-        } else {
-            for (uint32_t k = 0; k < R.width; k++) dst[k] = src[k];
+    const bool w8 = R.width == 8;
+    for (uint32_t j0 = 0; j0 < kRtItems; j0 += kRtBatch) {
+        uint32_t g[kRtBatch], o[kRtBatch], loc[kRtBatch];
+        uint64_t id[kRtBatch];
+#pragma unroll
+        for (uint32_t b = 0; b < kRtBatch; b++) {
+            const uint64_t i = b0 + (j0 + b) * kRtBlock + tid;
+            const bool act = i < R.n;
+            g[b] = act ? R.slot[i] : 0xffffffffu;
+            id[b] = act && w8 ? *reinterpret_cast<const uint64_t *>(R.ids + i * 8) : 0;
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kRtBatch; b++) {
+            o[b] = route_own_raw(R, g[b]);
+            loc[b] = o[b] < R.world ? R.kloc[g[b]] : kNoSlot;
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kRtBatch; b++) {
+            const uint64_t i = b0 + (j0 + b) * kRtBlock + tid;
+            const bool act = i < R.n;
+            const uint32_t ow = o[b] < R.world ? o[b] : 0u;
+            const uint32_t r = base[ow] + route_wave_rank(ow, act, c);
+            if (!act) continue;
+            const uint32_t p = ow * cap + (r < cap ? r : r % cap);
+            R.pos[i] = p;
+            if (r >= cap) continue;  // overflow: tot[o] > cap reports it
+            R.sslot[p] = loc[b];
+            if (w8) {
+                *reinterpret_cast<uint64_t *>(R.sids + uint64_t(p) * 8) = id[b];
+            } else {
+                const uint8_t *src = R.ids + i * R.width;
+                uint8_t *dst = R.sids + uint64_t(p) * R.width;
+                for (uint32_t k = 0; k < R.width; k++) dst[k] = src[k];
+            }
         }
     }
 }

@@ -230,12 +230,12 @@ def test_fail_lists_and_overflow_vs_oracle(engine, orc, invalid, error):
 
 
 @pytest.mark.parametrize("invalid", [0.1, 1.0])
-@pytest.mark.parametrize("capacity", [10_000_000, 20_000_000])
+@pytest.mark.parametrize("capacity", [10_000_000, 20_000_000, 40_000_000])
 def test_pass_a_counter_layouts_vs_oracle(engine, orc, invalid, capacity):
-    """The fail-list pass A's two counter tables: the 512-entry table of
-    chains under 512 slices (C3's 1e7 filter: 303) and the 2048-entry table
-    (2e7: 604 slices); a ragged last tile; answers and registers == the
-    oracle."""
+    """The fail-list pass A's two counter tables: 1024 counters (two per
+    thread) for chains under 512 slice pairs (C3's 1e7 filter: 303 slices,
+    2e7: 604) and 2048 for longer ones (4e7: over 1100 slices); a ragged last
+    tile; answers and registers == the oracle."""
     from rtsas_amd import synthetic
     from rtsas_amd.engine import DeviceBuffer
     w = synthetic.WORKLOADS["c3"]
