@@ -237,7 +237,10 @@ int ske_swipes_fixed_bits(ske_ctx *ctx, uint32_t fid, const uint32_t *slot, cons
 int ske_route_swipes(ske_ctx *ctx, const uint8_t *ids, uint32_t width, const uint32_t *gkey, uint64_t n,
                      uint32_t world, const uint32_t *key_owner, const uint32_t *key_local, uint32_t nkeys,
                      uint8_t *send_ids, uint32_t *send_slots, uint32_t *pos, uint64_t *counts);
-/* The same routing with no host synchronisation (enqueue only): owner o's
+/* The same routing with no host synchronisation (enqueue only), through one
+ * packed route word per key: key_route[g] = owner << 26 | local slot (local
+ * slot < 2^26), or 0xffffffff for a key no rank owns (rank 0, slot
+ * 0xffffffff, as above) -- one gather per swipe instead of two.  Owner o's
  * swipes fill rows [o*cap, o*cap + counts[o]) of send_ids / send_slots (device,
  * world*cap rows), so every peer pair exchanges exactly `cap` rows (an
  * all_to_all of equal splits the host sizes without reading the device).
@@ -249,9 +252,9 @@ int ske_route_swipes(ske_ctx *ctx, const uint8_t *ids, uint32_t width, const uin
  * (PFADD is idempotent, answers are rewritten).  world*cap < 2^32.
  * Replaces the per-event consumer loop's hand-off, attendance_processor.py:30-34. */
 int ske_route_swipes_cap_async(ske_ctx *ctx, const uint8_t *ids, uint32_t width, const uint32_t *gkey, uint64_t n,
-                               uint32_t world, const uint32_t *key_owner, const uint32_t *key_local, uint32_t nkeys,
-                               uint32_t cap, const uint32_t *sink_slots, uint8_t *send_ids, uint32_t *send_slots,
-                               uint32_t *pos, uint32_t *counts);
+                               uint32_t world, const uint32_t *key_route, uint32_t nkeys, uint32_t cap,
+                               const uint32_t *sink_slots, uint8_t *send_ids, uint32_t *send_slots, uint32_t *pos,
+                               uint32_t *counts);
 /* out[i] = answers[pos[i]]: the owners' BF.EXISTS answers, received back in
  * send order, into input order (enqueue only). */
 int ske_route_return_async(ske_ctx *ctx, const uint8_t *answers, const uint32_t *pos, uint64_t n,

@@ -1357,19 +1357,19 @@ int ske_route_swipes(ske_ctx *c, const uint8_t *ids, uint32_t width, const uint3
 }
 
 int ske_route_swipes_cap_async(ske_ctx *c, const uint8_t *ids, uint32_t width, const uint32_t *gkey, uint64_t n,
-                               uint32_t world, const uint32_t *key_owner, const uint32_t *key_local, uint32_t nkeys,
-                               uint32_t cap, const uint32_t *sink_slots, uint8_t *send_ids, uint32_t *send_slots,
-                               uint32_t *pos, uint32_t *counts) {
+                               uint32_t world, const uint32_t *key_route, uint32_t nkeys, uint32_t cap,
+                               const uint32_t *sink_slots, uint8_t *send_ids, uint32_t *send_slots, uint32_t *pos,
+                               uint32_t *counts) {
     if (!c || !counts || !sink_slots || world == 0 || world > 64 || width == 0 || width > 4096 ||
         n >= (uint64_t(1) << 32) || cap == 0 || uint64_t(cap) * world >= (uint64_t(1) << 32))
         return SKE_EINVAL;
     if (!send_ids || !send_slots || (n && (!ids || !gkey || !pos))) return SKE_EINVAL;
-    if (nkeys && (!key_owner || !key_local)) return SKE_EINVAL;
+    if (nkeys && !key_route) return SKE_EINVAL;
     hipError_t e = hipSuccess;
     uint32_t *hist = (uint32_t *)scratch_get(c->scratch, 40, route_hist_words(n, world) * 4 + 4, &e);
     if (e != hipSuccess) return scratch_error(c, e);
-    HIPCHK(c, launch_route_cap(ids, width, gkey, n, world, key_owner, key_local, nkeys, cap, sink_slots, send_ids,
-                               send_slots, pos, hist, counts, c->cus, c->st));
+    HIPCHK(c, launch_route_cap(ids, width, gkey, n, world, key_route, nkeys, cap, sink_slots, send_ids, send_slots,
+                               pos, hist, counts, c->cus, c->st));
     return SKE_OK;
 }
 

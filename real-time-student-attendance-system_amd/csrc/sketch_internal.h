@@ -87,9 +87,8 @@ uint64_t route_hist_words(uint64_t n, uint32_t world);
 // out (device) = answers in[0..n) packed 1 bit per swipe, LSB first; in must be 8-B aligned
 hipError_t launch_pack_bits(const uint8_t *in, uint64_t n, uint8_t *out, int cus, hipStream_t st);
 hipError_t launch_route_cap(const uint8_t *ids, uint32_t width, const uint32_t *slot, uint64_t n, uint32_t world,
-                            const uint32_t *kown, const uint32_t *kloc, uint32_t nkeys, uint32_t cap,
-                            const uint32_t *sink, uint8_t *sids, uint32_t *sslot, uint32_t *pos, uint32_t *hist,
-                            uint32_t *tot, int cus, hipStream_t st);
+                            const uint32_t *kroute, uint32_t nkeys, uint32_t cap, const uint32_t *sink, uint8_t *sids,
+                            uint32_t *sslot, uint32_t *pos, uint32_t *hist, uint32_t *tot, int cus, hipStream_t st);
 hipError_t launch_route_return(const uint8_t *ans, const uint32_t *pos, uint64_t n, uint8_t *out, int cus,
                                hipStream_t st);
 

@@ -34,8 +34,8 @@
 //
 // Two instantiations of the passes, picked by the host per chain:
 //   * one link of k = 11 (C3/C5's RESERVE 0.001 / 1e7 filter, the headline):
-//     k_part_a3 -> k_part_b<2, 3 or 4, true> -> k_part_c_fl (slice pairs,
-//     line-aligned pair runs, fail lists);
+//     k_part_a3 -> k_part_b<2, 4, true> -> k_part_c_fl (slice pairs, dense
+//     pair runs, fail lists);
 //   * any other chain the slice plan takes (several links, or k != 11; up to
 //     22 probes per swipe): k_part_a -> k_part_b<1 or 2> -> k_part_c (fail
 //     bytes).
@@ -43,7 +43,8 @@
 // numbers): 512-thread pass A without fail lists, 2048-swipe tiles, the
 // 16-copy counter table, pass A at three blocks per CU, the register
 // pre-check in pass A, PFADD by owned register lines, pass C on a side or
-// CU-masked stream.
+// CU-masked stream; in round 4 also pair runs padded to 128-B lines, the
+// tile parity unrolled, and a two-phase pass C.
 //
 // Placement of blocks on XCDs is a speed matter only; every (tile, slice) run
 // is read by exactly one block, and fail marks are only ever set.
@@ -349,55 +350,26 @@ __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const Par
 //     record's byte offset in the tile's LDS record array is the atomic's
 //     return value plus that word: one shift and one add per record;
 //   * full tiles take a probe loop without the past-the-batch select;
-//   * the two slices of a pair are counted apart (slice index = the DS
-//     address) but their runs are adjacent, and every pair's run starts on a
-//     multiple of kAlign records: kAlign 32 (chains of <= kAlignMaxUnits
-//     pairs, C3/C5) puts every run start on a 128-B line, so pass B reads
-//     ceil(len / 32) lines per run with no line shared between two pairs'
-//     runs; the gaps are never written (pass B's run bounds skip them).
-//     off[pair][tile] = start | count << 16 (one word per run for pass B);
-//   * the tile's counter parity is a compile-time constant (the tile loop
-//     runs two tiles per iteration), so every counter address is a DS
-//     immediate offset from the slice index.
+//   * the two slices of a pair are counted apart but their runs are
+//     adjacent with no gap (dense pair runs, round 4): pass B reads one word
+//     per (pair, tile), off[pair][tile] = start | count << 16.  Runs padded
+//     to 128-B lines made pass B read 12 % fewer lines but pass A write 21 %
+//     more bytes, a net loss (A/B in DESIGN.md section 3);
+//   * the counter scan's wave prefix is DPP (part_wave_scan) and a probe's
+//     counter address is v_bfe + v_lshl_add (0.238 -> 0.222 ms, round 4).
 // Counters of the two tile parities are one array (bias index par*kCnt + g);
 // lanes past the batch count into the first pair past the chain (the sink),
-// whose records land past the copy-out.
+// whose records land past the copy-out.  kCnt: 1024 (two counters per
+// thread) for chains of < 512 pairs (C3/C5: 152), else 2048.
 constexpr uint32_t kOORa = 0x80000000u;  // a buffer offset past every range: load 0, store dropped
-#ifndef SKE_PA_UNROLL
-#define SKE_PA_UNROLL 0
-#endif
-#ifndef SKE_ALIGN_BIG
-#define SKE_ALIGN_BIG 32
-#endif
-#ifndef SKE_A4_MAX_UNITS
-#define SKE_A4_MAX_UNITS (kCnt / 2 - 1)
-#endif
-#ifndef SKE_ALIGN_SMALL
-#define SKE_ALIGN_SMALL 1
-#endif
-// The line-aligned instantiation (kAlign 32, runs on 128-B lines) gives
-// wrong answers on MI355X once a pass-A block takes two or more tiles
-// (round 4: tests/test_k1_partitioned.py at >= 512k swipes; the same
-// algorithm passes in a host emulation and as kAlign 4), cause not found
-// yet: off by default, every fail-list chain takes kAlign 4.
-#ifndef SKE_ALIGN_MAX_UNITS
-#define SKE_ALIGN_MAX_UNITS 0
-#endif
-constexpr uint32_t kAlignMaxUnits = SKE_ALIGN_MAX_UNITS;  // pairs of the line-aligned instantiation (C3/C5: 152)
-#ifndef SKE_PA_WPE
-#define SKE_PA_WPE 4  // waves per SIMD: two 512-thread blocks per CU
-#endif
-template <int KM, uint32_t kCnt, uint32_t kAlign>
-__global__ void __launch_bounds__(512, SKE_PA_WPE) k_part_a3(const PartArgs A) {
+template <int KM, uint32_t kCnt>
+__global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two blocks per CU
     constexpr uint32_t kT = 512;
     constexpr uint32_t kU = 1024 / kT, kTile = 1024;
     constexpr uint32_t kPer = kCnt / kT;  // counters per thread: kPer / 2 whole pairs
-    constexpr uint32_t kMaxUnits = kAlign >= SKE_ALIGN_BIG ? kAlignMaxUnits : SKE_A4_MAX_UNITS;
-    // records, plus the largest padding, rounded so the fixed-count copy-out's
-    // LDS reads stay inside the block (the counters follow the records)
-    constexpr uint32_t kRecWords = kTile * KM + (kAlign > 1 ? kAlign * (kMaxUnits + 1) : 0);
-    constexpr uint32_t kCo = (kRecWords / 4 + kT - 1) / kT;
-    static_assert(kCnt % (2 * kT) == 0 && kRecWords < 65536u && 4u * kTile * KM < 65536u,
+    constexpr uint32_t kRecWords = kTile * KM;  // (the sink's records land past the copy-out)
+    constexpr uint32_t kCo = (kRecWords / 4 + kT - 1) / kT;  // 16-B copy-out pieces per thread
+    static_assert(kCnt % (2 * kT) == 0 && 4u * kTile * KM < 65536u,
                   "whole pairs per thread; a rank * 4 below bit 16; starts fit 16 bits");
     // one LDS object, counters first: it sits at LDS address 0, so a probe's
     // counter address is its slice field shifted and added to the parity's
@@ -461,8 +433,8 @@ __global__ void __launch_bounds__(512, SKE_PA_WPE) k_part_a3(const PartArgs A) {
         asm("v_bfe_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "i"(kPSliceLog), "i"(kW));
         return r;
     };
-    auto tile = [&](const uint32_t t, auto parc) {
-        const uint32_t cb = uint32_t(parc) * kCnt;
+    auto tile = [&](const uint32_t t, const uint32_t par) {
+        const uint32_t cb = par * kCnt;
         const uint32_t pb = cb * 4;  // the parity's byte base, above (kCnt - 1) * 4
         uint32_t rv[kU][KM], rp[kU][KM];
         const uint32_t tn = t + tstep < gt1 ? t + tstep : t;
@@ -507,7 +479,7 @@ __global__ void __launch_bounds__(512, SKE_PA_WPE) k_part_a3(const PartArgs A) {
         lds_barrier();
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++) part_id_load(rbytes, nb_[u], ne_[u], it[u]);  // the next tile's ids
-        // exclusive scan over pairs of their counts rounded up to kAlign
+        // exclusive scan over pairs of their two slices' counts
         uint32_t v[kPer], s = 0;
 #pragma unroll
         for (uint32_t j = 0; j < kPer; j++) {
@@ -515,7 +487,7 @@ __global__ void __launch_bounds__(512, SKE_PA_WPE) k_part_a3(const PartArgs A) {
             v[j] = (cnt[c] - (c << 18)) >> 2;
         }
 #pragma unroll
-        for (uint32_t j = 0; j < kPer; j += 2) s += (v[j] + v[j + 1] + kAlign - 1) & ~(kAlign - 1);
+        for (uint32_t j = 0; j < kPer; j += 2) s += v[j] + v[j + 1];
         const uint32_t incl = part_wave_scan(s);
         if (lane == 63) swsum[wave] = incl;
         lds_barrier();
@@ -529,7 +501,7 @@ __global__ void __launch_bounds__(512, SKE_PA_WPE) k_part_a3(const PartArgs A) {
             if (g == sink) stot = run;
             cnt[c] = 4 * run - (c << 18);
             cnt[c + 1] = 4 * (run + v[j]) - ((c + 1) << 18);
-            run += (n2 + kAlign - 1) & ~(kAlign - 1);
+            run += n2;
         }
         lds_barrier();
 #pragma unroll
@@ -545,7 +517,7 @@ __global__ void __launch_bounds__(512, SKE_PA_WPE) k_part_a3(const PartArgs A) {
         lds_barrier();
         const uint32_t total = stot;
         // a fixed number of 16-B pieces per thread (those past the tile's
-        // total go out of range; the gaps between runs are copied as they are)
+        // total go out of range)
         const __amdgpu_buffer_rsrc_t rdst = part_rsrc(A.rec + size_t(t) * A.stride, A.stride * 4);
         // (a piece past the records reads the last piece instead: an LDS read
         // past srec would be undefined behaviour, from which the compiler may
@@ -560,15 +532,8 @@ __global__ void __launch_bounds__(512, SKE_PA_WPE) k_part_a3(const PartArgs A) {
                                                    rdst, j * 4 < total ? j * 16 : kOORa, 0, nt_aux<4>());
         }
     };
-#if SKE_PA_UNROLL
-    for (uint32_t t = gt0 + blockIdx.x / kPGroups; t < gt1; t += 2 * tstep) {
-        tile(t, std::integral_constant<uint32_t, 0>{});
-        if (t + tstep < gt1) tile(t + tstep, std::integral_constant<uint32_t, 1>{});
-    }
-#else
     uint32_t par = 0;
     for (uint32_t t = gt0 + blockIdx.x / kPGroups; t < gt1; t += tstep, par ^= 1) tile(t, par);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -975,11 +940,11 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
 // (Its loads and stores at a fixed count per tile, as pass A's, measured
 // equal, 0.408 vs 0.409 ms: pass C is bound by the memory side's random
 // requests, not by its waves' waits.)
-// kPhase (SKE_PC_PHASES 2): 1 = the answers and the rank-1 updates only
-// (a register still 0 gets a plain byte store of 1: every writer of this
-// phase writes 1, so no update can be lost), 2 = the rank >= 2 updates by
-// CAS, after phase 1 has finished; 0 = both in one pass (CAS for all).
-template <int U, int kPhase = 0>
+// (A two-phase form -- the answers and the rank-1 raises as plain byte
+// stores first, the rank >= 2 raises by CAS in a second kernel -- measured
+// slower, 0.409 -> 0.436 ms, round 4: the line traffic, not the CAS count,
+// holds this pass.)
+template <int U>
 __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
     static_assert(kPcBlock * U == 1024, "one 1024-swipe tile per sub-step");
     constexpr uint32_t kRun = kPbGroup;  // tiles per block iteration
@@ -1050,8 +1015,8 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
                 if (valid[u]) {
                     const uint32_t rk = cur.hv[u] >> 16;
                     if (cur.sl[u] >= A.nslots) {
-                        if (kPhase != 2) atomicOr(A.err, 1u);
-                    } else if (kPhase == 0 || (kPhase == 1) == (rk == 1)) {
+                        atomicOr(A.err, 1u);
+                    } else {
                         const uint32_t ridx = cur.hv[u] & 0xffffu;
                         w[u] = reinterpret_cast<uint32_t *>(A.regs + (uint64_t(cur.sl[u]) << kHllP) + (ridx & ~3u));
                         sh[u] = (ridx & 3) * 8;
@@ -1061,21 +1026,6 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
             }
 #pragma unroll
             for (int u = 0; u < U; u++) cw[u] = w[u] ? nt_ld<32>(w[u]) : 0xffffffffu;
-            if constexpr (kPhase == 1) {
-#pragma unroll
-                for (int u = 0; u < U; u++)
-                    if (w[u] && ((cw[u] >> sh[u]) & 0xffu) == 0)
-                        reinterpret_cast<uint8_t *>(w[u])[sh[u] / 8] = 1;
-                if (A.out) {
-#pragma unroll
-                    for (int u = 0; u < U; u++) {
-                        const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
-                        if (i < A.n) nt_st<16>(A.out + i, uint8_t(valid[u]));
-                    }
-                }
-                cur = nxt;
-                continue;
-            }
             // every raising CAS of the tile in flight at once, then settled
             // (a lost race retries from the word the CAS returned)
 #pragma unroll
@@ -1084,7 +1034,7 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
                 if (w[u] && ((cw[u] >> sh[u]) & 0xffu) < rank[u])
                     seen[u] = atomicCAS(w[u], cw[u], (cw[u] & ~(0xffu << sh[u])) | (rank[u] << sh[u]));
             }
-            if (kPhase == 0 && A.out) {
+            if (A.out) {
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
@@ -1122,10 +1072,8 @@ static uint32_t part_km(uint32_t ksum) {
 static uint32_t part_stride(uint32_t ksum) { return ((ksum << kPTileLog) + 31) & ~31u; }
 
 // the fail-list instantiation: one link of k = 11 (C3/C5's filter), slice
-// pairs, pair runs aligned to part_align() records (the sink pair must fit
-// k_part_a3<11, 2048>'s counters)
+// pairs (the sink pair must fit k_part_a3<11, 2048>'s counters)
 static bool part_flist(const PartArgs &A) { return A.nlinks == 1 && A.ksum == 11 && A.nslices <= 2046; }
-static uint32_t part_align(const PartArgs &A) { return A.nunits <= kAlignMaxUnits ? SKE_ALIGN_BIG : SKE_ALIGN_SMALL; }
 
 static bool part_plan(const ChainDev &ch, PartArgs *A) {
     if (ch.nlinks < 1 || ch.nlinks > kPMaxLinks) return false;
@@ -1151,8 +1099,6 @@ static bool part_plan(const ChainDev &ch, PartArgs *A) {
     A->ksum = ksum;
     A->nunits = (slices + 1) / 2;
     A->stride = part_stride(ksum);
-    if (part_flist(*A))  // room for the pair runs' alignment gaps
-        A->stride = (A->stride + part_align(*A) * (A->nunits + 1) + 31) & ~31u;
     return true;
 }
 
@@ -1195,15 +1141,6 @@ hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratc
     return part_scratch(&A, n ? n : 1, part_sub(sub_opt), scr);
 }
 
-#ifndef SKE_PC_PHASES
-#define SKE_PC_PHASES 1
-#endif
-#ifndef SKE_PA_CNT_AL
-#define SKE_PA_CNT_AL 1024
-#endif
-#ifndef SKE_PB_R_AL
-#define SKE_PB_R_AL 3
-#endif
 // Units = (batch, sub-batch of at most `sub` swipes), in order, each as the
 // three passes on `st`.  `hook` (pass timing) brackets every kernel.
 hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t nb, uint8_t *regs,
@@ -1223,10 +1160,9 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
     const uint32_t km = part_km(A.ksum);
     // one link of k = 11 (C3/C5): slice pairs and fail lists
     const bool flist = part_flist(A) && A.flist != nullptr;
-    const bool aligned = part_align(A) == SKE_ALIGN_BIG;
     const bool pairs = A.nlinks == 1;  // a one-link chain is probed in slice pairs (128 KiB images)
     const unsigned ga = unsigned(cus) * (km <= 11 ? 2u : 1u) / kPGroups * kPGroups;  // blocks past a group's tiles exit
-    const unsigned g2 = unsigned(cus) * (SKE_PA_WPE / 2) / kPGroups * kPGroups;  // pass A: resident blocks
+    const unsigned g2 = unsigned(cus) * 2 / kPGroups * kPGroups;  // k_part_a3: two blocks per CU
     const unsigned gb = unsigned(cus) * (pairs ? 1 : 2) / kPGroups * kPGroups;  // all resident
     for (uint32_t j = 0; j < nb; j++) {
         const PartBatch &B = bt[j];
@@ -1246,21 +1182,17 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             A.slot = B.slot + s0;
             A.out = B.out ? B.out + s0 : nullptr;
             if (hook) hook(hook_user, 0, 0, st);
-            if (flist && aligned)  // runs on 128-B lines (C3/C5: 152 pairs)
-                hipLaunchKernelGGL((k_part_a3<11, SKE_PA_CNT_AL, SKE_ALIGN_BIG>), dim3(g2), dim3(512), 0, st, A);
-            else if (flist && A.nunits < 512)  // C3/C5: 152 pairs, two counters per thread
-                hipLaunchKernelGGL((k_part_a3<11, 1024, SKE_ALIGN_SMALL>), dim3(g2), dim3(512), 0, st, A);
+            if (flist && A.nunits < 512)  // C3/C5: 152 pairs, two counters per thread
+                hipLaunchKernelGGL((k_part_a3<11, 1024>), dim3(g2), dim3(512), 0, st, A);
             else if (flist)
-                hipLaunchKernelGGL((k_part_a3<11, 2048, SKE_ALIGN_SMALL>), dim3(g2), dim3(512), 0, st, A);
+                hipLaunchKernelGGL((k_part_a3<11, 2048>), dim3(g2), dim3(512), 0, st, A);
             else if (km <= 11)
                 hipLaunchKernelGGL(k_part_a<11>, dim3(ga), dim3(kPaBlock), 0, st, A);
             else
                 hipLaunchKernelGGL(k_part_a<22>, dim3(ga), dim3(kPaBlock), 0, st, A);
             if (hook) hook(hook_user, 0, 1, st);
             if (hook) hook(hook_user, 1, 0, st);
-            if (flist && aligned)  // a run of up to 96 records in 3 lines (longer: the tail loop)
-                hipLaunchKernelGGL((k_part_b<2, SKE_PB_R_AL, true>), dim3(gb), dim3(kPbBlock), 0, st, A);
-            else if (flist)
+            if (flist)
                 hipLaunchKernelGGL((k_part_b<2, 4, true>), dim3(gb), dim3(kPbBlock), 0, st, A);
             else if (pairs)
                 hipLaunchKernelGGL(k_part_b<2>, dim3(gb), dim3(kPbBlock), 0, st, A);
@@ -1271,12 +1203,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             if (flist) {
                 const unsigned gc =
                     (part_grid(ms, 1024 * kPbGroup, unsigned(cus) * 8) + kPGroups - 1) / kPGroups * kPGroups;
-#if SKE_PC_PHASES == 2
-                hipLaunchKernelGGL((k_part_c_fl<4, 1>), dim3(gc), dim3(kPcBlock), 0, st, A);
-                hipLaunchKernelGGL((k_part_c_fl<4, 2>), dim3(gc), dim3(kPcBlock), 0, st, A);
-#else
                 hipLaunchKernelGGL(k_part_c_fl<4>, dim3(gc), dim3(kPcBlock), 0, st, A);
-#endif
             } else {
                 const unsigned gc = (part_grid(ms, kPcBlock * 2, unsigned(cus) * 8) + kPGroups - 1) / kPGroups * kPGroups;
                 hipLaunchKernelGGL(k_part_c<2>, dim3(gc), dim3(kPcBlock), 0, st, A);

@@ -20,6 +20,10 @@
 //                   local slots scattered there, pos[i] recorded
 //   k_route_return  out[i] = answers[pos[i]]
 //
+// The capacity form (no host synchronisation) takes one packed route word per
+// key, owner << 26 | local slot: k_route_count_cap gathers it once per swipe
+// and parks it in pos[i], k_route_scatter_cap streams it back (no gather).
+//
 // The order inside an (owner, block) segment is whatever the LDS atomics
 // give -- immaterial: every swipe keeps its position, and the registers are
 // a max.  Streams of bytes, HBM bound: per swipe the id, the slot, the
@@ -41,6 +45,7 @@ struct RouteArgs {
     const uint32_t *slot;  // global key indices
     const uint32_t *kown;  // [nkeys] owner rank of each global key
     const uint32_t *kloc;  // [nkeys] local slot of each global key on its owner
+    const uint32_t *kroute;  // [nkeys] owner << 26 | local slot (the capacity form), ~0: no owner
     uint8_t *sids;         // n x width, owner major
     uint32_t *sslot;       // local slots, owner major
     uint32_t *pos;         // input swipe -> position in the send buffers
@@ -189,6 +194,43 @@ __global__ void __launch_bounds__(kRtBlock) k_route_scatter(const RouteArgs R) {
 // same owner, answered for another swipe) -- tot[o] > cap tells the host,
 // which then re-runs the batch with exact splits (PFADD is idempotent and
 // the answers are rewritten).
+// The capacity form's count: one gather per swipe of its key's packed route
+// word, kept in pos[i] for the scatter (which then gathers nothing: every
+// access of k_route_scatter_cap is a coalesced stream).
+__device__ __forceinline__ uint32_t route_word_owner(const RouteArgs &R, uint32_t kr) {
+    return (kr >> 26) < R.world ? kr >> 26 : 0u;  // ~0 (no owner) -> rank 0
+}
+__device__ __forceinline__ uint32_t route_word_slot(const RouteArgs &R, uint32_t kr) {
+    return (kr >> 26) < R.world ? kr & 0x3ffffffu : kNoSlot;
+}
+
+__global__ void __launch_bounds__(kRtBlock) k_route_count_cap(const RouteArgs R) {
+    __shared__ uint32_t c[kRtMaxWorld];
+    const uint32_t tid = threadIdx.x;
+    if (tid < R.world) c[tid] = 0;
+    __syncthreads();
+    const uint64_t b0 = uint64_t(blockIdx.x) * kRtTile;
+    for (uint32_t j0 = 0; j0 < kRtItems; j0 += kRtBatch) {
+        uint32_t g[kRtBatch], kr[kRtBatch];
+#pragma unroll
+        for (uint32_t b = 0; b < kRtBatch; b++) {
+            const uint64_t i = b0 + (j0 + b) * kRtBlock + tid;
+            g[b] = i < R.n ? R.slot[i] : 0xffffffffu;
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kRtBatch; b++) kr[b] = g[b] < R.nkeys ? R.kroute[g[b]] : 0xffffffffu;
+#pragma unroll
+        for (uint32_t b = 0; b < kRtBatch; b++) {
+            const uint64_t i = b0 + (j0 + b) * kRtBlock + tid;
+            const bool act = i < R.n;
+            if (act) R.pos[i] = kr[b];
+            route_wave_rank(route_word_owner(R, kr[b]), act, c);
+        }
+    }
+    __syncthreads();
+    if (tid < R.world) R.hist[size_t(tid) * R.nblocks + blockIdx.x] = c[tid];
+}
+
 __global__ void __launch_bounds__(kRtBlock) k_route_scatter_cap(const RouteArgs R, uint32_t cap) {
     __shared__ uint32_t c[kRtMaxWorld], base[kRtMaxWorld];
     const uint32_t tid = threadIdx.x;
@@ -201,31 +243,26 @@ __global__ void __launch_bounds__(kRtBlock) k_route_scatter_cap(const RouteArgs 
     const uint64_t b0 = uint64_t(blockIdx.x) * kRtTile;
     const bool w8 = R.width == 8;
     for (uint32_t j0 = 0; j0 < kRtItems; j0 += kRtBatch) {
-        uint32_t g[kRtBatch], o[kRtBatch], loc[kRtBatch];
+        uint32_t kr[kRtBatch];
         uint64_t id[kRtBatch];
 #pragma unroll
         for (uint32_t b = 0; b < kRtBatch; b++) {
             const uint64_t i = b0 + (j0 + b) * kRtBlock + tid;
             const bool act = i < R.n;
-            g[b] = act ? R.slot[i] : 0xffffffffu;
+            kr[b] = act ? R.pos[i] : 0xffffffffu;  // the count's route word
             id[b] = act && w8 ? *reinterpret_cast<const uint64_t *>(R.ids + i * 8) : 0;
-        }
-#pragma unroll
-        for (uint32_t b = 0; b < kRtBatch; b++) {
-            o[b] = route_own_raw(R, g[b]);
-            loc[b] = o[b] < R.world ? R.kloc[g[b]] : kNoSlot;
         }
 #pragma unroll
         for (uint32_t b = 0; b < kRtBatch; b++) {
             const uint64_t i = b0 + (j0 + b) * kRtBlock + tid;
             const bool act = i < R.n;
-            const uint32_t ow = o[b] < R.world ? o[b] : 0u;
+            const uint32_t ow = route_word_owner(R, kr[b]);
             const uint32_t r = base[ow] + route_wave_rank(ow, act, c);
             if (!act) continue;
             const uint32_t p = ow * cap + (r < cap ? r : r % cap);
             R.pos[i] = p;
             if (r >= cap) continue;  // overflow: tot[o] > cap reports it
-            R.sslot[p] = loc[b];
+            R.sslot[p] = route_word_slot(R, kr[b]);
             if (w8) {
                 *reinterpret_cast<uint64_t *>(R.sids + uint64_t(p) * 8) = id[b];
             } else {
@@ -254,19 +291,18 @@ __global__ void __launch_bounds__(256) k_route_pad(const RouteArgs R, uint32_t c
 }
 
 hipError_t launch_route_cap(const uint8_t *ids, uint32_t width, const uint32_t *slot, uint64_t n, uint32_t world,
-                            const uint32_t *kown, const uint32_t *kloc, uint32_t nkeys, uint32_t cap,
-                            const uint32_t *sink, uint8_t *sids, uint32_t *sslot, uint32_t *pos, uint32_t *hist,
-                            uint32_t *tot, int cus, hipStream_t st) {
+                            const uint32_t *kroute, uint32_t nkeys, uint32_t cap, const uint32_t *sink, uint8_t *sids,
+                            uint32_t *sslot, uint32_t *pos, uint32_t *hist, uint32_t *tot, int cus, hipStream_t st) {
     if (world == 0 || world > kRtMaxWorld || width == 0 || n >= (uint64_t(1) << 32) || cap == 0 ||
         uint64_t(cap) * world >= (uint64_t(1) << 32))
         return hipErrorInvalidValue;
-    RouteArgs R{ids, slot, kown, kloc, sids, sslot, pos, hist, tot, n, width, world,
+    RouteArgs R{ids, slot, nullptr, nullptr, kroute, sids, sslot, pos, hist, tot, n, width, world,
                 uint32_t((n + kRtTile - 1) / kRtTile), nkeys};
     if (n == 0) {
         hipError_t e = hipMemsetAsync(tot, 0, size_t(world) * 4, st);
         if (e != hipSuccess) return e;
     } else {
-        hipLaunchKernelGGL(k_route_count, dim3(R.nblocks), dim3(kRtBlock), 0, st, R);
+        hipLaunchKernelGGL(k_route_count_cap, dim3(R.nblocks), dim3(kRtBlock), 0, st, R);
         hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(1024), 0, st, R);
         hipLaunchKernelGGL(k_route_scatter_cap, dim3(R.nblocks), dim3(kRtBlock), 0, st, R, cap);
     }
@@ -276,17 +312,30 @@ hipError_t launch_route_cap(const uint8_t *ids, uint32_t width, const uint32_t *
     return hipGetLastError();
 }
 
+// four answers per thread: one 16-B load of positions, one 4-B store (pos
+// and out 16-B / 4-B aligned, checked by the host; else one per thread)
 __global__ void __launch_bounds__(256) k_route_return(const uint8_t *ans, const uint32_t *pos, uint64_t n,
                                                       uint8_t *out) {
     for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256)
         out[i] = ans[pos[i]];
+}
+__global__ void __launch_bounds__(256) k_route_return4(const uint8_t *ans, const uint32_t *pos, uint64_t n,
+                                                       uint8_t *out) {
+    const uint64_t n4 = n / 4;
+    for (uint64_t q = uint64_t(blockIdx.x) * 256 + threadIdx.x; q < n4; q += uint64_t(gridDim.x) * 256) {
+        const uint4 p = reinterpret_cast<const uint4 *>(pos)[q];
+        const uint32_t v = uint32_t(ans[p.x]) | uint32_t(ans[p.y]) << 8 | uint32_t(ans[p.z]) << 16 |
+                           uint32_t(ans[p.w]) << 24;
+        reinterpret_cast<uint32_t *>(out)[q] = v;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) out[n4 * 4 + threadIdx.x] = ans[pos[n4 * 4 + threadIdx.x]];
 }
 
 hipError_t launch_route(const uint8_t *ids, uint32_t width, const uint32_t *slot, uint64_t n, uint32_t world,
                         const uint32_t *kown, const uint32_t *kloc, uint32_t nkeys, uint8_t *sids,
                         uint32_t *sslot, uint32_t *pos, uint32_t *hist, uint32_t *tot, hipStream_t st) {
     if (world == 0 || world > kRtMaxWorld || width == 0 || n >= (uint64_t(1) << 32)) return hipErrorInvalidValue;
-    RouteArgs R{ids, slot, kown, kloc, sids, sslot, pos, hist, tot, n, width, world,
+    RouteArgs R{ids, slot, kown, kloc, nullptr, sids, sslot, pos, hist, tot, n, width, world,
                 uint32_t((n + kRtTile - 1) / kRtTile), nkeys};
     if (n == 0) return hipMemsetAsync(tot, 0, size_t(world) * 4, st);
     hipLaunchKernelGGL(k_route_count, dim3(R.nblocks), dim3(kRtBlock), 0, st, R);
@@ -327,9 +376,13 @@ uint64_t route_hist_words(uint64_t n, uint32_t world) { return uint64_t(world) *
 hipError_t launch_route_return(const uint8_t *ans, const uint32_t *pos, uint64_t n, uint8_t *out, int cus,
                                hipStream_t st) {
     if (n == 0) return hipSuccess;
-    const uint64_t g = (n + 255) / 256;
-    const unsigned grid = unsigned(g < uint64_t(cus) * 8 ? g : uint64_t(cus) * 8);
-    hipLaunchKernelGGL(k_route_return, dim3(grid), dim3(256), 0, st, ans, pos, n, out);
+    const bool v4 = (reinterpret_cast<uintptr_t>(pos) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 3) == 0;
+    const uint64_t g = ((v4 ? n / 4 : n) + 255) / 256;
+    const unsigned grid = unsigned(g < 1 ? 1 : g < uint64_t(cus) * 8 ? g : uint64_t(cus) * 8);
+    if (v4)
+        hipLaunchKernelGGL(k_route_return4, dim3(grid), dim3(256), 0, st, ans, pos, n, out);
+    else
+        hipLaunchKernelGGL(k_route_return, dim3(grid), dim3(256), 0, st, ans, pos, n, out);
     return hipGetLastError();
 }
 

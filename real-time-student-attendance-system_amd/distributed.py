@@ -117,6 +117,22 @@ class KeyMap:
                               torch.from_numpy(self.local.view(np.int32)).to(device))
         return self._dev[key]
 
+    def route_words(self) -> np.ndarray:
+        """uint32 owner << 26 | local slot per key (ske_route_swipes_cap_async's
+        key_route; local slots < 2^26)."""
+        own = self.owner.astype(np.uint64)
+        loc = self.local.astype(np.uint64)
+        assert loc.size == 0 or int(loc.max()) < (1 << 26)
+        return ((own << np.uint64(26)) | loc).astype(np.uint32)
+
+    def route_table(self, device):
+        """route_words() as an int32 torch tensor on `device` (cached)."""
+        import torch
+        key = "route:" + str(device)
+        if key not in self._dev:
+            self._dev[key] = torch.from_numpy(self.route_words().view(np.int32)).to(device)
+        return self._dev[key]
+
 
 class LibsketchOps:
     """Device side of the sharded queries (torch tensors on this rank's GPU)."""
@@ -508,7 +524,7 @@ class SwipeExchange:
         dev = ids.device
         ids = ids.contiguous()
         g32 = gkeys.to(torch.int32).contiguous()
-        own, loc = self.keymap.tables(dev)
+        kroute = self.keymap.route_table(dev)
         rows = self.world * cap
         send_ids = torch.empty(rows * w + 16, dtype=torch.uint8, device=dev)  # + K1's readable tail
         send_slots = torch.empty(rows, dtype=torch.int32, device=dev)
@@ -521,7 +537,7 @@ class SwipeExchange:
         try:
             eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
             eng.ctx.call("ske_route_swipes_cap_async", C.c_void_p(ids.data_ptr()), w, C.c_void_p(g32.data_ptr()), n,
-                         self.world, C.c_void_p(own.data_ptr()), C.c_void_p(loc.data_ptr()), len(self.keymap),
+                         self.world, C.c_void_p(kroute.data_ptr()), len(self.keymap),
                          cap, C.c_void_p(self._sink_dev.data_ptr()), C.c_void_p(send_ids.data_ptr()),
                          C.c_void_p(send_slots.data_ptr()), C.c_void_p(pos.data_ptr()),
                          C.c_void_p(counts.data_ptr()))
