@@ -202,6 +202,10 @@ def test_key_map_is_one_rule(pkg):
     assert sum(km.count(r) for r in range(5)) == len(names)
     enc = [n.encode() for n in names]
     assert murmur64a_many(enc, 0x1234).tolist() == [murmur64a(b, 0x1234) for b in enc]
+    # the capacity routing's packed word per key: owner << 26 | local slot
+    w = km.route_words()
+    assert w.dtype == np.uint32
+    assert ((w >> 26) == km.owner).all() and ((w & 0x3ffffff) == km.local).all()
 
 
 def test_exchange_one_rank_no_group(orc):
