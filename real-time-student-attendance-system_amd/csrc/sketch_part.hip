@@ -116,6 +116,15 @@ __device__ __forceinline__ void part_group(uint32_t ntiles, uint32_t x, uint32_t
     t1 = uint32_t(uint64_t(ntiles) * (x + 1) / kPGroups);
 }
 
+// Bit (pos & 31) of w: v_bfe_u32 reads only its offset operand's low 5 bits,
+// so pos goes in as it is (the compiler's ubfe masks it first: one VALU per
+// probe record in pass B)
+__device__ __forceinline__ uint32_t part_bit(uint32_t w, uint32_t pos) {
+    uint32_t r;
+    asm("v_bfe_u32 %0, %1, %2, 1" : "=v"(r) : "v"(w), "v"(pos));
+    return r;
+}
+
 // Inclusive prefix sum over a wave's 64 lanes on DPP: row shifts 1, 2, 4, 8
 // inside 16-lane rows, then row_bcast:15 / row_bcast:31 across rows (gfx9);
 // a lane whose source is outside its row adds the identity.  VALU only.
@@ -747,16 +756,16 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                 rec[4 * c + 2] = r[c].z;
                 rec[4 * c + 3] = r[c].w;
             }
-            auto in_run = [&](uint32_t lo) {  // 4-bit mask of lo + j in [bc, ec), j < 4
-                const int32_t hi = int32_t(ec) - int32_t(lo), lw = int32_t(bc) - int32_t(lo);
-                const uint32_t nh = uint32_t(hi < 0 ? 0 : (hi > 4 ? 4 : hi));
-                const uint32_t nl = uint32_t(lw < 0 ? 0 : (lw > 4 ? 4 : lw));
-                return ((1u << nh) - 1u) & ~((1u << nl) - 1u);
-            };
+            // bit 4c + j: record lo0 + 32c + j lies in [bc, ec).  Only piece 0
+            // can start before bc (s0 = bc & ~31), so the lower bound masks
+            // piece 0 alone; the upper bound clamps every piece.
+            auto clamp4 = [](int32_t v) { return uint32_t(v < 0 ? 0 : (v > 4 ? 4 : v)); };
             const uint32_t lo0 = s0 + qq * 4;
+            const int32_t dh = int32_t(ec) - int32_t(lo0);
             uint32_t vm = 0;
 #pragma unroll
-            for (uint32_t c = 0; c < R; c++) vm |= in_run(lo0 + c * 32) << (4 * c);
+            for (uint32_t c = 0; c < R; c++) vm |= ((1u << clamp4(dh - int32_t(32 * c))) - 1u) << (4 * c);
+            vm &= ~((1u << clamp4(int32_t(bc) - int32_t(lo0))) - 1u);
             // bit set in the image: its 32-bit word, bit (offset & 31); with
             // slice pairs the record's parity bit selects the image half
             const uint32_t *img32 = reinterpret_cast<const uint32_t *>(img);
@@ -767,7 +776,7 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                 const uint32_t o = FL ? (rr & 0xfffffu)  // k_part_a3: the offset in the pair
                                       : SP == 1 ? (rr & kPSliceMask)
                                                 : ((rr & kPSliceMask) | ((rr >> kPTileLog) & kPSliceBits));
-                okm |= __builtin_amdgcn_ubfe(img32[o >> 5], rr & 31, 1) << j;
+                okm |= part_bit(img32[o >> 5], rr) << j;
             }
             uint32_t fm = vm & ~okm;
             const uint32_t tbase = (tg + k) << kPTileLog;
