@@ -125,6 +125,13 @@ __device__ __forceinline__ uint32_t part_bit(uint32_t w, uint32_t pos) {
     return r;
 }
 
+// ((1 << width) - 1) << offset (width, offset < 32) as one v_bfm_b32
+__device__ __forceinline__ uint32_t part_bfm(uint32_t width, uint32_t offset) {
+    uint32_t r;
+    asm("v_bfm_b32 %0, %1, %2" : "=v"(r) : "v"(width), "s"(offset));
+    return r;
+}
+
 // Inclusive prefix sum over a wave's 64 lanes on DPP: row shifts 1, 2, 4, 8
 // inside 16-lane rows, then row_bcast:15 / row_bcast:31 across rows (gfx9);
 // a lane whose source is outside its row adds the identity.  VALU only.
@@ -719,23 +726,27 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
         };
         // 16-byte pieces qq, qq + 8, ... of the run from the 128-B line holding
         // its start: every piece is one whole line (one request, not two)
+        // (one byte offset per lane; piece c adds 128 c, an immediate of the
+        // load; a piece past the run's end goes out of range)
         auto load_recs = [&](uint32_t tg, uint32_t b, uint32_t e, uint4 (&r)[R]) {
-            const uint32_t base = (tg + k) * A.stride, s0 = b & ~31u;
+            const uint32_t i0 = (b & ~31u) + qq * 4;
+            const uint32_t v0 = ((tg + k) * A.stride + i0) * 4;
+            const int32_t left = int32_t(e) - int32_t(i0);
 #pragma unroll
-            for (uint32_t c = 0; c < R; c++) {
-                const uint32_t i = s0 + c * 32 + qq * 4;
+            for (uint32_t c = 0; c < R; c++)
                 r[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     rrec, i < e ? (base + i) * 4 : kOOR, 0, 2));
-            }
+                                                     rrec, (left > int32_t(32 * c) ? v0 : kOOR) + 128 * c, 0, 2));
         };
         uint32_t tg = ta + wave * kPbGroup;
         uint32_t Bc, Ec, Bn, En;  // boundaries of rounds [8q, 8q + 8) and of the 8 after
         load_be8(tg, Bc, Ec);
         load_be8(tg + kPbGroup * kStep, Bn, En);
         uint32_t bc = __shfl(Bc, k, 64), ec = __shfl(Ec, k, 64);
-        uint4 r[R];
-        load_recs(tg, bc, ec, r);
-        for (uint32_t rr = 0; tg < tb; tg += kStep, rr++) {
+        // one round = kPbGroup tiles' runs of this unit; the next round's
+        // records load while this one is tested.  Two rounds per loop
+        // iteration with the record buffers in turn (no register copies).
+        uint32_t rr = 0;
+        auto round = [&](const uint4 (&r)[R], uint4 (&rn)[R]) {
             const uint32_t nr = (rr + 1) % kPbGroup;
             if (nr == 0) {  // wave-uniform
                 Bc = Bn;
@@ -743,7 +754,6 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                 load_be8(tg + (kPbGroup + 1) * kStep, Bn, En);
             }
             const uint32_t b1 = __shfl(Bc, nr * kPbGroup + k, 64), e1 = __shfl(Ec, nr * kPbGroup + k, 64);
-            uint4 rn[R];
             load_recs(tg + kStep, b1, e1, rn);
             // the (up to) 4R records of this lane: piece c starts at record
             // lo_c = s0 + c*32 + qq*4; bit j of vm: record j in [bc, ec)
@@ -759,13 +769,14 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
             // bit 4c + j: record lo0 + 32c + j lies in [bc, ec).  Only piece 0
             // can start before bc (s0 = bc & ~31), so the lower bound masks
             // piece 0 alone; the upper bound clamps every piece.
+            // (v_bfm: ((1 << width) - 1) << offset in one VALU)
             auto clamp4 = [](int32_t v) { return uint32_t(v < 0 ? 0 : (v > 4 ? 4 : v)); };
             const uint32_t lo0 = s0 + qq * 4;
             const int32_t dh = int32_t(ec) - int32_t(lo0);
             uint32_t vm = 0;
 #pragma unroll
-            for (uint32_t c = 0; c < R; c++) vm |= ((1u << clamp4(dh - int32_t(32 * c))) - 1u) << (4 * c);
-            vm &= ~((1u << clamp4(int32_t(bc) - int32_t(lo0))) - 1u);
+            for (uint32_t c = 0; c < R; c++) vm |= part_bfm(clamp4(dh - int32_t(32 * c)), 4 * c);
+            vm &= ~part_bfm(clamp4(int32_t(bc) - int32_t(lo0)), 0);
             // bit set in the image: its 32-bit word, bit (offset & 31); with
             // slice pairs the record's parity bit selects the image half
             const uint32_t *img32 = reinterpret_cast<const uint32_t *>(img);
@@ -866,10 +877,17 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                                                              tbase + ((rr >> (FL ? 20 : kPSliceLog)) & tmask), 0, 0);
                 }
             }
-#pragma unroll
-            for (uint32_t c = 0; c < R; c++) r[c] = rn[c];
             bc = b1;
             ec = e1;
+            tg += kStep;
+            rr++;
+        };
+        uint4 ra[R], rb[R];
+        load_recs(tg, bc, ec, ra);
+        while (tg < tb) {
+            round(ra, rb);
+            if (tg >= tb) break;  // wave-uniform
+            round(rb, ra);
         }
     }
     PB_STAMP(1);
