@@ -296,6 +296,7 @@ class SwipeExchange:
         self.engine = engine
         backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
         self.device_collectives = backend == "nccl"
+        self.solo = world == 1  # one rank (no process group needed): the exchange is local
         # swipes_async: sink_slots[r] = a local slot rank r keeps for no key
         # (it absorbs the padding rows' PFADDs); slack = capacity over an
         # even share, adapted by settle() to the largest share it has seen
@@ -327,7 +328,7 @@ class SwipeExchange:
         return dest, local
 
     def _a2a(self, out, inp, out_splits, in_splits):
-        if self.world == 1:  # one rank (no process group): everything is local
+        if self.solo:  # one rank (no process group): everything is local
             out.copy_(inp)
             return out
         if self.device_collectives or inp.device.type == "cpu":
@@ -478,7 +479,7 @@ class SwipeExchange:
             if p["n"]:
                 share = max(share, float(c.max(initial=0)) * self.world / p["n"])
         v = torch.tensor(flags + [int(share * 1e6)], dtype=torch.int64)
-        if self.world > 1:
+        if not self.solo:
             if self.device_collectives:
                 v = v.to(pend[0]["ans"].device)
             self.dist.all_reduce(v, op=self.dist.ReduceOp.MAX, group=self.group)

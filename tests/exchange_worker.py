@@ -41,7 +41,12 @@ def main(out_dir, mode="exact"):
     from rtsas_amd.engine import SketchEngine
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo")
+    # WORKER_BACKEND=nccl: RCCL with every rank on this box's one GPU (the
+    # device collectives of a multi-GPU node, rehearsed); default gloo
+    if os.environ.get("WORKER_BACKEND", "gloo") == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo")
     w = workload()
     eng = SketchEngine(0)
     eng.reserve(0, w.bf_error, w.bf_capacity)
@@ -64,6 +69,9 @@ def main(out_dir, mode="exact"):
     k1 = engine_k1(eng)
     ex = SwipeExchange(rank, world, k1, km, engine=eng, sink_slots=sinks,
                        slack=-0.6 if mode == "async_overflow" else world - 1.0)
+    force = os.environ.get("WORKER_FORCE_COLLECTIVES") == "1"  # world 1: collectives still called
+    if force:
+        ex.solo = False
     if mode == "exact":
         ans = ex.swipes(ids, slots)
     else:
@@ -76,6 +84,8 @@ def main(out_dir, mode="exact"):
     torch.cuda.synchronize()
     eng.sync()
     sk = ShardedSketch(client, rank, world)
+    if force:
+        sk.solo = False
     union = sk.pfcount_union(nm)
     each = sk.pfcount_each(nm)
     roll = sk.rollup(groups(nm))

@@ -35,9 +35,14 @@ def main():
     out = sys.argv[1]
     pkg = ge.load_package()
     from rtsas_amd.distributed import ShardedSketch, route
-    dist.init_process_group("gloo")
-    rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
+    # WORKER_BACKEND=nccl: RCCL with every rank on this box's one GPU (the
+    # device collectives of a multi-GPU node, rehearsed); default gloo
+    if os.environ.get("WORKER_BACKEND", "gloo") == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
     members, ids, keys, groups = workload()
     client = pkg.SketchClient(decode_responses=True, device=0)
     client.execute_command("BF.RESERVE", "bf:students", 0.01, 20000)
@@ -46,6 +51,8 @@ def main():
     buf, offs = pkg.pack_ints(ids[mine])
     client.swipes("bf:students", [keys[i] for i in mine], packed=(buf, offs))
     sk = ShardedSketch(client, rank, world)
+    if os.environ.get("WORKER_FORCE_COLLECTIVES") == "1":
+        sk.solo = False  # world 1: the collectives are still called
     all_keys = sorted(set(keys))
     union = sk.pfcount_union(all_keys)
     roll = sk.rollup(groups)

@@ -18,20 +18,26 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("world,mode", [(2, "exact"), (3, "exact"), (2, "async"), (3, "async"),
-                                        (2, "async_overflow")])
-def test_exchange_on_device_equals_oracle(orc, engine, tmp_path, world, mode):
+@pytest.mark.parametrize("world,mode,backend", [(2, "exact", "gloo"), (3, "exact", "gloo"), (2, "async", "gloo"),
+                                                (3, "async", "gloo"), (2, "async_overflow", "gloo"),
+                                                (1, "exact", "nccl"), (1, "async", "nccl")])
+def test_exchange_on_device_equals_oracle(orc, engine, tmp_path, world, mode, backend):
     """mode exact: SwipeExchange.swipes (the host reads the routing counts);
     async: swipes_async over two batches (ske_route_swipes_cap_async, equal
     splits of a capacity that cannot overflow, padding into each rank's sink
     slot) then settle(); async_overflow: a capacity below the owners' shares,
-    so settle() re-runs both batches with exact splits."""
+    so settle() re-runs both batches with exact splits.  backend nccl: RCCL
+    (one GPU holds one RCCL rank: world 1, with the collectives forced on --
+    the device all_to_all_single / all_reduce / reduce_scatter_tensor /
+    all_gather calls of a multi-GPU node, on their RCCL code path)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from exchange_worker import NK, groups, names, workload
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", WORKER_BACKEND=backend,
+               WORKER_FORCE_COLLECTIVES="1" if backend == "nccl" else "0")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
-                        "--master-port", str(29650 + world), os.path.join(ROOT, "tests", "exchange_worker.py"),
+                        "--master-port", str(29650 + world + (10 if backend == "nccl" else 0)),
+                        os.path.join(ROOT, "tests", "exchange_worker.py"),
                         str(tmp_path), mode], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[:4000] + r.stderr[-1500:]
     w = workload()

@@ -15,15 +15,20 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_queries_equal_one_shard(orc, tmp_path, world):
+@pytest.mark.parametrize("world,backend", [(2, "gloo"), (4, "gloo"), (1, "nccl")])
+def test_sharded_queries_equal_one_shard(orc, tmp_path, world, backend):
+    """backend nccl: RCCL, one rank on the box's one GPU with the collectives
+    forced on (reduce_scatter_tensor / all_reduce / all_gather on their RCCL
+    code path; a second RCCL rank on the same GPU is refused: "Duplicate GPU")."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from sharded_worker import workload
     out = str(tmp_path / "res.npz")
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", WORKER_BACKEND=backend,
+               WORKER_FORCE_COLLECTIVES="1" if backend == "nccl" else "0")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
-                        "--master-port", str(29600 + world), os.path.join(ROOT, "tests", "sharded_worker.py"),
+                        "--master-port", str(29600 + world + (10 if backend == "nccl" else 0)),
+                        os.path.join(ROOT, "tests", "sharded_worker.py"),
                         out], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     res = np.load(out)
