@@ -191,7 +191,9 @@ __device__ __forceinline__ void part_id_load(const __amdgpu_buffer_rsrc_t &rb, u
     const uint32_t s8 = b & 7;
     const bool sh = d.len && d.len <= 8;
     const uint32_t o0 = sh ? (b & ~7u) : 0xfffffff8u;
-    const uint32_t o1 = (sh && s8 + d.len > 8) ? o0 + 8 : o0;
+    // (an id inside one aligned word needs no second word: its load goes
+    // past the range, no memory access; the hash masks those bytes off)
+    const uint32_t o1 = (sh && s8 + d.len > 8) ? o0 + 8 : 0xfffffff8u;
     d.w0 = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rb, o0, 0, nt_aux<2>()));
     d.w1 = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rb, o1, 0, nt_aux<2>()));
 }
@@ -418,10 +420,10 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
     auto offsets = [&](uint32_t t, uint32_t u, uint32_t &b, uint32_t &e) {
         const uint32_t i = t * kTile + u * kT + tid;
         const uint32_t ic = i < A.n ? i : A.n - 1;
-        const uint32_t lb = __builtin_amdgcn_raw_buffer_load_b32(roffs, ic * 4, 0, nt_aux<2>());
-        const uint32_t le = __builtin_amdgcn_raw_buffer_load_b32(roffs, ic * 4 + 4, 0, nt_aux<2>());
-        b = A.offs ? lb : ic * A.fixed_w;
-        e = A.offs ? le : b + A.fixed_w;
+        // the swipe's two offsets in one 8-B load
+        const uint2 lbe = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(roffs, ic * 4, 0, nt_aux<2>()));
+        b = A.offs ? lbe.x : ic * A.fixed_w;
+        e = A.offs ? lbe.y : b + A.fixed_w;
     };
     uint32_t gt0, gt1;
     part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
