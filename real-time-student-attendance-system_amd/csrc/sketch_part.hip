@@ -380,6 +380,9 @@ __global__ void __launch_bounds__(kPaBlock, KM <= 11 ? 8 : 4) k_part_a(const Par
 // whose records land past the copy-out.  kCnt: 1024 (two counters per
 // thread) for chains of < 512 pairs (C3/C5: 152), else 2048.
 constexpr uint32_t kOORa = 0x80000000u;  // a buffer offset past every range: load 0, store dropped
+#ifndef SKE_PA_WAIT_LAST
+#define SKE_PA_WAIT_LAST 1  // round 4 A/B: pass A 0.226-0.230 -> 0.225 ms
+#endif
 template <int KM, uint32_t kCnt>
 __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two blocks per CU
     constexpr uint32_t kT = 512;
@@ -492,7 +495,10 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
                     if (q + 1 < KM) wk.step(L.d);
                 }
             }
-            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this swipe's atomics, once
+            // lgkmcnt(0): this swipe's atomics, once (SKE_PA_WAIT_LAST: only
+            // after the last swipe, so the first one's atomics overlap the
+            // second one's hash)
+            if (!SKE_PA_WAIT_LAST || u + 1 == kU) __builtin_amdgcn_s_waitcnt(0xc07f);
         }
         lds_barrier();
 #pragma unroll
