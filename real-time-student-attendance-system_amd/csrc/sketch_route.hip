@@ -16,8 +16,9 @@
 //   k_route_scan    exclusive scan over (owner, block), owner major -> base[o][b]
 //                   (and the per-owner totals)
 //   k_route_scatter per block: the same swipes, a rank within (owner, block)
-//                   from LDS atomics, position = base[o][b] + rank; ids and
-//                   local slots scattered there, pos[i] recorded
+//                   from one LDS atomic per (wave, owner), position =
+//                   base[o][b] + rank; ids and local slots scattered there,
+//                   pos[i] recorded
 //   k_route_return  out[i] = answers[pos[i]]
 //
 // The capacity form (no host synchronisation) takes one packed route word per
@@ -26,8 +27,11 @@
 //
 // The order inside an (owner, block) segment is whatever the LDS atomics
 // give -- immaterial: every swipe keeps its position, and the registers are
-// a max.  Streams of bytes, HBM bound: per swipe the id, the slot, the
-// scattered id and slot, the position (2w + 12 B), and 1 + 4 + 1 B to return.
+// a max.  Streams of bytes: per swipe the id, the slot, the scattered id and
+// slot, the position (2w + 12 B), and 1 + 4 + 1 B to return; the capacity
+// form's count adds one gather from the route table (the L2's random rate:
+// 60 us of its 0.17 ms per 16M swipes at N = 1) and writes the word, its
+// scatter reads it back.
 #include "sketch_common.h"
 #include "sketch_internal.h"
 
