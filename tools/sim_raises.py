@@ -78,6 +78,13 @@ def main():
         idx, rank = hll_idx_rank(ids, synthetic.id_width(w))
         flat = slot * 16384 + idx
         old = regs[flat]
+        # exact no-op filters from summaries taken at the step's start: the
+        # key's minimum register, and its 128-register line's minimum (an
+        # update with rank <= the minimum cannot raise anything)
+        kmin = regs.reshape(w.n_keys, 16384).min(axis=1)
+        lmin = regs.reshape(w.n_keys * 128, 128).min(axis=1)
+        skip_key = rank <= kmin[slot]
+        skip_line = rank <= lmin[flat // 128]
         up = rank > old
         lect = slot // days
         cls = np.where(lect == 0, 0, np.where(lect < 10, 1, 2))
@@ -94,6 +101,7 @@ def main():
         lines = np.unique(keys[rose] // 128)
         lcls = np.where(lines * 128 // 16384 // days == 0, 0, np.where(lines * 128 // 16384 // days < 10, 1, 2))
         row = {"step": s, "updates": int(valid.sum()), "raises_vs_start": int(up.sum()),
+               "skippable_key_min": int(skip_key.sum()), "skippable_line_min": int(skip_line.sum()),
                "distinct_raised": int(rose.sum()), "distinct_lines": int(lines.size),
                "by_class": {name: {"updates": int((cls == c).sum()), "raises_vs_start": int((up & (cls == c)).sum()),
                                    "distinct_raised": int((rose & (kcls == c)).sum()),
