@@ -58,7 +58,16 @@ namespace ske {
 
 constexpr uint32_t kPaBlock = 1024;
 constexpr uint32_t kPbBlock = 1024;
-constexpr uint32_t kPcBlock = 256;
+// pass C's block: 1024 threads x 1 swipe per tile (round 4 A/B, three
+// alternations: 0.406-0.407 ms at 256 x 4, 0.402 at 512 x 2, 0.400 at 1024 x 1)
+#ifndef SKE_PC_BLOCK
+#define SKE_PC_BLOCK 1024
+#endif
+#ifndef SKE_PC_BLOCKS_PER_CU
+#define SKE_PC_BLOCKS_PER_CU 8
+#endif
+constexpr uint32_t kPcBlock = 256;            // k_part_c (fail bytes)
+constexpr uint32_t kPcFlBlock = SKE_PC_BLOCK;  // k_part_c_fl (fail lists)
 constexpr uint32_t kPSliceMask = kPSliceBits - 1;
 constexpr uint32_t kPSliceBytes = kPSliceBits / 8;  // 64 KiB
 constexpr uint32_t kPSub = 1u << 24;                // swipes per sub-batch (passes A-B-C)
@@ -980,12 +989,12 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
 // slower, 0.409 -> 0.436 ms, round 4: the line traffic, not the CAS count,
 // holds this pass.)
 template <int U>
-__global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
-    static_assert(kPcBlock * U == 1024, "one 1024-swipe tile per sub-step");
+__global__ void __launch_bounds__(kPcFlBlock) k_part_c_fl(const PartArgs A) {
+    static_assert(kPcFlBlock * U == 1024, "one 1024-swipe tile per sub-step");
     constexpr uint32_t kRun = kPbGroup;  // tiles per block iteration
     __shared__ uint16_t mark[kRun * 1024];
     const uint32_t tid = threadIdx.x;
-    for (uint32_t j = tid; j < kRun * 1024; j += kPcBlock) mark[j] = 0;
+    for (uint32_t j = tid; j < kRun * 1024; j += kPcFlBlock) mark[j] = 0;
     uint32_t gt0, gt1;
     part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
     const uint32_t nblk = gridDim.x / kPGroups;
@@ -997,7 +1006,7 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
     auto load = [&](uint32_t t, uint32_t tend, In &in) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
+            const uint32_t i = t * 1024 + uint32_t(u) * kPcFlBlock + tid;
             const bool act = t < tend && i < A.n;
             in.fb[u] = act ? nt_ld<16>(A.fail + i) : 1u;
             in.sl[u] = act ? nt_ld<16>(A.slot + i) : 0u;
@@ -1011,12 +1020,12 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
         In cur;
         load(r0, r1, cur);
         // the run's lists: piece p = (unit p / kRun, tile r0 + p % kRun)
-        for (uint32_t p0 = 0; p0 < npieces; p0 += 4 * kPcBlock) {
+        for (uint32_t p0 = 0; p0 < npieces; p0 += 4 * kPcFlBlock) {
             part_u32x4 e[4];
             bool ok[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const uint32_t p = p0 + uint32_t(j) * kPcBlock + tid;
+                const uint32_t p = p0 + uint32_t(j) * kPcFlBlock + tid;
                 const uint32_t un = p / kRun, tt = r0 + p % kRun;
                 ok[j] = p < npieces && tt < r1;
                 e[j] = __builtin_bit_cast(part_u32x4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -1024,7 +1033,7 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const uint32_t base = ((p0 + uint32_t(j) * kPcBlock + tid) % kRun) * 1024;
+                const uint32_t base = ((p0 + uint32_t(j) * kPcFlBlock + tid) % kRun) * 1024;
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
                     const uint32_t lo = e[j][c] & 0xffffu, hi = e[j][c] >> 16;
@@ -1043,8 +1052,8 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
             uint32_t rank[U], sh[U], cw[U], seen[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
-                valid[u] = i < A.n && cur.fb[u] == 0 && mk[uint32_t(u) * kPcBlock + tid] != ep;
+                const uint32_t i = t * 1024 + uint32_t(u) * kPcFlBlock + tid;
+                valid[u] = i < A.n && cur.fb[u] == 0 && mk[uint32_t(u) * kPcFlBlock + tid] != ep;
                 w[u] = nullptr;
                 rank[u] = sh[u] = 0;
                 if (valid[u]) {
@@ -1072,7 +1081,7 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c_fl(const PartArgs A) {
             if (A.out) {
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    const uint32_t i = t * 1024 + uint32_t(u) * kPcBlock + tid;
+                    const uint32_t i = t * 1024 + uint32_t(u) * kPcFlBlock + tid;
                     if (i < A.n) nt_st<16>(A.out + i, uint8_t(valid[u]));
                 }
             }
@@ -1237,8 +1246,9 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             if (hook) hook(hook_user, 2, 0, st);
             if (flist) {
                 const unsigned gc =
-                    (part_grid(ms, 1024 * kPbGroup, unsigned(cus) * 8) + kPGroups - 1) / kPGroups * kPGroups;
-                hipLaunchKernelGGL(k_part_c_fl<4>, dim3(gc), dim3(kPcBlock), 0, st, A);
+                    (part_grid(ms, 1024 * kPbGroup, unsigned(cus) * SKE_PC_BLOCKS_PER_CU) + kPGroups - 1) /
+                    kPGroups * kPGroups;
+                hipLaunchKernelGGL(k_part_c_fl<1024 / kPcFlBlock>, dim3(gc), dim3(kPcFlBlock), 0, st, A);
             } else {
                 const unsigned gc = (part_grid(ms, kPcBlock * 2, unsigned(cus) * 8) + kPGroups - 1) / kPGroups * kPGroups;
                 hipLaunchKernelGGL(k_part_c<2>, dim3(gc), dim3(kPcBlock), 0, st, A);
