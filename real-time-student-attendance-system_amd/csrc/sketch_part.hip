@@ -987,7 +987,8 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
 // (A two-phase form -- the answers and the rank-1 raises as plain byte
 // stores first, the rank >= 2 raises by CAS in a second kernel -- measured
 // slower, 0.409 -> 0.436 ms, round 4: the line traffic, not the CAS count,
-// holds this pass.)
+// holds this pass.)  U swipes per thread per tile, kPcFlBlock * U = 1024
+// (1024 x 1 since round 4; see SKE_PC_BLOCK).
 template <int U>
 __global__ void __launch_bounds__(kPcFlBlock) k_part_c_fl(const PartArgs A) {
     static_assert(kPcFlBlock * U == 1024, "one 1024-swipe tile per sub-step");
