@@ -76,7 +76,7 @@ def test_route_cap_layout(engine, slack, world):
     swipe of that owner), counts are the owners' counts -- also with
     capacities below the owners' shares (slack < 0)."""
     import torch
-    from rtsas_amd.distributed import KeyMap, SwipeExchange
+    from rtsas_amd.distributed import NO_SLOT, KeyMap, SwipeExchange
     names = [f"hll:unique:L{k:03d}:2025-01-01" for k in range(37)]
     km = KeyMap(names, world)
     sinks = [km.slots_end(r) for r in range(world)]
@@ -85,13 +85,17 @@ def test_route_cap_layout(engine, slack, world):
     cap = ex.capacity(200_000)
     for n in (200_000, 199_000, 1):
         idn = rng.integers(48, 58, (n, 8), dtype=np.uint8)
-        gk = rng.integers(0, 37, n)
+        # global keys -1 and 37..39 are outside the universe: rank 0, slot NO_SLOT
+        gk = rng.integers(-1, 40, n)
         send_ids, send_slots, pos, counts = ex._route_cap_native(torch.from_numpy(idn).cuda(),
                                                                  torch.from_numpy(gk).cuda(), cap)
         torch.cuda.synchronize()
         sid, ssl = send_ids.cpu().numpy(), send_slots.cpu().numpy().view(np.uint32)
         ps, ct = pos.cpu().numpy()[:n].astype(np.int64), counts.cpu().numpy()
-        own = km.owner[gk].astype(np.int64)
+        known = (gk >= 0) & (gk < 37)
+        gc = np.where(known, gk, 0)
+        own = np.where(known, km.owner[gc], 0).astype(np.int64)
+        loc = np.where(known, km.local[gc], NO_SLOT).astype(np.uint32)
         assert ct.tolist() == np.bincount(own, minlength=world).tolist()
         assert ((ps // cap) == own).all()
         for o in range(world):
@@ -105,7 +109,7 @@ def test_route_cap_layout(engine, slack, world):
         def key(row, slot, id64):
             return (row.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)) ^ (slot.astype(np.uint64) << np.uint64(40)) \
                 ^ id64
-        want = key(ps, km.local[gk], idn.view(np.uint64).ravel())
+        want = key(ps, loc, idn.view(np.uint64).ravel())
         rr = np.unique(ps)
         have = key(rr, ssl[rr], sid.view(np.uint64).ravel()[rr])
         assert np.isin(have, want).all()
