@@ -174,6 +174,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t part_rsrc(const void *p, uint3
 // two alternations): records nt: pass B 0.276 -> 0.260 ms; + bits 1|2|4:
 // 0.25 ms; bits 8 and 16 neutral to slightly slower; bit 32 makes pass C
 // 0.39 -> 0.59 ms (the raising CAS no longer finds its line near).  Default 7.
+// (Round 4, final kernels: 15 and 23 within 0.1 % of 7, profiles/r04_ab_nt.txt.)
 #ifndef SKE_NT
 #define SKE_NT 7
 #endif
