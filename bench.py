@@ -122,7 +122,16 @@ def parse(argv=None):
                          "config's step swipes, each rank's batch the probability mass of the keys "
                          "it owns (the fixed 1B-event stream of north_star, cut per step); "
                          "equal = every rank the config's step swipes over its own keys")
-    return ap.parse_args(argv)
+    ap.add_argument("--shard", type=int, default=0,
+                    help="N > 0: run ONE rank's share of an N-rank job on this GPU (its owned keys and, "
+                         "with --shares mass, its batch), to measure the per-GPU work of the N-GPU "
+                         "configuration on one GPU; no collective (the line keeps n_gpus 1)")
+    ap.add_argument("--shard-rank", type=int, default=-1,
+                    help="with --shard: the rank simulated (-1 = the one owning the most key mass)")
+    a = ap.parse_args(argv)
+    if a.shard and a.exchange:
+        ap.error("--shard simulates owner-routed input only")
+    return a
 
 
 def free_port():
@@ -389,6 +398,17 @@ def load_pmc(config, kernel):
     return None, None
 
 
+class _ShardView:
+    """The slot layout of one simulated rank (--shard) as verify() sees it:
+    a one-rank map whose workload slots end where the shard's do."""
+
+    def __init__(self, end):
+        self.end = end
+
+    def slots_end(self, r):
+        return self.end
+
+
 class Run:
     """One workload on one context: setup, timed steps, instrumented replay."""
 
@@ -403,9 +423,18 @@ class Run:
         self.w_all = w_all
         # the job's key universe and its one ownership rule (distributed.KeyMap)
         self.names = synthetic.key_names(w_all)
-        self.km = KeyMap(self.names, world)
-        mine = self.km.keys_of(rank)
         probs = synthetic.key_probs(w_all)
+        # --shard N: this process plays one rank (kr) of an N-rank job (kw)
+        kw = args.shard if args.shard else world
+        self.km = KeyMap(self.names, kw)
+        if args.shard:
+            masses = [float(probs[self.km.keys_of(r)].sum()) if probs is not None
+                      else self.km.keys_of(r).size / len(self.names) for r in range(kw)]
+            kr = args.shard_rank if args.shard_rank >= 0 else int(max(range(kw), key=lambda r: masses[r]))
+        else:
+            kr = rank
+        self.kw, self.kr = kw, kr
+        mine = self.km.keys_of(kr)
         if args.exchange:
             # unpartitioned input: the stream spans every key (global indices);
             # this rank's slab holds the keys it owns
@@ -422,7 +451,7 @@ class Run:
         # the probability mass of this rank's keys in the global stream
         self.mass = float(probs[mine].sum()) if probs is not None else mine.size / len(self.names)
         self.shares = "equal" if args.exchange else args.shares
-        self.n = n = rank_swipes(args.batch or w.step_swipes, self.mass, world, self.shares)
+        self.n = n = rank_swipes(args.batch or w.step_swipes, self.mass, kw, self.shares)
         self.engine = engine = SketchEngine(local)
         self.stream = stream = torch.cuda.Stream()  # shared by libsketch and torch
         torch.cuda.set_stream(stream)
@@ -441,12 +470,17 @@ class Run:
         t0 = time.perf_counter()
         engine.preload(0, p, w.n_members)
         self.preload_s = time.perf_counter() - t0
-        self.nslots = self.km.slots_end(rank)
+        self.nslots = self.km.slots_end(kr)
         # past the workload's keys: the verification universes (verify(), up
         # to 2 x VERIFY_KEYS slots), then the exchange's sink slot (padding
         # rows of SwipeExchange.swipes_async; no key lives there)
-        self.sinks = [self.km.slots_end(r) + 2 * VERIFY_KEYS for r in range(world)]
-        engine.hll_reserve(self.sinks[rank] + 1)
+        self.sinks = [self.km.slots_end(r) + 2 * VERIFY_KEYS for r in range(kw)]
+        engine.hll_reserve(self.sinks[kr] + 1)
+        if args.shard:  # verify() runs as one rank above this shard's slots
+            self.sinks = [self.sinks[kr]]
+            self.km_verify = _ShardView(self.km.slots_end(kr))
+        else:
+            self.km_verify = self.km
         self.variant = variant = engine.variant(0)
         self.lds_k1 = lds_k1 = variant == 1
         self.persistent = bool(args.persistent if args.persistent >= 0 else lds_k1) and not args.exchange
@@ -695,7 +729,10 @@ class Run:
 
     def config(self):
         a, w = self.args, self.w
-        return {"workload": w.name, "swipes_per_step": self.n, "students": w.n_members,
+        shard = ({"shard_of": self.kw, "shard_rank": self.kr,
+                  "what": "one rank's share of the %d-GPU job, run alone on this GPU" % self.kw}
+                 if a.shard else {})
+        return {"workload": w.name, **shard, "swipes_per_step": self.n, "students": w.n_members,
                 "hll_keys_total": self.w_all.n_keys, "hll_keys_this_gpu": w.n_keys,
                 "key_ownership": "MurmurHash64A(key name, 0) mod world (distributed.KeyMap)",
                 "invalid_frac": w.invalid_frac,
@@ -829,13 +866,15 @@ def main():
     }
     line["config"]["swipes_per_step_all_ranks"] = total_swipes
     if run.ex is not None:
-        line["exchange"] = {**run.ex.stats, "slack": run.ex.slack, "capacity_rows_per_peer": run.ex.capacity(run.n)}
+        # cap_rows_per_peer / slack_used: what the timed steps were enqueued
+        # with; slack_next: what settle() adapted it to for later batches
+        line["exchange"] = {**run.ex.stats, "slack_next": run.ex.slack}
     want_cpu = rank == 0 and world == 1 and not args.no_cpu and args.cpu_seconds > 0
     if not args.no_check or want_cpu:
         orc = ge.load_oracle()
         chain = oracle_chain(run.engine, orc, run.w, run.p)
         if not args.no_check:
-            chk = checked(verify, run.engine, orc, chain, run.w, run.km, rank, world, dist, dev,
+            chk = checked(verify, run.engine, orc, chain, run.w, run.km_verify, rank, world, dist, dev,
                           bool(args.exchange), run.sinks)
             if world > 1 and not args.exchange and getattr(verify, "last_map", None) is not None:
                 # the unpartitioned-input path too (SwipeExchange: alltoallv over
@@ -846,7 +885,7 @@ def main():
             line["check"] = chk
         if want_cpu:
             line["cpu_baseline"] = cpu_baseline(orc, chain, run.w, run.batches[0], args.cpu_seconds,
-                                                lambda s: run.names[int(run.km.keys_of(0)[s])])
+                                                lambda s: run.names[int(run.km.keys_of(run.kr)[s])])
     run.free()
     sec = args.secondary
     if sec == "auto":

@@ -1347,6 +1347,10 @@ int ske_route_swipes(ske_ctx *c, const uint8_t *ids, uint32_t width, const uint3
     uint32_t *hist = (uint32_t *)scratch_get(c->scratch, 40, route_hist_words(n, world) * 4 + 4, &e);
     uint32_t *tot = e == hipSuccess ? (uint32_t *)scratch_get(c->scratch, 41, size_t(world) * 4, &e) : nullptr;
     if (e != hipSuccess) return scratch_error(c, e);
+    unsigned long long cid = 0;
+    const int rc = scratch_user_begin(c, &cid);  // an async routing call on another stream finishes first
+    if (rc) return rc;
+    scratch_user_end(c, cid);
     HIPCHK(c, launch_route(ids, width, gkey, n, world, key_owner, key_local, nkeys, send_ids, send_slots, pos,
                            hist, tot, c->st));
     uint32_t h[64];
@@ -1368,9 +1372,19 @@ int ske_route_swipes_cap_async(ske_ctx *c, const uint8_t *ids, uint32_t width, c
     hipError_t e = hipSuccess;
     uint32_t *hist = (uint32_t *)scratch_get(c->scratch, 40, route_hist_words(n, world) * 4 + 4, &e);
     if (e != hipSuccess) return scratch_error(c, e);
-    HIPCHK(c, launch_route_cap(ids, width, gkey, n, world, key_route, nkeys, cap, sink_slots, send_ids, send_slots,
-                               pos, hist, counts, c->cus, c->st));
-    return SKE_OK;
+    // the histogram is context scratch (slot 40): a routing call on another
+    // stream waits for this one's kernels (scratch_user_begin/end)
+    unsigned long long cid = 0;
+    const int rc = scratch_user_begin(c, &cid);
+    if (rc) return rc;
+    const hipError_t le = launch_route_cap(ids, width, gkey, n, world, key_route, nkeys, cap, sink_slots, send_ids,
+                                           send_slots, pos, hist, counts, c->cus, c->st);
+    if (le != hipSuccess) {
+        c->last_hip = std::string("launch_route_cap: ") + hipGetErrorString(le);
+        scratch_user_end(c, cid);
+        return SKE_EHIP;
+    }
+    return scratch_user_end(c, cid);
 }
 
 int ske_route_return_async(ske_ctx *c, const uint8_t *answers, const uint32_t *pos, uint64_t n, uint8_t *out) {

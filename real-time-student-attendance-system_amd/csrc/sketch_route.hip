@@ -201,11 +201,18 @@ __global__ void __launch_bounds__(kRtBlock) k_route_scatter(const RouteArgs R) {
 // The capacity form's count: one gather per swipe of its key's packed route
 // word, kept in pos[i] for the scatter (which then gathers nothing: every
 // access of k_route_scatter_cap is a coalesced stream).
+// ~0 is "no owner" at every world size (at world 64 its owner field would
+// read 63): such keys go to rank 0 with kNoSlot, as the torch path's
+// owner_local; KeyMap.route_words keeps local slots below 2^26 - 1, so no
+// real key packs to ~0
+__device__ __forceinline__ bool route_word_owned(const RouteArgs &R, uint32_t kr) {
+    return kr != 0xffffffffu && (kr >> 26) < R.world;
+}
 __device__ __forceinline__ uint32_t route_word_owner(const RouteArgs &R, uint32_t kr) {
-    return (kr >> 26) < R.world ? kr >> 26 : 0u;  // ~0 (no owner) -> rank 0
+    return route_word_owned(R, kr) ? kr >> 26 : 0u;
 }
 __device__ __forceinline__ uint32_t route_word_slot(const RouteArgs &R, uint32_t kr) {
-    return (kr >> 26) < R.world ? kr & 0x3ffffffu : kNoSlot;
+    return route_word_owned(R, kr) ? kr & 0x3ffffffu : kNoSlot;
 }
 
 __global__ void __launch_bounds__(kRtBlock) k_route_count_cap(const RouteArgs R) {

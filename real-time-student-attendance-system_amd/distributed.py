@@ -119,10 +119,10 @@ class KeyMap:
 
     def route_words(self) -> np.ndarray:
         """uint32 owner << 26 | local slot per key (ske_route_swipes_cap_async's
-        key_route; local slots < 2^26)."""
+        key_route; local slots < 2^26 - 1, so no key packs to the no-owner word ~0)."""
         own = self.owner.astype(np.uint64)
         loc = self.local.astype(np.uint64)
-        assert loc.size == 0 or int(loc.max()) < (1 << 26)
+        assert loc.size == 0 or int(loc.max()) < (1 << 26) - 1  # ~0 stays the no-owner word
         return ((own << np.uint64(26)) | loc).astype(np.uint32)
 
     def route_table(self, device):
@@ -397,7 +397,7 @@ class SwipeExchange:
         return ans
 
     # ---- host-free form: equal splits of `cap` rows per peer
-    def swipes_async(self, ids, gkeys, n_max: int | None = None):
+    def swipes_async(self, ids, gkeys, n_max: int | None = None, inputs_stable: bool = True):
         """``swipes`` with no host synchronisation (enqueue only on a device).
 
         Every peer pair exchanges exactly ``cap = capacity(n_max)`` rows
@@ -409,7 +409,15 @@ class SwipeExchange:
         final after ``settle()``, which every rank calls at the same point:
         a batch in which some owner got more than cap swipes on any rank is
         then run again through ``swipes`` (exact splits; PFADD is idempotent
-        and its answers are rewritten)."""
+        and its answers are rewritten).
+
+        That re-run reads ``ids`` and ``gkeys`` again: they must hold the
+        same swipes until ``settle()`` returns.  A caller that refills its
+        input buffers sooner (a ring buffer) passes ``inputs_stable=False``,
+        and the batch is kept as a device copy (one more read + write of
+        its ids and keys) instead of by reference."""
+        if not inputs_stable:
+            ids, gkeys = ids.clone(), gkeys.clone()
         with self._on_stream(ids) as caller:
             ans = self._swipes_async(ids, gkeys, n_max)
             if caller is not None:
@@ -429,6 +437,10 @@ class SwipeExchange:
         else:
             send_ids, send_slots, pos, counts = self._route_cap_torch(ids, gkeys, cap)
         rows = self.world * cap
+        # the capacity and slack these rows were sized with (settle() may
+        # adapt the slack for the next batches)
+        self.stats["cap_rows_per_peer"] = cap
+        self.stats["slack_used"] = self.slack
         if self.world == 1:
             # one rank: the exchange is the identity, K1 reads the send rows
             # in place (their storage has the 16 readable bytes K1 wants)

@@ -148,10 +148,18 @@ class AttendanceProcessor:
         if callable(index):  # SketchClient: the key table's stem index
             keys = index(stem)
         else:  # any redis-py-like client: SCAN for exactly <stem>:YYYY-MM-DD
-            pat = "".join("[" + ch + "]" if ch in "*?[]\\^" else ch for ch in stem)
+            pat = glob_escape(stem)
             keys = list(self.redis_client.scan_iter(match=pat + ":" + "[0-9]" * 4 + "-" + "[0-9]" * 2 + "-" +
                                                      "[0-9]" * 2, _type="string"))
         return {"unique_attendees": self.redis_client.pfcount(*keys) if keys else 0}
+
+
+def glob_escape(text: str) -> str:
+    """`text` as a Redis MATCH pattern that matches exactly it: every glob
+    special byte backslash-escaped (redis src/util.c stringmatchlen reads
+    ``\\x`` as a literal x outside a class; a bracket class would not do:
+    ``[^]`` is an empty negated class, ``[]]`` and ``[\\]`` misparse)."""
+    return "".join("\\" + ch if ch in "*?[]\\^" else ch for ch in text)
 
 
 def rank_top_bottom(counts: np.ndarray, keys: Sequence[str], k: int) -> tuple[list, list]:

@@ -66,3 +66,18 @@ def test_redis_glob_dialect(pkg):
     assert g(b"hll:unique:L1:????-??-??", b"hll:unique:L1:2025-03-19")
     assert not g(b"hll:unique:L1:????-??-??", b"hll:unique:L1:x:2025-03-19")
     assert not g(b"*", b"")  # stringmatchlen itself; SCAN / KEYS bypass a bare '*'
+
+
+def test_glob_escape_stems(pkg):
+    """processor.glob_escape (the SCAN fallback of get_attendance_stats):
+    a lecture stem holding glob specials matches exactly its own day keys."""
+    from rtsas_amd.client import redis_glob as g
+    from rtsas_amd.processor import glob_escape
+    day = ":" + "[0-9]" * 4 + "-" + "[0-9]" * 2 + "-" + "[0-9]" * 2
+    for stem in ["hll:unique:A^B", "hll:unique:a]b", "hll:unique:a\\b", "hll:unique:[x]*?", "hll:unique:^",
+                 "hll:unique:]", "hll:unique:\\", "hll:unique:plain"]:
+        pat = (glob_escape(stem) + day).encode()
+        assert g(pat, (stem + ":2025-03-19").encode()), stem
+        assert not g(pat, (stem + "x:2025-03-19").encode()), stem
+        assert not g(pat, (stem[:-1] + "Q:2025-03-19").encode()), stem
+        assert not g(pat, (stem + ":2025-03-19:x").encode()), stem
