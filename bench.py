@@ -52,6 +52,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_MEASURED_GBS = 6290.0  # MI355X_MICROARCH.md: measured streaming read rate
 # tools/randbench.hip on MI355X (profiles/r02_randbench.json): one random
 # 4-byte read per lane over a 1.6 GB table -- 55 G sectors/s; the register
 # update of pass C is priced against it as well as against the HBM peak
@@ -63,8 +64,8 @@ RANDOM_SECTOR_GPS = 55.3
 RANDOM_CAS_GPS = 21.1
 MALL_BYTES = 256 << 20  # Infinity Cache: a slab this small stays on chip
 METRIC = "swipes/sec (fused BF.EXISTS+PFADD) at 1/2/4/8 GPUs; % of HBM peak"
-PASS_NAMES = ["k1", "k_part_a", "k_part_b", "k_part_c"]
-PMC_ROUNDS = ["r04", "r03", "r02"]  # newest committed PMC summaries first
+PASS_NAMES = ["k1", "k_part_a", "k_part_b", "k_part_c", "k_seg_d", "k_seg_e"]
+PMC_ROUNDS = ["r05", "r04", "r03", "r02"]  # newest committed PMC summaries first
 VERIFY_KEYS = 64
 
 
@@ -359,11 +360,18 @@ def verify(engine, orc, chain, w, km, rank, world, dist, dev, exchange, sinks, p
             "backend": dist.get_backend() if world > 1 else "none"}
 
 
-def pass_bytes(n, nvalid, probes, width, fixed, geometry, lds_k1=False, slab_bytes=0, cus=256):
+def pass_bytes(n, nvalid, probes, width, fixed, geometry, lds_k1=False, slab_bytes=0, cus=256, seg=False,
+               nsub=1):
     """Algorithmic bytes per launch of each K1 kernel: streams
     at their size, every random access at one 64-B HBM sector.  The LDS K1
     (lds_k1) reads the filter once per block (staged into LDS, probes cost no
-    HBM) and its register words only when the slab does not fit on chip."""
+    HBM) and its register words only when the slab does not fit on chip.
+    seg: the segmented PFADD -- pass C writes a 4-B record per valid swipe
+    instead of touching registers; the level-2 sort reads and writes every
+    record once; the window pass reads every record and the slab once and
+    writes the slab back once (its lines that rose, at most the whole slab).
+    Per-launch figures of the per-sub-batch kernels are per sub-batch
+    (nsub sub-batches of n / nsub swipes)."""
     s_off = 0 if fixed else 4
     ksum = sum(k for _, k in geometry)
     nslices = sum(-(-bits // (1 << 19)) for bits, _ in geometry)
@@ -383,8 +391,11 @@ def pass_bytes(n, nvalid, probes, width, fixed, geometry, lds_k1=False, slab_byt
         # probe records + their run boundaries in, the filter staged once
         "k_part_b": rec + 8 * nslices * ntiles + filter_bytes,
         # fail byte, HLL word, slot in, answer out; per valid swipe its register's
-        # sector read + written (SURVEY §8d's 128·v, as the one-kernel K1 above)
-        "k_part_c": n * (len(geometry) + 4 + 4 + 1) + 128 * nvalid,
+        # sector read + written (SURVEY §8d's 128·v, as the one-kernel K1 above),
+        # or (seg) its 4-B record written
+        "k_part_c": n * (len(geometry) + 4 + 4 + 1) + (4 if seg else 128) * nvalid,
+        "k_seg_d": 8 * nvalid,
+        "k_seg_e": 4 * nvalid * nsub + 2 * slab_bytes,
     }
 
 
@@ -640,8 +651,14 @@ class Run:
         """§3's roofline on the kernel that takes the most time."""
         a, n = self.args, self.n
         cus = self.torch.cuda.get_device_properties(self.dev).multi_processor_count
-        alg = pass_bytes(n, self.nvalid, self.probes, self.width, self.fixed, chain_geometry(self.engine),
-                         lds_k1=self.lds_k1, slab_bytes=(self.nslots + VERIFY_KEYS) * 16384, cus=cus)
+        seg = bool(pt) and len(pt) > 5 and pt[5][1] > 0
+        # per launch of the per-sub-batch kernels: one sub-batch (bench batches
+        # are cut into even sub-batches of at most 16M swipes)
+        nsub = -(-n // (a.part_sub or (1 << 24)))
+        alg = pass_bytes(n / nsub, self.nvalid / nsub, self.probes / nsub, self.width, self.fixed,
+                         chain_geometry(self.engine), lds_k1=self.lds_k1,
+                         slab_bytes=(self.nslots if seg else self.nslots + VERIFY_KEYS) * 16384, cus=cus,
+                         seg=seg, nsub=nsub)
         passes = {}
         for i, (ms, cnt) in enumerate(pt or []):
             if cnt:
@@ -653,7 +670,9 @@ class Run:
                 passes[name] = {"ms": mean, "launches": cnt, "alg_bytes": ab,
                                 "GBps": ab / (mean * 1e-3) / 1e9}
         if passes:
-            dom = max(passes, key=lambda k: passes[k]["ms"])
+            # the kernel that takes the most time per step (a per-sub-batch
+            # kernel launches nsub times per step, the window pass once)
+            dom = max(passes, key=lambda k: passes[k]["ms"] * passes[k]["launches"])
             kern_ms, dom_bytes = passes[dom]["ms"], passes[dom]["alg_bytes"]
         else:  # graph replay: the launch time is the timed region's events / steps
             dom, kern_ms, dom_bytes = "k1", step_ms, alg["k1"] + alg["k1_stage"]
@@ -661,7 +680,7 @@ class Run:
         # HBM-side bytes per launch of that kernel from the committed rocprofv3
         # PMC passes of this workload (FETCH_SIZE + WRITE_SIZE, separate passes,
         # FETCH corrected for 16-B-per-lane streams where the summary says so)
-        pmc, pmc_src = load_pmc(self.cfg, dom)
+        pmc, pmc_src = load_pmc(self.pmc_tag(seg), dom)
         traffic = None
         if pmc is not None:
             # request-size-calibrated bytes where the summary has them (round 4:
@@ -674,7 +693,10 @@ class Run:
                 launches = passes["k1"]["launches"] if "k1" in passes else -(-a.steps // 48)
                 traffic *= a.steps / launches / pmc.get("steps_per_dispatch", a.steps)
         r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": pmc_src,
+             "frac": achieved / HBM_PEAK_GBS,
+             # also against the measured streaming rate
+             "peak_measured": HBM_MEASURED_GBS, "frac_measured_peak": achieved / HBM_MEASURED_GBS,
+             "traffic": traffic, "traffic_source": pmc_src, "pfadd_form": "segmented" if seg else "cas",
              "kernel": dom, "kernel_ms": kern_ms, "alg_bytes_per_launch": dom_bytes,
              "kernel_times": "instrumented replay of the timed steps" if passes else "timed region events",
              "device_ms_per_step": step_ms, "probes_per_swipe": self.probes / n,
@@ -682,7 +704,7 @@ class Run:
         if dom.startswith("k_part"):
             # SURVEY §8(d)'s whole-path model prices every probe as a random
             # 64-B HBM sector; the partitioned K1 answers probes from LDS slices
-            whole = alg["k1"]
+            whole = alg["k1"] * nsub
             r["whole_path_model"] = {
                 "what": "SURVEY §8(d) bytes for the whole path (every probe a random 64-B sector): not an HBM "
                         "roofline for the partitioned K1, whose probes are served from LDS-resident filter "
@@ -690,15 +712,15 @@ class Run:
                         "(passes[*].alg_bytes), the dominant pass's taken above",
                 "bytes_per_step": whole, "would_need_GBps": whole / (step_ms * 1e-3) / 1e9,
                 "of_peak": whole / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
-        if dom == "k_part_c":
-            sectors = self.nvalid / (kern_ms * 1e-3) / 1e9
+        if dom == "k_part_c" and not seg:
+            sectors = self.nvalid / nsub / (kern_ms * 1e-3) / 1e9
             r["random_sector_bound"] = {
                 "what": "one 64-B HBM sector per valid swipe's register, against the measured random "
                         "4-B read rate over a 1.6 GB table (tools/randbench.hip)",
                 "achieved_Gsectors_per_s": sectors, "peak_Gsectors_per_s": RANDOM_SECTOR_GPS,
                 "frac": sectors / RANDOM_SECTOR_GPS}
             if pmc and "TCC_EA0_ATOMIC_sum" in pmc.get("mean", {}):
-                req = (self.nvalid + pmc["mean"]["TCC_EA0_ATOMIC_sum"]) / (kern_ms * 1e-3) / 1e9
+                req = (self.nvalid / nsub + pmc["mean"]["TCC_EA0_ATOMIC_sum"]) / (kern_ms * 1e-3) / 1e9
                 r["random_sector_bound"].update({
                     "what": "random 64-B requests into the 1.6 GB register slab per second: one "
                             "pre-check load per valid swipe plus one memory-side CAS per raise "
@@ -726,6 +748,17 @@ class Run:
                     m["SQ_INSTS_VALU"] / max(1.0, pmc.get("swipes_per_dispatch", 0) / 64),
                 "lds_bank_conflict_rate": pmc.get("lds_bank_conflict_rate")}
         return r
+
+    def pmc_tag(self, seg):
+        """The name of this workload's committed PMC summaries
+        (profiles/<round>_pmc_<tag>_<kernel>.json): the config, then the
+        simulated shard, a non-default batch and the segmented PFADD."""
+        a, tag = self.args, self.cfg
+        if a.shard:
+            tag += "_shard%d" % self.kw
+        if a.batch:
+            tag += "_b%dm" % (a.batch >> 20)
+        return tag + ("_seg" if seg else "")
 
     def config(self):
         a, w = self.args, self.w

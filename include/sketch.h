@@ -296,8 +296,13 @@ int ske_swipes_variant(ske_ctx *ctx, uint32_t fid);
 /* Tuning options (no reference counterpart): "variant" (-1 auto, 0..3 as
  * above), "tile" (LDS K1 swipes per thread: 1, 2, 4, 8), "k1_grid" (LDS K1
  * blocks, 0 = one per CU), "k1_persistent" (0/1), "part_sub" (partitioned K1
- * swipes per sub-batch, 0 = 16M), "pass_timing" (0/1).  Any other name or an
- * out-of-range value: SKE_EINVAL.  None changes an answer or a register. */
+ * swipes per sub-batch, 0 = 16M), "pass_timing" (0/1); the partitioned K1's
+ * segmented PFADD: "hll_seg" (-1 auto, 0 never, 1 whenever the
+ * chain and slab allow), "seg_density" (auto: swipes per 128-B slab line at
+ * which a batch is segmented, x100), "seg_dense_min" (records per window line
+ * at which a window is staged in LDS, x100), "seg_klog" (2 or 3: keys per
+ * window 4 or 8).  Any other name or an out-of-range value: SKE_EINVAL.  None
+ * changes an answer or a register. */
 int ske_set_option(ske_ctx *ctx, const char *name, int64_t value);
 /* Kernel timing for the benchmark's roofline: with option "pass_timing" = 1
  * every K1 kernel launched outside a capture is bracketed by a HIP event pair
@@ -305,8 +310,10 @@ int ske_set_option(ske_ctx *ctx, const char *name, int64_t value);
  * returns, per pass kind, the summed milliseconds and the kernel count:
  * [0] single-kernel K1 (LDS / global / XCD-partitioned variants), [1] [2] [3]
  * the partitioned K1's passes A (hash + probe records), B (slice probes),
- * C (answers + register max).  reset != 0 zeroes the sums after reading. */
-#define SKE_PASS_KINDS 4
+ * C (answers + register max, or the segmented PFADD's answers + level-1
+ * records), [4] the segmented PFADD's level-2 sort, [5] its window apply.
+ * reset != 0 zeroes the sums after reading. */
+#define SKE_PASS_KINDS 6
 int ske_pass_times(ske_ctx *ctx, double *ms_out, uint64_t *count_out, int reset);
 
 /* ---- ingest: JSON event decode + key-slot resolution ----

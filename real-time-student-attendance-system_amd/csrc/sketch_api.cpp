@@ -79,6 +79,7 @@ struct ske_ctx {
     int pb = 2;           // K1 tile: swipes per thread in flight (1, 2, 4, 8)
     int variant = -1;     // -1 auto, 0 global, 1 LDS, 2 XCD-partitioned, 3 partitioned
     uint32_t part_sub = 0;  // partitioned K1: swipes per sub-batch (0: default)
+    SegOpts seg;            // partitioned K1: the segmented PFADD's options
     bool lds_ok = false;
     bool k1_ok = false;       // short-id LDS K1 (sketch_k1.hip) usable
     int k1_grid = 0;          // blocks of the short-id LDS K1 (0: one per CU)
@@ -543,7 +544,7 @@ int launch_part(ske_ctx *c, const ChainDev &ch, const PartBatch *bt, uint32_t nb
     uint64_t nmax = 0;
     for (uint32_t j = 0; j < nb; j++) nmax = bt[j].n > nmax ? bt[j].n : nmax;
     if (nmax == 0) return SKE_OK;
-    hipError_t e = part_reserve(ch, nmax, c->part_sub, c->scratch);
+    hipError_t e = part_reserve(ch, nmax, c->part_sub, c->nslots, c->seg, c->scratch);
     if (e != hipSuccess) return scratch_error(c, e);
     unsigned long long cid = 0;
     int rc = scratch_user_begin(c, &cid);
@@ -551,7 +552,7 @@ int launch_part(ske_ctx *c, const ChainDev &ch, const PartBatch *bt, uint32_t nb
     // one event pair per kernel and unit, bracketed on the kernel's stream;
     // back-to-back kernels on one stream share the event between them
     struct Hook {
-        PassMark pm[3];
+        PassMark pm[5];
         PassMark last;  // the mark whose end event was recorded last, if nothing came after it
     } hs;
     auto hook = [](void *u, int pass, int end, hipStream_t st) {
@@ -567,7 +568,7 @@ int launch_part(ske_ctx *c, const ChainDev &ch, const PartBatch *bt, uint32_t nb
         }
     };
     c->hook_arg = &hs;
-    e = launch_swipes_part(ch, bt, nb, c->regs, c->nslots, c->scratch, c->err, c->cus, c->part_sub, c->st,
+    e = launch_swipes_part(ch, bt, nb, c->regs, c->nslots, c->scratch, c->err, c->cus, c->part_sub, c->seg, c->st,
                            c->timing && !c->capturing ? +hook : nullptr, c);
     if (e != hipSuccess) {
         c->last_hip = std::string("launch_swipes_part: ") + hipGetErrorString(e);
@@ -807,6 +808,26 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
     if (!strcmp(name, "part_sub")) {  // partitioned K1 sub-batch (swipes; 0 = default)
         if (value < 0 || value > (int64_t(1) << 24)) return SKE_EINVAL;
         c->part_sub = uint32_t(value);
+        return SKE_OK;
+    }
+    if (!strcmp(name, "hll_seg")) {  // segmented PFADD: -1 auto, 0 never, 1 when the chain and slab allow
+        if (value < -1 || value > 1) return SKE_EINVAL;
+        c->seg.mode = int(value);
+        return SKE_OK;
+    }
+    if (!strcmp(name, "seg_density")) {  // auto threshold: swipes per slab line x100
+        if (value < 0 || value > 1000000) return SKE_EINVAL;
+        c->seg.density_x100 = uint32_t(value);
+        return SKE_OK;
+    }
+    if (!strcmp(name, "seg_dense_min")) {  // records per window line x100 to stage a window in LDS
+        if (value < 0 || value > 1000000) return SKE_EINVAL;
+        c->seg.dense_min_x100 = uint32_t(value);
+        return SKE_OK;
+    }
+    if (!strcmp(name, "seg_klog")) {  // keys per window 2^klog
+        if (value != 2 && value != 3) return SKE_EINVAL;
+        c->seg.klog = int(value);
         return SKE_OK;
     }
     if (!strcmp(name, "k1_grid")) {

@@ -138,11 +138,22 @@ constexpr uint32_t kPMaxSlices = 2047;
 constexpr int kPMaxLinks = 8;
 struct Scratch;
 bool part_supported(const ChainDev &ch);
+// The segmented PFADD (k_seg_*, the pass C of one-link chains when a batch's
+// register updates are dense in the slab) -- options "hll_seg" (mode),
+// "seg_density" and "seg_dense_min" (x100), "seg_klog".
+struct SegOpts {
+    int mode = -1;                  // -1 auto, 0 never (pass C), 1 whenever the chain and slab allow
+    uint32_t density_x100 = 200;    // auto: a batch's swipes per 128-B line of the slab, x100
+    uint32_t dense_min_x100 = 100;  // a window is staged in LDS from this many records per line, x100
+    int klog = 3;                   // keys per window: 2^klog (3: 128 KiB of LDS, 2: 64 KiB)
+};
 // sizes the context scratch for batches of up to n swipes (no launch)
 // sub: swipes per sub-batch of the three passes (0: the default, 16M)
-hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub, Scratch *scr);
+hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub, uint32_t nslots, const SegOpts &so,
+                        Scratch *scr);
 // hook (may be null): called as hook(user, pass, 0) right before and
-// hook(user, pass, 1) right after each pass's launch (pass 0..2 = A, B, C)
+// hook(user, pass, 1) right after each pass's launch (pass 0..4 = A, B, C or
+// the segmented C1, the segmented level-2 sort, the segmented window apply)
 typedef void (*PassHook)(void *user, int pass, int end, hipStream_t st);
 struct PartBatch {
     const uint8_t *bytes;
@@ -155,7 +166,8 @@ struct PartBatch {
 // every pass of every (batch, sub-batch) unit on st, in order
 hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t nb, uint8_t *regs,
                               uint32_t nslots, Scratch *scr, unsigned int *err, int cus, uint32_t sub,
-                              hipStream_t st, PassHook hook = nullptr, void *hook_user = nullptr);
+                              const SegOpts &so, hipStream_t st, PassHook hook = nullptr,
+                              void *hook_user = nullptr);
 
 
 // sketch_order.hip -- order-exact paths (replies that depend on item order)

@@ -1097,6 +1097,510 @@ __global__ void __launch_bounds__(kPcFlBlock) k_part_c_fl(const PartArgs A) {
 }
 
 // ---------------------------------------------------------------------------
+// Segmented PFADD (north_star's HLL kernel form): pass C of the one-link
+// partitioned K1 when the call's register updates are dense in the slab --
+// the batch is segmented by key, each key window's registers are staged in
+// LDS, raised there, and flushed to HBM as whole lines.  Same result as
+// k_part_c_fl (hllAdd's register max, attendance_processor.py:127-129; max is
+// commutative, so the order of updates is free).
+//
+// Why.  k_part_c_fl costs one random 128-B line read per valid swipe (its
+// register's pre-check) plus one memory-side CAS per raise: 14.4 M + 7 M
+// random requests per 16 M-swipe C3 step.  When a call's updates are dense
+// in the slab -- an 8-way shard (12.5 k keys, 205 MB, ~9 updates per 128-B
+// line per 16 M swipes) or a large batch -- reading every line of the slab
+// once and writing back the lines that rose costs fewer bytes than the
+// random requests, and no atomics reach memory.
+//
+//   C1 (k_seg_c1)   per run of 8 tiles (8192 swipes; pass B's fail lists of a
+//                   run are one line per unit): the answers as k_part_c_fl,
+//                   and for each valid swipe one 4-byte record
+//                   (slot-in-bucket << 20 | register << 6 | rank),
+//                   counting-sorted in LDS by level-1 bucket (slot >> s1,
+//                   <= 512 buckets) and written as the run's block of
+//                   records; o1[bucket][run] = the bucket's start in it.
+//   S  (k_seg_scan) per bucket: prefix of its run lengths over the runs,
+//                   and the run holding the first record of each of its
+//                   8192-record level-2 chunks.
+//   D  (k_seg_d)    per chunk: its records gathered from the runs,
+//                   counting-sorted in LDS by window (2^klog keys) within
+//                   the bucket; o2[chunk][window] = the window's start.
+//   E  (k_seg_e)    per window, once per call (after every sub-batch's C1,
+//                   S, D): its records' runs over every chunk of its bucket;
+//                   with at least dense_min records the window's registers
+//                   (2^klog x 16 KiB) are loaded into LDS in whole lines,
+//                   raised there (LDS CAS; registers only grow), and the
+//                   lines that rose are stored back; a sparse window raises
+//                   its records in place (pre-check load + CAS, as pass C).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSegRunTiles = kPbGroup;                 // tiles per level-1 run
+constexpr uint32_t kSegRunSw = kSegRunTiles << kPTileLog;  // 8192 swipes
+constexpr uint32_t kSegMaxB1 = 512;                         // level-1 buckets
+constexpr uint32_t kSegMaxWpb = 512;                        // windows per bucket
+constexpr uint32_t kSegChunk = 8192;                        // records per level-2 chunk
+constexpr uint32_t kSegMaxRuns = kPSub / kSegRunSw;         // 2048 runs per sub-batch
+constexpr uint32_t kSegRecShift = 20;                       // record: slot-in-bucket above bit 20
+constexpr uint32_t kSegEPairs = 1024;                       // E: (sub-batch, chunk) runs staged at once
+constexpr uint32_t kSegSlice = 65536;                       // E: records per block and window (hot windows are cut)
+
+struct SegArgs {
+    uint32_t *r1;     // [nruns][kSegRunSw] level-1 records of a sub-batch, bucket-sorted per run
+    uint32_t *o1;     // [nb1 + 1][kSegMaxRuns] bucket h's start in run r; [nb1][r] = the run's total
+    uint32_t *p1;     // [nb1][kSegMaxRuns + 1] prefix over runs of bucket h's lengths; [h][nruns] = total
+    uint32_t *cst;    // [nb1][kSegMaxRuns + 1] run holding chunk c's first record
+    uint32_t *r2;     // [nsub][maxch][kSegChunk] level-2 records, window-sorted per chunk
+    uint32_t *o2;     // [nsub][maxch][wpb + 1] window w's start in chunk q
+    uint32_t *cb;     // [nsub][nb1 + 1] first chunk of bucket h in sub-batch s (prefix)
+    uint32_t nruns;   // level-1 runs of this sub-batch
+    uint32_t nb1;     // level-1 buckets (slot >> s1)
+    uint32_t s1;      // slot bits below the bucket (<= 12)
+    uint32_t wlog;    // windows per bucket = 1 << wlog
+    uint32_t klog;    // keys per window = 1 << klog
+    uint32_t s;       // this sub-batch's index in the call
+    uint32_t nsub;    // sub-batches of the call
+    uint32_t maxch;   // level-2 chunk slots per sub-batch
+    uint32_t nwin;    // windows of the slab (E)
+    uint32_t dense_min;  // E: records at which a window is staged in LDS
+    uint32_t *q;      // window pass queue header: [0] queued slices, [1] copies, [2] cut windows (zeroed per call)
+    uint4 *qitems;    // queued slices (window, slice, copy)
+    uint4 *mlist;     // cut windows (window, first copy, slices)
+    uint8_t *copies;  // [ccap][window bytes] LDS copies of cut windows' slices
+    uint32_t ccap;    // copies (and queue entries) available
+};
+
+// Exclusive prefix of one value per thread over the block (blockDim a
+// multiple of 64); every thread also gets the total.  `ws`: blockDim / 64
+// words of LDS.  LDS-only barriers (global loads and stores stay in flight).
+__device__ __forceinline__ uint32_t seg_scan(uint32_t v, uint32_t *ws, uint32_t &total) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    const uint32_t inc = part_wave_scan(v);
+    lds_barrier();  // the previous scan's readers of ws are done
+    if (lane == 63) ws[wave] = inc;
+    lds_barrier();
+    uint32_t pre = 0, tot = 0;
+    for (uint32_t w = 0; w < nw; w++) {
+        const uint32_t x = ws[w];
+        pre += w < wave ? x : 0;
+        tot += x;
+    }
+    total = tot;
+    return pre + inc - v;
+}
+
+// index of the last entry of a[0..n) that is <= v (a ascending, a[0] <= v)
+__device__ __forceinline__ uint32_t seg_last_le(const uint32_t *a, uint32_t n, uint32_t v) {
+    uint32_t lo = 0, len = n;
+    while (len > 1) {
+        const uint32_t half = len >> 1;
+        if (a[lo + half] <= v) lo += half;
+        len -= half;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(1024, 8) k_seg_c1(const PartArgs A, const SegArgs S) {
+    __shared__ uint16_t mark[kSegRunSw];
+    __shared__ __attribute__((aligned(16))) uint32_t srec[kSegRunSw];
+    __shared__ uint32_t cnt[kSegMaxB1 + 1];
+    __shared__ uint32_t ws[16];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t j = tid; j < kSegRunSw; j += 1024) mark[j] = 0;
+    const uint32_t npieces = A.nunits * kSegRunTiles;  // 16-B lists of one run
+    const __amdgpu_buffer_rsrc_t rfl = part_rsrc(A.flist, A.nunits * A.fl_stride * kPbLanes * 2);
+    const uint32_t smask = (1u << S.s1) - 1;
+    lds_barrier();  // marks cleared before any run sets one
+    for (uint32_t r = blockIdx.x; r < S.nruns; r += gridDim.x) {
+        const uint32_t t0 = r * kSegRunTiles;
+        const uint32_t t1 = t0 + kSegRunTiles < A.ntiles ? t0 + kSegRunTiles : A.ntiles;
+        const uint16_t ep = uint16_t(r + 1);  // <= 2048: marks are never cleared
+        // the run's streams, every tile's in flight together
+        uint32_t fb[kSegRunTiles], sl[kSegRunTiles], hv[kSegRunTiles];
+#pragma unroll
+        for (uint32_t u = 0; u < kSegRunTiles; u++) {
+            const uint32_t i = (t0 + u) * 1024 + tid;
+            const bool act = t0 + u < t1 && i < A.n;
+            fb[u] = act ? nt_ld<16>(A.fail + i) : 1u;
+            sl[u] = act ? nt_ld<16>(A.slot + i) : 0u;
+            hv[u] = act ? nt_ld<16>(A.hllw + i) : 0u;
+        }
+        if (tid <= S.nb1) cnt[tid] = 0;
+        // the run's fail lists -> marks (piece p = unit p / 8, tile t0 + p % 8)
+        for (uint32_t p0 = 0; p0 < npieces; p0 += 4 * 1024) {
+            part_u32x4 e[4];
+            bool ok[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t p = p0 + uint32_t(j) * 1024 + tid;
+                const uint32_t un = p / kSegRunTiles, tt = t0 + p % kSegRunTiles;
+                ok[j] = p < npieces && tt < t1;
+                e[j] = __builtin_bit_cast(part_u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                         rfl, ok[j] ? (un * A.fl_stride + tt) * kPbLanes * 2 : kOOR, 0, 0));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t base = ((p0 + uint32_t(j) * 1024 + tid) % kSegRunTiles) * 1024;
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const uint32_t lo = e[j][c] & 0xffffu, hi = e[j][c] >> 16;
+                    if (ok[j] && lo != 0xffffu) mark[base + (lo & 1023u)] = ep;
+                    if (ok[j] && hi != 0xffffu) mark[base + (hi & 1023u)] = ep;
+                }
+            }
+        }
+        lds_barrier();
+        uint32_t rec[kSegRunTiles], pos[kSegRunTiles];
+#pragma unroll
+        for (uint32_t u = 0; u < kSegRunTiles; u++) {
+            const uint32_t i = (t0 + u) * 1024 + tid;
+            const bool act = t0 + u < t1 && i < A.n;
+            const bool valid = act && fb[u] == 0 && mark[u * 1024 + tid] != ep;
+            if (A.out && act) nt_st<16>(A.out + i, uint8_t(valid));
+            pos[u] = 0xffffffffu;
+            rec[u] = 0;
+            if (valid) {
+                if (sl[u] >= A.nslots) {
+                    atomicOr(A.err, 1u);
+                } else {
+                    const uint32_t b = sl[u] >> S.s1;
+                    rec[u] = ((sl[u] & smask) << kSegRecShift) | ((hv[u] & 0x3fffu) << 6) | (hv[u] >> 16);
+                    pos[u] = (b << 16) | atomicAdd(&cnt[b], 1u);
+                }
+            }
+        }
+        lds_barrier();
+        uint32_t total;
+        const uint32_t ex = seg_scan(tid <= S.nb1 ? cnt[tid] : 0u, ws, total);
+        if (tid <= S.nb1) {  // [nb1] = the run's total
+            cnt[tid] = ex;
+            S.o1[size_t(tid) * kSegMaxRuns + r] = ex;
+        }
+        lds_barrier();
+#pragma unroll
+        for (uint32_t u = 0; u < kSegRunTiles; u++)
+            if (pos[u] != 0xffffffffu) srec[cnt[pos[u] >> 16] + (pos[u] & 0xffffu)] = rec[u];
+        lds_barrier();
+        uint4 *dst = reinterpret_cast<uint4 *>(S.r1 + size_t(r) * kSegRunSw);
+        const uint4 *src = reinterpret_cast<const uint4 *>(srec);
+        for (uint32_t j = tid; j * 4 < total; j += 1024) dst[j] = src[j];
+        // (the next run rewrites cnt, marks and srec only behind barriers
+        // that every reader of this run's values has passed)
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_seg_scan(const SegArgs S) {
+    __shared__ uint32_t ws[16];
+    const uint32_t h = blockIdx.x, tid = threadIdx.x;
+    const uint32_t *oa = S.o1 + size_t(h) * kSegMaxRuns, *ob = oa + kSegMaxRuns;
+    uint32_t *pp = S.p1 + size_t(h) * (kSegMaxRuns + 1);
+    uint32_t *cs = S.cst + size_t(h) * (kSegMaxRuns + 1);
+    const uint32_t r0 = 2 * tid, r1 = 2 * tid + 1;  // nruns <= 2048
+    const uint32_t c0 = r0 < S.nruns ? ob[r0] - oa[r0] : 0u;
+    const uint32_t c1 = r1 < S.nruns ? ob[r1] - oa[r1] : 0u;
+    uint32_t total;
+    const uint32_t a0 = seg_scan(c0 + c1, ws, total);
+    const uint32_t a1 = a0 + c0;
+    if (r0 < S.nruns) pp[r0] = a0;
+    if (r1 < S.nruns) pp[r1] = a1;
+    if (tid == 0) pp[S.nruns] = total;
+    // a run holds <= 8192 records: at most one chunk starts inside it
+    for (uint32_t q = (a0 + kSegChunk - 1) / kSegChunk; q * kSegChunk < a0 + c0; q++) cs[q] = r0;
+    for (uint32_t q = (a1 + kSegChunk - 1) / kSegChunk; q * kSegChunk < a1 + c1; q++) cs[q] = r1;
+}
+
+__global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
+    __shared__ uint32_t tot[kSegMaxB1], cbl[kSegMaxB1 + 1];
+    __shared__ uint32_t spp[kSegMaxRuns + 1], sob[kSegMaxRuns];
+    __shared__ uint32_t c2[kSegMaxWpb + 1];
+    __shared__ __attribute__((aligned(16))) uint32_t sb[kSegChunk];
+    __shared__ uint32_t ws[16];
+    const uint32_t tid = threadIdx.x, wpb = 1u << S.wlog;
+    // the buckets' chunk bases (every block; block 0 keeps them for E)
+    uint32_t t = 0;
+    if (tid < S.nb1) {
+        t = S.p1[size_t(tid) * (kSegMaxRuns + 1) + S.nruns];
+        tot[tid] = t;
+    }
+    uint32_t nq;
+    const uint32_t cbase = seg_scan(tid < S.nb1 ? (t + kSegChunk - 1) / kSegChunk : 0u, ws, nq);
+    if (tid <= S.nb1) {
+        cbl[tid] = cbase;
+        if (blockIdx.x == 0) S.cb[size_t(S.s) * (S.nb1 + 1) + tid] = cbase;
+    }
+    lds_barrier();
+    uint32_t *r2 = S.r2 + size_t(S.s) * S.maxch * kSegChunk;
+    uint32_t *o2 = S.o2 + size_t(S.s) * S.maxch * (wpb + 1);
+    for (uint32_t q = blockIdx.x; q < nq; q += gridDim.x) {
+        const uint32_t h = seg_last_le(cbl, S.nb1, q);  // buckets without chunks share the next one's base
+        const uint32_t c = q - cbl[h], w0 = c * kSegChunk;
+        const uint32_t w1 = tot[h] - w0 < kSegChunk ? tot[h] : w0 + kSegChunk;
+        const uint32_t *pp = S.p1 + size_t(h) * (kSegMaxRuns + 1);
+        const uint32_t *cs = S.cst + size_t(h) * (kSegMaxRuns + 1);
+        const uint32_t ga = cs[c];
+        const uint32_t gb = w1 < tot[h] ? cs[c + 1] + 1 : S.nruns;  // runs [ga, gb) hold [w0, w1)
+        const uint32_t ng = gb - ga;
+        for (uint32_t j = tid; j <= ng; j += 1024) {
+            spp[j] = pp[ga + j];
+            if (j < ng) sob[j] = S.o1[size_t(h) * kSegMaxRuns + ga + j];
+        }
+        if (tid <= wpb) c2[tid] = 0;
+        lds_barrier();
+        // 8 consecutive records per thread: one search, then a walk
+        uint32_t rec[8], pos[8];
+        const uint32_t p0 = w0 + tid * 8;
+        uint32_t k = p0 < w1 ? seg_last_le(spp, ng, p0) : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            const uint32_t p = p0 + j;
+            rec[j] = 0;
+            if (p < w1) {
+                while (spp[k + 1] <= p) k++;
+                rec[j] = S.r1[size_t(ga + k) * kSegRunSw + sob[k] + (p - spp[k])];
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            pos[j] = 0xffffffffu;
+            if (p0 + j < w1) {
+                const uint32_t w2 = (rec[j] >> (kSegRecShift + S.klog)) & (wpb - 1);
+                pos[j] = (w2 << 16) | atomicAdd(&c2[w2], 1u);
+            }
+        }
+        lds_barrier();
+        uint32_t total;
+        const uint32_t ex = seg_scan(tid <= wpb ? c2[tid] : 0u, ws, total);
+        if (tid <= wpb) {
+            c2[tid] = ex;
+            o2[size_t(q) * (wpb + 1) + tid] = ex;
+        }
+        lds_barrier();
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++)
+            if (pos[j] != 0xffffffffu) sb[c2[pos[j] >> 16] + (pos[j] & 0xffffu)] = rec[j];
+        lds_barrier();
+        uint4 *dst = reinterpret_cast<uint4 *>(r2 + size_t(q) * kSegChunk);
+        const uint4 *src = reinterpret_cast<const uint4 *>(sb);
+        for (uint32_t j = tid; j * 4 < total; j += 1024) dst[j] = src[j];
+    }
+}
+
+// byte max of an LDS register (the window's copy); true if it rose
+__device__ __forceinline__ bool seg_lds_max(uint32_t *w, uint32_t sh, uint32_t rank) {
+    uint32_t old = *w;
+    while (((old >> sh) & 0xffu) < rank) {
+        const uint32_t prev = atomicCAS(w, old, (old & ~(0xffu << sh)) | (rank << sh));
+        if (prev == old) return true;
+        old = prev;
+    }
+    return false;
+}
+
+// The window pass.  A window whose records exceed kSegSlice (a hot key's:
+// at the 8-way shard the hottest lecture's day keys take ~1.8 M records of
+// one window per step) is cut into slices so that no block reads more than
+// kSegSlice records: pass E1 (QUEUE = false) takes every window's first
+// slice and queues the others; E2 (QUEUE = true) takes the queued slices;
+// each slice of a cut window raises its own LDS copy of the window, stored
+// whole to a copy buffer, and M (k_seg_m) stores the byte max of the copies.
+// An uncut window's risen lines go straight back to the slab.
+template <int KLOG, bool QUEUE>
+__global__ void __launch_bounds__(1024, KLOG >= 3 ? 4 : 8) k_seg_e(const PartArgs A, const SegArgs S) {
+    constexpr uint32_t KW = 1u << KLOG, WB = KW << kHllP, NPC = WB / 16 / 1024;  // 16-B pieces per thread
+    constexpr uint32_t NL = KW * (kHllRegs / 128);                                 // 128-B lines
+    constexpr uint32_t PIECE = 1024;                                               // records per wave piece
+    __shared__ __attribute__((aligned(16))) uint8_t win[WB];
+    __shared__ uint8_t dirty[NL];
+    __shared__ uint32_t rbase[kSegEPairs], rlen[kSegEPairs], rpre[kSegEPairs];
+    __shared__ uint32_t spre[65], ws[16], hdr[2];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t wpb = 1u << S.wlog;
+    const __amdgpu_buffer_rsrc_t rr2 = part_rsrc(S.r2, S.nsub * S.maxch * kSegChunk * 4);
+    const uint32_t nitems = QUEUE ? S.q[0] : S.nwin;
+    for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
+        uint32_t wi, sl = 0, copy = 0xffffffffu;
+        if (QUEUE) {
+            const uint4 e = S.qitems[it];
+            wi = e.x;
+            sl = e.y;
+            copy = e.z;
+        } else {
+            wi = it;
+        }
+        const uint32_t h = wi >> S.wlog, w2 = wi & (wpb - 1);
+        const uint32_t slot0 = wi << KLOG;
+        const uint32_t nk = A.nslots - slot0 < KW ? A.nslots - slot0 : KW;
+        // the window's runs: pair x = (sub-batch s, chunk q of bucket h in
+        // s), in that order; spre = prefix of the sub-batches' chunk counts
+        uint32_t np;
+        {
+            uint32_t v = 0;
+            if (tid < S.nsub)
+                v = S.cb[size_t(tid) * (S.nb1 + 1) + h + 1] - S.cb[size_t(tid) * (S.nb1 + 1) + h];
+            const uint32_t ex = seg_scan(v, ws, np);
+            if (tid < S.nsub) spre[tid] = ex;
+        }
+        lds_barrier();
+        auto run_of = [&](uint32_t x, uint32_t &base) -> uint32_t {
+            const uint32_t s = seg_last_le(spre, S.nsub, x);
+            const uint32_t q = S.cb[size_t(s) * (S.nb1 + 1) + h] + (x - spre[s]);
+            const size_t row = size_t(s) * S.maxch + q;
+            const uint32_t *o = S.o2 + row * (wpb + 1) + w2;
+            const uint32_t b = o[0];
+            base = uint32_t(row * kSegChunk + b);  // < 2^32: the host plan checks nsub * maxch * kSegChunk
+            return o[1] - b;
+        };
+        uint32_t nrec = 0;
+        for (uint32_t x0 = 0; x0 < np; x0 += 1024) {
+            uint32_t base, len = 0, t;
+            if (x0 + tid < np) len = run_of(x0 + tid, base);
+            (void)seg_scan(len, ws, t);
+            nrec += t;
+        }
+        if (nrec == 0) continue;  // block-uniform
+        uint32_t nsl = 1;
+        if (!QUEUE) {
+            nsl = (nrec + kSegSlice - 1) / kSegSlice;
+            if (nsl > 1) {
+                if (tid == 0) {
+                    uint32_t base = atomicAdd(&S.q[1], nsl);
+                    if (base + nsl > S.ccap) {
+                        base = 0xffffffffu;  // out of copies (cannot happen: see seg_scratch): one slice
+                    } else {
+                        const uint32_t qp = atomicAdd(&S.q[0], nsl - 1);
+                        for (uint32_t k = 1; k < nsl; k++) S.qitems[qp + k - 1] = make_uint4(wi, k, base + k, 0);
+                        S.mlist[atomicAdd(&S.q[2], 1u)] = make_uint4(wi, base, nsl, 0);
+                    }
+                    hdr[0] = base;
+                }
+                lds_barrier();
+                copy = hdr[0];
+                if (copy == 0xffffffffu) nsl = 1;
+                lds_barrier();  // hdr is rewritten by the next window
+            }
+        }
+        const bool cut = copy != 0xffffffffu;
+        const uint32_t lo = cut ? sl * kSegSlice : 0;
+        const uint32_t hi = cut ? (nrec - lo < kSegSlice ? nrec : lo + kSegSlice) : nrec;
+        const bool dense = cut || nrec >= S.dense_min;
+        uint8_t *g = A.regs + (size_t(slot0) << kHllP);
+        const uint32_t npc = nk << (kHllP - 4);  // the window's 16-B pieces in the slab
+        if (dense) {
+            // the window's registers into LDS, whole lines, all in flight
+            part_u32x4 v[NPC];
+#pragma unroll
+            for (uint32_t i = 0; i < NPC; i++) {
+                const uint32_t j = i * 1024 + tid;
+                v[i] = j < npc ? reinterpret_cast<const part_u32x4 *>(g)[j] : part_u32x4{0, 0, 0, 0};
+            }
+            for (uint32_t j = tid; j < NL; j += 1024) dirty[j] = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < NPC; i++) reinterpret_cast<part_u32x4 *>(win)[i * 1024 + tid] = v[i];
+        }
+        // records [lo, hi) of the window's concatenated runs, in pieces of up
+        // to PIECE records of one run (aligned to 4 records), one per wave
+        uint32_t p0 = 0;  // records of the runs before this batch
+        for (uint32_t x0 = 0; x0 < np && p0 < hi; x0 += kSegEPairs) {
+            const uint32_t nx = np - x0 < kSegEPairs ? np - x0 : kSegEPairs;
+            uint32_t npieces, btot;
+            {
+                uint32_t base = 0, len = 0;
+                if (tid < nx) len = run_of(x0 + tid, base);
+                const uint32_t pre = p0 + seg_scan(len, ws, btot);
+                // this run's part of [lo, hi), as absolute r2 indices [b, e)
+                const uint32_t a = pre > lo ? pre : lo, z = pre + len < hi ? pre + len : hi;
+                uint32_t pc = 0, b = 0, e = 0;
+                if (a < z) {
+                    b = base + (a - pre);
+                    e = base + (z - pre);
+                    pc = (e - (b & ~3u) + PIECE - 1) / PIECE;
+                }
+                const uint32_t ex = seg_scan(pc, ws, npieces);
+                if (tid < nx) {
+                    rbase[tid] = b;
+                    rlen[tid] = e;
+                    rpre[tid] = ex;
+                }
+            }
+            lds_barrier();  // (the window's LDS image is complete here too)
+            for (uint32_t pc = wave; pc < npieces; pc += 16) {
+                const uint32_t j = seg_last_le(rpre, nx, pc);
+                const uint32_t b = rbase[j], e = rlen[j];
+                const uint32_t x = (b & ~3u) + (pc - rpre[j]) * PIECE;
+                part_u32x4 r[PIECE / 256];
+#pragma unroll
+                for (uint32_t i = 0; i < PIECE / 256; i++) {
+                    const uint32_t xi = x + i * 256 + lane * 4;
+                    r[i] = __builtin_bit_cast(part_u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                             rr2, xi < e ? xi * 4 : kOOR, 0, 0));
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < PIECE / 256; i++) {
+#pragma unroll
+                    for (uint32_t c = 0; c < 4; c++) {
+                        const uint32_t xi = x + i * 256 + lane * 4 + c;
+                        const uint32_t rec = r[i][c];
+                        const uint32_t rank = rec & 63u;
+                        if (xi < b || xi >= e || rank == 0) continue;
+                        const uint32_t ad = (((rec >> kSegRecShift) & (KW - 1)) << kHllP) | ((rec >> 6) & 0x3fffu);
+                        if (dense) {
+                            if (seg_lds_max(reinterpret_cast<uint32_t *>(win + (ad & ~3u)), (ad & 3u) * 8, rank))
+                                dirty[ad >> 7] = 1;
+                        } else {
+                            uint32_t *w = reinterpret_cast<uint32_t *>(g + (ad & ~3u));
+                            part_reg_max(w, (ad & 3u) * 8, rank, *w);
+                        }
+                    }
+                }
+            }
+            p0 += btot;
+            lds_barrier();  // rbase / rlen / rpre are rewritten by the next batch of runs
+        }
+        if (cut) {
+            // a slice of a cut window: the whole LDS copy, merged by k_seg_m
+            part_u32x4 *dst = reinterpret_cast<part_u32x4 *>(S.copies + size_t(copy) * WB);
+#pragma unroll
+            for (uint32_t i = 0; i < NPC; i++) dst[i * 1024 + tid] = reinterpret_cast<const part_u32x4 *>(win)[i * 1024 + tid];
+            lds_barrier();
+        } else if (dense) {
+            // the lines that rose, stored back whole
+#pragma unroll
+            for (uint32_t i = 0; i < NPC; i++) {
+                const uint32_t j = i * 1024 + tid;
+                if (j < npc && dirty[j >> 3])
+                    reinterpret_cast<part_u32x4 *>(g)[j] = reinterpret_cast<const part_u32x4 *>(win)[j];
+            }
+            lds_barrier();  // the next window's image overwrites win
+        }
+    }
+}
+
+// bytewise max of two 16-byte pieces
+__device__ __forceinline__ part_u32x4 seg_max16(part_u32x4 a, part_u32x4 b) {
+    typedef unsigned char u8x16 __attribute__((ext_vector_type(16)));
+    return __builtin_bit_cast(part_u32x4,
+                              __builtin_elementwise_max(__builtin_bit_cast(u8x16, a), __builtin_bit_cast(u8x16, b)));
+}
+
+// M: every cut window = the byte max of its slices' copies (each started
+// from the slab's registers, so the max holds every slice's raises)
+template <int KLOG>
+__global__ void __launch_bounds__(1024) k_seg_m(const PartArgs A, const SegArgs S) {
+    constexpr uint32_t KW = 1u << KLOG, WB = KW << kHllP;
+    const uint32_t nm = S.q[2];
+    for (uint32_t m = blockIdx.x; m < nm; m += gridDim.x) {
+        const uint4 e = S.mlist[m];
+        const uint32_t slot0 = e.x << KLOG;
+        const uint32_t nk = A.nslots - slot0 < KW ? A.nslots - slot0 : KW;
+        part_u32x4 *g = reinterpret_cast<part_u32x4 *>(A.regs + (size_t(slot0) << kHllP));
+        for (uint32_t j = threadIdx.x; j < (nk << (kHllP - 4)); j += 1024) {
+            part_u32x4 v = reinterpret_cast<const part_u32x4 *>(S.copies + size_t(e.y) * WB)[j];
+            for (uint32_t c = 1; c < e.z; c++)
+                v = seg_max16(v, reinterpret_cast<const part_u32x4 *>(S.copies + size_t(e.y + c) * WB)[j]);
+            g[j] = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 static inline unsigned part_grid(uint64_t n, unsigned block, unsigned cap) {
@@ -1181,17 +1685,101 @@ static uint32_t part_sub(uint32_t sub_opt) {
 }
 
 // the scratch before the first launch (so a graph recorded later holds it)
-hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, Scratch *scr) {
+// The segmented PFADD's geometry for a slab of nslots keys and a batch of n
+// swipes in sub-batches of `sub`: windows of 2^klog keys; the level-1 bucket
+// is slot >> s1 with 2^wlog windows each, wlog ~ log2(windows) / 2 so that
+// both levels' runs stay long (at C3: 98 buckets x 128 windows at 100 k keys,
+// 25 x 64 at the 8-way shard); false when the slab is too large for 512
+// buckets of 4096 keys.
+struct SegPlan {
+    uint32_t s1, wlog, klog, nb1, nwin, maxch, nsub, dense_min;
+};
+static bool seg_plan(uint32_t nslots, uint64_t n, uint32_t sub, const SegOpts &so, SegPlan *P) {
+    if (nslots == 0 || n == 0 || (so.klog != 2 && so.klog != 3)) return false;
+    const uint32_t klog = uint32_t(so.klog);
+    const uint32_t nwin = uint32_t((uint64_t(nslots) + (1u << klog) - 1) >> klog);
+    uint32_t wlog = 0;
+    while ((uint64_t(1) << (2 * wlog)) < nwin) wlog++;
+    uint32_t s1 = klog + wlog;
+    while (((uint64_t(nslots) + (uint64_t(1) << s1) - 1) >> s1) > kSegMaxB1) {
+        s1++;
+        wlog++;
+    }
+    if (wlog > 9 || s1 > 12) return false;
+    P->klog = klog;
+    P->wlog = wlog;
+    P->s1 = s1;
+    P->nwin = nwin;
+    P->nb1 = uint32_t((uint64_t(nslots) + (uint64_t(1) << s1) - 1) >> s1);
+    P->nsub = uint32_t((n + sub - 1) / sub);
+    P->maxch = (sub + kSegChunk - 1) / kSegChunk + P->nb1;
+    if (P->nsub > 64 || uint64_t(P->nsub) * P->maxch * kSegChunk >= (uint64_t(1) << 32)) return false;
+    const uint64_t dm = uint64_t(so.dense_min_x100) * ((uint64_t(1) << klog) * (kHllRegs / 128)) / 100;
+    P->dense_min = dm < 1 ? 1u : (dm > 0xffffffffu ? 0xffffffffu : uint32_t(dm));
+    return true;
+}
+
+// segmented for this batch: the fail-list chain, the option, and (auto) at
+// least density_x100 / 100 swipes per 128-B register line of the slab
+static bool seg_use(const PartArgs &A, const SegOpts &so, uint32_t nslots, uint64_t n, uint32_t sub, SegPlan *P) {
+    if (so.mode == 0 || !part_flist(A) || !seg_plan(nslots, n, sub, so, P)) return false;
+    if (so.mode == 1) return true;
+    return n * 100 >= uint64_t(so.density_x100) * nslots * (kHllRegs / 128);
+}
+
+// the segmented PFADD's scratch (context slots 32-38)
+static hipError_t seg_scratch(const SegPlan &P, uint32_t sub, uint64_t n, Scratch *scr, SegArgs *S) {
+    const uint64_t m = n < sub ? n : sub;
+    hipError_t e = hipSuccess;
+    S->r1 = (uint32_t *)scratch_get(scr, 32, size_t((m + kSegRunSw - 1) / kSegRunSw) * kSegRunSw * 4, &e);
+    if (e == hipSuccess) S->o1 = (uint32_t *)scratch_get(scr, 33, size_t(P.nb1 + 1) * kSegMaxRuns * 4, &e);
+    if (e == hipSuccess) S->p1 = (uint32_t *)scratch_get(scr, 34, size_t(P.nb1) * (kSegMaxRuns + 1) * 4, &e);
+    if (e == hipSuccess) S->cst = (uint32_t *)scratch_get(scr, 35, size_t(P.nb1) * (kSegMaxRuns + 1) * 4, &e);
+    if (e == hipSuccess)
+        S->r2 = (uint32_t *)scratch_get(scr, 36, size_t(P.nsub) * P.maxch * kSegChunk * 4, &e);
+    if (e == hipSuccess)
+        S->o2 = (uint32_t *)scratch_get(scr, 37, size_t(P.nsub) * P.maxch * ((1u << P.wlog) + 1) * 4, &e);
+    if (e == hipSuccess) S->cb = (uint32_t *)scratch_get(scr, 38, size_t(P.nsub) * (P.nb1 + 1) * 4, &e);
+    // the window pass's cut windows: a cut window has > kSegSlice records and
+    // ceil(records / kSegSlice) < 2 records / kSegSlice slices, so 2 n /
+    // kSegSlice copies, queue entries and cut windows always suffice
+    const uint32_t ccap = uint32_t(2 * ((n + kSegSlice - 1) / kSegSlice) + 2);
+    const size_t wb = size_t(1) << (P.klog + kHllP);
+    if (e == hipSuccess) S->q = (uint32_t *)scratch_get(scr, 39, 16, &e);
+    if (e == hipSuccess) S->qitems = (uint4 *)scratch_get(scr, 42, size_t(ccap) * 16, &e);
+    if (e == hipSuccess) S->mlist = (uint4 *)scratch_get(scr, 43, size_t(ccap) * 16, &e);
+    if (e == hipSuccess) S->copies = (uint8_t *)scratch_get(scr, 45, size_t(ccap) * wb, &e);
+    S->ccap = ccap;
+    S->nb1 = P.nb1;
+    S->s1 = P.s1;
+    S->wlog = P.wlog;
+    S->klog = P.klog;
+    S->nsub = P.nsub;
+    S->maxch = P.maxch;
+    S->nwin = P.nwin;
+    S->dense_min = P.dense_min;
+    return e;
+}
+
+hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, uint32_t nslots, const SegOpts &so,
+                        Scratch *scr) {
     PartArgs A{};
     if (!part_plan(ch, &A)) return hipErrorInvalidValue;
-    return part_scratch(&A, n ? n : 1, part_sub(sub_opt), scr);
+    const uint32_t sub = part_sub(sub_opt);
+    hipError_t e = part_scratch(&A, n ? n : 1, sub, scr);
+    SegPlan P;
+    if (e == hipSuccess && seg_use(A, so, nslots, n ? n : 1, sub, &P)) {
+        SegArgs S{};
+        e = seg_scratch(P, sub, n, scr, &S);
+    }
+    return e;
 }
 
 // Units = (batch, sub-batch of at most `sub` swipes), in order, each as the
 // three passes on `st`.  `hook` (pass timing) brackets every kernel.
 hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t nb, uint8_t *regs,
                               uint32_t nslots, Scratch *scr, unsigned int *err, int cus, uint32_t sub_opt,
-                              hipStream_t st, PassHook hook, void *hook_user) {
+                              const SegOpts &so, hipStream_t st, PassHook hook, void *hook_user) {
     PartArgs A{};
     if (!part_plan(ch, &A)) return hipErrorInvalidValue;
     const uint32_t sub = part_sub(sub_opt);
@@ -1218,7 +1806,22 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             const uint64_t cap = (0xffffff00ull / B.fixed_w) / kPaBlock * kPaBlock;
             subj = cap < sub ? uint32_t(cap < kPaBlock ? kPaBlock : cap) : sub;
         }
-        for (uint64_t s0 = 0; s0 < B.n; s0 += subj) {
+        // sub-batches of even size (a 17.6 M batch as 2 x 8.8 M, not 16 M +
+        // 1.6 M: a small last sub-batch cannot fill the chip)
+        if (B.n > subj) {
+            const uint64_t ns = (B.n + subj - 1) / subj;
+            subj = uint32_t(((B.n + ns - 1) / ns + kPaBlock - 1) / kPaBlock * kPaBlock);
+        }
+        // the segmented PFADD (k_seg_*) for this batch, or pass C per sub-batch
+        SegPlan P;
+        SegArgs S{};
+        const bool seg = flist && seg_use(A, so, nslots, B.n, subj, &P);
+        if (seg) {
+            e = seg_scratch(P, subj, B.n, scr, &S);
+            if (e != hipSuccess) return e;
+        }
+        uint32_t si = 0;
+        for (uint64_t s0 = 0; s0 < B.n; s0 += subj, si++) {
             const uint32_t ms = B.n - s0 < subj ? uint32_t(B.n - s0) : subj;
             A.fixed_w = B.fixed_w;
             A.n = ms;
@@ -1246,7 +1849,16 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
                 hipLaunchKernelGGL(k_part_b<1>, dim3(gb), dim3(kPbBlock), 0, st, A);
             if (hook) hook(hook_user, 1, 1, st);
             if (hook) hook(hook_user, 2, 0, st);
-            if (flist) {
+            if (seg) {
+                S.s = si;
+                S.nruns = (A.ntiles + kSegRunTiles - 1) / kSegRunTiles;
+                hipLaunchKernelGGL(k_seg_c1, dim3(std::min(S.nruns, unsigned(cus) * 2)), dim3(1024), 0, st, A, S);
+                if (hook) hook(hook_user, 2, 1, st);
+                if (hook) hook(hook_user, 3, 0, st);
+                hipLaunchKernelGGL(k_seg_scan, dim3(S.nb1), dim3(1024), 0, st, S);
+                hipLaunchKernelGGL(k_seg_d, dim3(unsigned(cus) * 2), dim3(1024), 0, st, S);
+                if (hook) hook(hook_user, 3, 1, st);
+            } else if (flist) {
                 const unsigned gc =
                     (part_grid(ms, 1024 * kPbGroup, unsigned(cus) * SKE_PC_BLOCKS_PER_CU) + kPGroups - 1) /
                     kPGroups * kPGroups;
@@ -1255,7 +1867,28 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
                 const unsigned gc = (part_grid(ms, kPcBlock * 2, unsigned(cus) * 8) + kPGroups - 1) / kPGroups * kPGroups;
                 hipLaunchKernelGGL(k_part_c<2>, dim3(gc), dim3(kPcBlock), 0, st, A);
             }
-            if (hook) hook(hook_user, 2, 1, st);
+            if (!seg && hook) hook(hook_user, 2, 1, st);
+            e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        if (seg) {
+            // every window of the slab once, after the batch's sub-batches:
+            // E1 (first slices), E2 (queued slices of cut windows), M (cut
+            // windows merged)
+            A.n = 0;
+            if (hook) hook(hook_user, 4, 0, st);
+            e = hipMemsetAsync(S.q, 0, 16, st);
+            if (e != hipSuccess) return e;
+            if (P.klog >= 3) {
+                hipLaunchKernelGGL((k_seg_e<3, false>), dim3(unsigned(cus)), dim3(1024), 0, st, A, S);
+                hipLaunchKernelGGL((k_seg_e<3, true>), dim3(unsigned(cus)), dim3(1024), 0, st, A, S);
+                hipLaunchKernelGGL(k_seg_m<3>, dim3(unsigned(cus)), dim3(1024), 0, st, A, S);
+            } else {
+                hipLaunchKernelGGL((k_seg_e<2, false>), dim3(unsigned(cus) * 2), dim3(1024), 0, st, A, S);
+                hipLaunchKernelGGL((k_seg_e<2, true>), dim3(unsigned(cus) * 2), dim3(1024), 0, st, A, S);
+                hipLaunchKernelGGL(k_seg_m<2>, dim3(unsigned(cus)), dim3(1024), 0, st, A, S);
+            }
+            if (hook) hook(hook_user, 4, 1, st);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
         }

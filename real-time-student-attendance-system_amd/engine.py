@@ -15,6 +15,8 @@ import numpy as np
 from ._lib import Context, GenParams, SKE_MEM_DEVICE
 from . import synthetic
 
+PASS_KINDS = 6  # SKE_PASS_KINDS (include/sketch.h)
+
 
 class DeviceBuffer:
     def __init__(self, ctx: Context, nbytes: int):
@@ -219,11 +221,12 @@ class SketchEngine:
     def pass_times(self, reset: bool = True) -> list[tuple[float, int]]:
         """(summed ms, kernel count) per K1 pass kind, from the HIP event
         pairs the library records around each kernel while the option
-        "pass_timing" is on: [single-kernel K1, partitioned A, B, C]."""
-        ms = (C.c_double * 4)()
-        cnt = (C.c_uint64 * 4)()
+        "pass_timing" is on: [single-kernel K1, partitioned A, B, C (or the
+        segmented C1), segmented level-2 sort, segmented window apply]."""
+        ms = (C.c_double * PASS_KINDS)()
+        cnt = (C.c_uint64 * PASS_KINDS)()
         self.ctx.call("ske_pass_times", ms, cnt, 1 if reset else 0)
-        return [(ms[i], cnt[i]) for i in range(4)]
+        return [(ms[i], cnt[i]) for i in range(PASS_KINDS)]
 
     def set_stream(self, stream_ptr: int | None):
         self.ctx.call("ske_set_stream", C.c_void_p(stream_ptr) if stream_ptr else None)
