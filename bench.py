@@ -123,6 +123,12 @@ def parse(argv=None):
                          "config's step swipes, each rank's batch the probability mass of the keys "
                          "it owns (the fixed 1B-event stream of north_star, cut per step); "
                          "equal = every rank the config's step swipes over its own keys")
+    ap.add_argument("--rollup", type=int, default=-1,
+                    help="1: after the K1 steps, time the rankings / campus PFMERGE over the registers "
+                         "(ShardedSketch; default on for --config c5)")
+    ap.add_argument("--host-fed", type=int, default=1,
+                    help="N = 1: also time one 16M-swipe sample handed over in host memory (PCIe-inclusive, "
+                         "pageable / pinned / fixed-width 1-bit answers), reported as host_fed, never value")
     ap.add_argument("--shard", type=int, default=0,
                     help="N > 0: run ONE rank's share of an N-rank job on this GPU (its owned keys and, "
                          "with --shares mass, its batch), to measure the per-GPU work of the N-GPU "
@@ -263,6 +269,186 @@ def cpu_baseline(orc, chain, w, b0, seconds, key_name):
                                  "sample": f"{m} JSON messages: json.loads + fromisoformat + "
                                            "oracle BF.EXISTS / PFADD per event "
                                            "(attendance_processor.py:100-137 without transport)"}}
+
+
+def host_fed(engine, batch, reps=3, cap=1 << 24):
+    """SURVEY §7 item 8 / DESIGN §4: the PCIe-inclusive rate -- the same
+    swipes handed over in HOST memory (the reference's loop is fed from the
+    host, attendance_processor.py:101-113): ske_swipes(..., SKE_MEM_HOST)
+    stages ids, offsets and slots host -> device, runs K1 and copies the
+    answers back; ske_swipes_fixed_bits the fixed-width form with 1-bit
+    answers.  Pageable numpy and pinned torch buffers; median of `reps`
+    synchronous calls over the first min(n, cap) swipes of the batch.  Never
+    `value` (that one starts with the batch resident in HBM).  Answers are
+    compared with the device-resident call's."""
+    import numpy as np
+    import torch
+    from rtsas_amd._lib import SKE_MEM_HOST
+    from rtsas_amd.engine import DeviceBuffer
+    buf, offs, slot = batch.to_host()
+    n = min(len(offs) - 1, cap)
+    width = int(offs[1] - offs[0])
+    fixed = bool(np.all(np.diff(offs[:n + 1]) == width))
+    buf = np.ascontiguousarray(buf[:int(offs[n]) + 16])
+    offs = np.ascontiguousarray(offs[:n + 1])
+    slot = np.ascontiguousarray(slot[:n].astype(np.uint32))
+    ref = DeviceBuffer(engine.ctx, n)
+    ptr = lambda a: C.c_void_p(a.ctypes.data if isinstance(a, np.ndarray) else a.data_ptr())
+    engine.ctx.call("ske_swipes", 0, C.c_void_p(batch.slot.ptr), C.c_void_p(batch.bytes.ptr),
+                    C.c_void_p(batch.offs.ptr), n, C.c_void_p(ref.ptr), 1)  # SKE_MEM_DEVICE
+    want = ref.to_host(np.uint8, n)
+    ref.free()
+
+    def timed(call):
+        call()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            call()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts))
+
+    out = {"swipes": n, "what": "ske_swipes(..., SKE_MEM_HOST): H2D of ids + offsets + slots, K1, D2H of the "
+                                "answers, synchronous; median of %d calls" % reps}
+
+    def offsets_form(b, o, sl, ans, label):
+        t = timed(lambda: engine.ctx.call("ske_swipes", 0, ptr(sl), ptr(b), ptr(o), n, ptr(ans), SKE_MEM_HOST))
+        got = ans if isinstance(ans, np.ndarray) else ans.numpy()
+        out[label] = {"swipes_per_s": n / t, "ms": t * 1e3,
+                      "host_GBps": (b.nbytes + o.nbytes + sl.nbytes + n) / t / 1e9,
+                      "answers_equal": bool(np.array_equal(got, want))}
+
+    offsets_form(buf, offs, slot, np.zeros(n, np.uint8), "pageable")
+    pb, po, ps = (torch.from_numpy(x).pin_memory() for x in (buf, offs, slot))
+    pans = torch.zeros(n, dtype=torch.uint8).pin_memory()
+    offsets_form(pb, po, ps, pans, "pinned")
+    if fixed:
+        ids = np.ascontiguousarray(buf[:n * width])
+        bits = np.zeros((n + 7) // 8, np.uint8)
+        pid = torch.from_numpy(ids).pin_memory()
+        pbits = torch.zeros((n + 7) // 8, dtype=torch.uint8).pin_memory()
+        for label, i_, s_, b_ in (("fixed_bits_pageable", ids, slot, bits), ("fixed_bits_pinned", pid, ps, pbits)):
+            t = timed(lambda: engine.ctx.call("ske_swipes_fixed_bits", 0, ptr(s_), ptr(i_), width, n, ptr(b_),
+                                              SKE_MEM_HOST))
+            got = b_ if isinstance(b_, np.ndarray) else b_.numpy()
+            out[label] = {"swipes_per_s": n / t, "ms": t * 1e3,
+                          "host_GBps": (n * width + 4 * n + (n + 7) // 8) / t / 1e9,
+                          "answers_equal": bool(np.array_equal(np.unpackbits(got, count=n, bitorder="little"),
+                                                               want))}
+    return out
+
+
+def rollup_bench(run, dist, reps=3):
+    """C5's query side after the K1 steps (attendance_analysis.py:87-97 in
+    PFCOUNT form, README.md:179): through distributed.ShardedSketch
+    planned queries -- PFCOUNT of every lecture-day key, the per-lecture
+    union of its day keys (K2 per group at N = 1; K3 + reduce_scatter MAX +
+    K2 at N > 1), the campus-wide PFMERGE of every key, and the top / bottom-3
+    lectures.  Best of `reps` after one untimed call; wall time around each
+    query (host staging included).  Checked against the oracle's estimator
+    (oracle hll_count_regs) over the device registers of sampled lectures and
+    keys, and of the campus union recomputed with torch amax."""
+    import numpy as np
+    import torch
+    import rtsas_amd
+    from rtsas_amd.distributed import ShardedSketch
+    from rtsas_amd.processor import rank_top_bottom
+    w = run.w_all
+    L, D = w.zipf_lectures, w.zipf_days
+    world, rank, dev = run.world, run.rank, run.dev
+    client = rtsas_amd.SketchClient(context=run.engine.ctx)
+    sk = ShardedSketch(client, rank, world)
+    km = run.km
+    groups = [np.arange(l * D, (l + 1) * D) for l in range(L)]
+    plan = sk.plan(km, groups)
+    allk = np.arange(len(km))
+    scratch = run.sinks[0 if run.args.shard else run.kr] + 1
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    def timed(fn):
+        out = fn()
+        best = 1e30
+        for _ in range(reps):
+            barrier()
+            t0 = time.perf_counter()
+            out = fn()
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t0)
+        t = torch.tensor([best], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0]), out
+
+    t_each, each = timed(lambda: sk.pfcount_each_planned(km, allk))
+    t_groups, lect = timed(lambda: sk.rollup_planned(plan))
+    t_merge, (campus, row) = timed(lambda: sk.pfmerge_planned(km, allk, scratch))
+    names = [f"LECT{l:05d}" for l in range(L)]
+    t0 = time.perf_counter()
+    head, tail = rank_top_bottom(lect.astype(np.int64), names, 3)
+    t_rank = time.perf_counter() - t0
+    # ---- checks: the oracle's estimator over the device registers
+    orc = __import__("__graft_entry__").load_oracle()
+    p_, nb = C.c_void_p(), C.c_uint64()
+    run.engine.ctx.call("ske_hll_slab", C.byref(p_), C.byref(nb))
+    nmine = km.count(run.kr)
+
+    class _V:
+        __cuda_array_interface__ = {"shape": (max(1, nmine), 16384), "typestr": "|u1", "data": (p_.value, False),
+                                    "version": 3, "strides": None}
+    slab = torch.as_tensor(_V(), device=dev)
+    cdev = dev if dist.is_initialized() and dist.get_backend() == "nccl" else "cpu"
+
+    def global_max(rows):
+        t = rows.to(cdev) if cdev == "cpu" else rows
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.cpu().numpy()
+
+    ok_l = True
+    for l in sorted({0, 1, L // 2, L - 1}):
+        g = groups[l]
+        mine = g[km.owner[g] == rank]
+        r = slab[torch.from_numpy(km.local[mine].astype(np.int64)).to(dev)].amax(0) if mine.size else \
+            torch.zeros(16384, dtype=torch.uint8, device=dev)
+        ok_l &= orc.hll_count_regs(global_max(r.reshape(1, -1))[0]) == int(lect[l])
+    rng = np.random.default_rng(11)
+    sample = rng.choice(len(km), size=64, replace=False)
+    want = np.zeros(64, np.int64)
+    for i, g in enumerate(sample):
+        if km.owner[g] == rank:
+            want[i] = orc.hll_count_regs(slab[int(km.local[g])].cpu().numpy())
+    wt = torch.from_numpy(want)
+    if world > 1:
+        wt = wt.to(cdev)
+        dist.all_reduce(wt, op=dist.ReduceOp.SUM)
+    ok_e = bool(np.array_equal(wt.cpu().numpy().astype(np.uint64), each[sample]))
+    u = torch.zeros(16384, dtype=torch.uint8, device=dev)
+    for a in range(0, nmine, 1 << 16):
+        u = torch.maximum(u, slab[a:min(nmine, a + (1 << 16))].amax(0))
+    ug = global_max(u.reshape(1, -1))[0]
+    ok_m = bool(np.array_equal(ug, row.cpu().numpy()[0])) and orc.hll_count_regs(ug) == campus
+    order = np.lexsort((np.arange(L), -lect.astype(np.int64)))
+    ok_r = list(head) == [int(i) for i in order[:3]] and list(tail) == [int(i) for i in order[-3:]]
+    ok = torch.tensor([int(ok_l and ok_e and ok_m and ok_r)], device=cdev)
+    if world > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    slab_rank = nmine * 16384
+    return {"each_ms": t_each * 1e3, "groups_ms": t_groups * 1e3, "merge_ms": t_merge * 1e3,
+            "rank_ms": t_rank * 1e3, "ok": bool(ok.item()),
+            "checks": {"sampled_lecture_unions": bool(ok_l), "sampled_key_counts": ok_e,
+                       "campus_pfmerge": ok_m, "top_bottom_3": ok_r},
+            "keys": len(km), "lectures": L, "days": D, "slab_GB_this_gpu": slab_rank / 1e9,
+            "GBps_this_gpu": {"each": slab_rank / t_each / 1e9, "groups": slab_rank / t_groups / 1e9,
+                              "merge": slab_rank / t_merge / 1e9},
+            "campus_pfcount": campus, "top3": {names[i]: int(lect[i]) for i in head},
+            "bottom3": {names[i]: int(lect[i]) for i in tail},
+            "what": "ShardedSketch planned queries over this run's registers; wall time per query, best "
+                    "of %d (host staging of the plan's slot arrays included); checked with the oracle's "
+                    "estimator over device registers" % reps}
 
 
 def checked(fn, *a, **k):
@@ -486,7 +672,7 @@ class Run:
         # to 2 x VERIFY_KEYS slots), then the exchange's sink slot (padding
         # rows of SwipeExchange.swipes_async; no key lives there)
         self.sinks = [self.km.slots_end(r) + 2 * VERIFY_KEYS for r in range(kw)]
-        engine.hll_reserve(self.sinks[kr] + 1)
+        engine.hll_reserve(self.sinks[kr] + 2)  # + the rollup's PFMERGE scratch slot
         if args.shard:  # verify() runs as one rank above this shard's slots
             self.sinks = [self.sinks[kr]]
             self.km_verify = _ShardView(self.km.slots_end(kr))
@@ -902,6 +1088,10 @@ def main():
         # cap_rows_per_peer / slack_used: what the timed steps were enqueued
         # with; slack_next: what settle() adapted it to for later batches
         line["exchange"] = {**run.ex.stats, "slack_next": run.ex.slack}
+    if (args.rollup if args.rollup >= 0 else args.config == "c5") and not args.shard and run.w_all.zipf_lectures:
+        line["rollup"] = checked(rollup_bench, run, dist)
+    if world == 1 and args.host_fed and not run.lds_k1:
+        line["host_fed"] = checked(host_fed, run.engine, run.batches[0])
     want_cpu = rank == 0 and world == 1 and not args.no_cpu and args.cpu_seconds > 0
     if not args.no_check or want_cpu:
         orc = ge.load_oracle()

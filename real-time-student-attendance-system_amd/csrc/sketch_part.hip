@@ -1402,18 +1402,36 @@ __device__ __forceinline__ bool seg_lds_max(uint32_t *w, uint32_t sh, uint32_t r
 // each slice of a cut window raises its own LDS copy of the window, stored
 // whole to a copy buffer, and M (k_seg_m) stores the byte max of the copies.
 // An uncut window's risen lines go straight back to the slab.
+//
+// Per window the block (1) issues the window's register loads (whole lines,
+// 8 x 16 B per thread, kept in registers) and, at the same time, (2) reads
+// the window's run table -- o2[chunk][window] of every chunk of its bucket
+// in every sub-batch, the chunk bases from an LDS copy of cb -- then (3)
+// reads the records 16 consecutive ones per thread (one search of the run
+// prefix per thread, all 16 loads in flight), raises them in LDS and (4)
+// stores the risen lines.  A window with fewer than dense_min records is
+// raised in place instead (its register loads are dropped).
+constexpr uint32_t kSegCbLds = 2048;  // cb words kept in LDS (nsub * (nb1 + 1)); more: read from L2
 template <int KLOG, bool QUEUE>
 __global__ void __launch_bounds__(1024, KLOG >= 3 ? 4 : 8) k_seg_e(const PartArgs A, const SegArgs S) {
     constexpr uint32_t KW = 1u << KLOG, WB = KW << kHllP, NPC = WB / 16 / 1024;  // 16-B pieces per thread
     constexpr uint32_t NL = KW * (kHllRegs / 128);                                 // 128-B lines
-    constexpr uint32_t PIECE = 1024;                                               // records per wave piece
+    // (windows of 4 keys: two blocks per CU, so under 80 KiB of LDS and 64 VGPRs)
+    constexpr uint32_t RPT = KLOG >= 3 ? 16 : 8;               // records per thread per round
+    constexpr uint32_t EP = KLOG >= 3 ? kSegEPairs : kSegEPairs / 2;
+    constexpr uint32_t CBL = KLOG >= 3 ? kSegCbLds : kSegCbLds / 2;
     __shared__ __attribute__((aligned(16))) uint8_t win[WB];
     __shared__ uint8_t dirty[NL];
-    __shared__ uint32_t rbase[kSegEPairs], rlen[kSegEPairs], rpre[kSegEPairs];
+    __shared__ uint32_t rb[EP], rp[EP + 1];
+    __shared__ uint32_t cbs[CBL];
     __shared__ uint32_t spre[65], ws[16], hdr[2];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t wpb = 1u << S.wlog;
-    const __amdgpu_buffer_rsrc_t rr2 = part_rsrc(S.r2, S.nsub * S.maxch * kSegChunk * 4);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wpb = 1u << S.wlog, cbw = S.nsub * (S.nb1 + 1);
+    const bool cbl = cbw <= CBL;
+    if (cbl)
+        for (uint32_t j = tid; j < cbw; j += 1024) cbs[j] = S.cb[j];
+    const uint32_t *cbp = cbl ? cbs : S.cb;
+    lds_barrier();
     const uint32_t nitems = QUEUE ? S.q[0] : S.nwin;
     for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
         uint32_t wi, sl = 0, copy = 0xffffffffu;
@@ -1428,148 +1446,143 @@ __global__ void __launch_bounds__(1024, KLOG >= 3 ? 4 : 8) k_seg_e(const PartArg
         const uint32_t h = wi >> S.wlog, w2 = wi & (wpb - 1);
         const uint32_t slot0 = wi << KLOG;
         const uint32_t nk = A.nslots - slot0 < KW ? A.nslots - slot0 : KW;
-        // the window's runs: pair x = (sub-batch s, chunk q of bucket h in
-        // s), in that order; spre = prefix of the sub-batches' chunk counts
+        uint8_t *g = A.regs + (size_t(slot0) << kHllP);
+        const uint32_t npc = nk << (kHllP - 4);  // the window's 16-B pieces in the slab
+        // (1) the window's registers, in flight while its run table is read
+        part_u32x4 v[NPC];
+#pragma unroll
+        for (uint32_t i = 0; i < NPC; i++) {
+            const uint32_t j = i * 1024 + tid;
+            v[i] = j < npc ? reinterpret_cast<const part_u32x4 *>(g)[j] : part_u32x4{0, 0, 0, 0};
+        }
+        // (2) runs: pair x = (sub-batch s, chunk q of bucket h in s), in that
+        // order; spre = prefix of the sub-batches' chunk counts (nsub <= 64)
         uint32_t np;
         {
-            uint32_t v = 0;
-            if (tid < S.nsub)
-                v = S.cb[size_t(tid) * (S.nb1 + 1) + h + 1] - S.cb[size_t(tid) * (S.nb1 + 1) + h];
-            const uint32_t ex = seg_scan(v, ws, np);
+            uint32_t c = 0;
+            if (tid < S.nsub) c = cbp[tid * (S.nb1 + 1) + h + 1] - cbp[tid * (S.nb1 + 1) + h];
+            const uint32_t ex = seg_scan(c, ws, np);
             if (tid < S.nsub) spre[tid] = ex;
         }
         lds_barrier();
         auto run_of = [&](uint32_t x, uint32_t &base) -> uint32_t {
             const uint32_t s = seg_last_le(spre, S.nsub, x);
-            const uint32_t q = S.cb[size_t(s) * (S.nb1 + 1) + h] + (x - spre[s]);
+            const uint32_t q = cbp[s * (S.nb1 + 1) + h] + (x - spre[s]);
             const size_t row = size_t(s) * S.maxch + q;
             const uint32_t *o = S.o2 + row * (wpb + 1) + w2;
             const uint32_t b = o[0];
             base = uint32_t(row * kSegChunk + b);  // < 2^32: the host plan checks nsub * maxch * kSegChunk
             return o[1] - b;
         };
-        uint32_t nrec = 0;
-        for (uint32_t x0 = 0; x0 < np; x0 += 1024) {
-            uint32_t base, len = 0, t;
+        // the record count (the first batch of runs is kept staged)
+        uint32_t nrec = 0, nrec0 = 0;
+        for (uint32_t x0 = 0; x0 < np; x0 += EP) {
+            uint32_t base = 0, len = 0, t;
             if (x0 + tid < np) len = run_of(x0 + tid, base);
-            (void)seg_scan(len, ws, t);
+            const uint32_t ex = seg_scan(len, ws, t);
+            if (x0 == 0 && tid < EP) {
+                rb[tid] = base;
+                rp[tid] = ex;
+                if (tid == 0) rp[np < EP ? np : EP] = t;
+                nrec0 = t;
+            }
             nrec += t;
         }
         if (nrec == 0) continue;  // block-uniform
-        uint32_t nsl = 1;
-        if (!QUEUE) {
-            nsl = (nrec + kSegSlice - 1) / kSegSlice;
-            if (nsl > 1) {
-                if (tid == 0) {
-                    uint32_t base = atomicAdd(&S.q[1], nsl);
-                    if (base + nsl > S.ccap) {
-                        base = 0xffffffffu;  // out of copies (cannot happen: see seg_scratch): one slice
-                    } else {
-                        const uint32_t qp = atomicAdd(&S.q[0], nsl - 1);
-                        for (uint32_t k = 1; k < nsl; k++) S.qitems[qp + k - 1] = make_uint4(wi, k, base + k, 0);
-                        S.mlist[atomicAdd(&S.q[2], 1u)] = make_uint4(wi, base, nsl, 0);
-                    }
-                    hdr[0] = base;
+        if (!QUEUE && nrec > kSegSlice) {
+            // a hot window: cut into slices, the others queued for E2
+            const uint32_t nsl = (nrec + kSegSlice - 1) / kSegSlice;
+            if (tid == 0) {
+                uint32_t base = atomicAdd(&S.q[1], nsl);
+                if (base + nsl > S.ccap) {
+                    base = 0xffffffffu;  // out of copies (cannot happen: see seg_scratch): one slice
+                } else {
+                    const uint32_t qp = atomicAdd(&S.q[0], nsl - 1);
+                    for (uint32_t k = 1; k < nsl; k++) S.qitems[qp + k - 1] = make_uint4(wi, k, base + k, 0);
+                    S.mlist[atomicAdd(&S.q[2], 1u)] = make_uint4(wi, base, nsl, 0);
                 }
-                lds_barrier();
-                copy = hdr[0];
-                if (copy == 0xffffffffu) nsl = 1;
-                lds_barrier();  // hdr is rewritten by the next window
+                hdr[0] = base;
             }
+            lds_barrier();
+            copy = hdr[0];
         }
         const bool cut = copy != 0xffffffffu;
         const uint32_t lo = cut ? sl * kSegSlice : 0;
         const uint32_t hi = cut ? (nrec - lo < kSegSlice ? nrec : lo + kSegSlice) : nrec;
         const bool dense = cut || nrec >= S.dense_min;
-        uint8_t *g = A.regs + (size_t(slot0) << kHllP);
-        const uint32_t npc = nk << (kHllP - 4);  // the window's 16-B pieces in the slab
         if (dense) {
-            // the window's registers into LDS, whole lines, all in flight
-            part_u32x4 v[NPC];
-#pragma unroll
-            for (uint32_t i = 0; i < NPC; i++) {
-                const uint32_t j = i * 1024 + tid;
-                v[i] = j < npc ? reinterpret_cast<const part_u32x4 *>(g)[j] : part_u32x4{0, 0, 0, 0};
-            }
             for (uint32_t j = tid; j < NL; j += 1024) dirty[j] = 0;
 #pragma unroll
             for (uint32_t i = 0; i < NPC; i++) reinterpret_cast<part_u32x4 *>(win)[i * 1024 + tid] = v[i];
         }
-        // records [lo, hi) of the window's concatenated runs, in pieces of up
-        // to PIECE records of one run (aligned to 4 records), one per wave
-        uint32_t p0 = 0;  // records of the runs before this batch
-        for (uint32_t x0 = 0; x0 < np && p0 < hi; x0 += kSegEPairs) {
-            const uint32_t nx = np - x0 < kSegEPairs ? np - x0 : kSegEPairs;
-            uint32_t npieces, btot;
-            {
+        // (3) records [lo, hi) of the concatenated runs, RPT consecutive ones
+        // per thread and round; runs staged kSegEPairs at a time
+        for (uint32_t x0 = 0, p0 = 0; x0 < np && p0 < hi; x0 += EP) {
+            const uint32_t nx = np - x0 < EP ? np - x0 : EP;
+            uint32_t btot = nrec0;
+            if (x0 > 0) {  // (a window with more than kSegEPairs runs: restage)
+                lds_barrier();
                 uint32_t base = 0, len = 0;
                 if (tid < nx) len = run_of(x0 + tid, base);
-                const uint32_t pre = p0 + seg_scan(len, ws, btot);
-                // this run's part of [lo, hi), as absolute r2 indices [b, e)
-                const uint32_t a = pre > lo ? pre : lo, z = pre + len < hi ? pre + len : hi;
-                uint32_t pc = 0, b = 0, e = 0;
-                if (a < z) {
-                    b = base + (a - pre);
-                    e = base + (z - pre);
-                    pc = (e - (b & ~3u) + PIECE - 1) / PIECE;
-                }
-                const uint32_t ex = seg_scan(pc, ws, npieces);
+                const uint32_t ex = seg_scan(len, ws, btot);
                 if (tid < nx) {
-                    rbase[tid] = b;
-                    rlen[tid] = e;
-                    rpre[tid] = ex;
+                    rb[tid] = base;
+                    rp[tid] = ex;
                 }
+                if (tid == 0) rp[nx] = btot;
             }
             lds_barrier();  // (the window's LDS image is complete here too)
-            for (uint32_t pc = wave; pc < npieces; pc += 16) {
-                const uint32_t j = seg_last_le(rpre, nx, pc);
-                const uint32_t b = rbase[j], e = rlen[j];
-                const uint32_t x = (b & ~3u) + (pc - rpre[j]) * PIECE;
-                part_u32x4 r[PIECE / 256];
+            // this batch's records [p0, p0 + btot) of the window; ours: [lo, hi)
+            const uint32_t f_lo = lo > p0 ? lo - p0 : 0, f_hi = hi - p0 < btot ? hi - p0 : btot;
+            for (uint32_t f0 = f_lo + tid * RPT; f0 - tid * RPT < f_hi; f0 += 1024 * RPT) {
+                uint32_t rec[RPT];
+                if (f0 < f_hi) {
+                    uint32_t j = seg_last_le(rp, nx, f0);
 #pragma unroll
-                for (uint32_t i = 0; i < PIECE / 256; i++) {
-                    const uint32_t xi = x + i * 256 + lane * 4;
-                    r[i] = __builtin_bit_cast(part_u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                             rr2, xi < e ? xi * 4 : kOOR, 0, 0));
+                    for (uint32_t c = 0; c < RPT; c++) {
+                        const uint32_t f = f0 + c;
+                        rec[c] = 0;
+                        if (f < f_hi) {
+                            while (rp[j + 1] <= f) j++;
+                            rec[c] = S.r2[rb[j] + (f - rp[j])];
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (uint32_t c = 0; c < RPT; c++) rec[c] = 0;
                 }
 #pragma unroll
-                for (uint32_t i = 0; i < PIECE / 256; i++) {
-#pragma unroll
-                    for (uint32_t c = 0; c < 4; c++) {
-                        const uint32_t xi = x + i * 256 + lane * 4 + c;
-                        const uint32_t rec = r[i][c];
-                        const uint32_t rank = rec & 63u;
-                        if (xi < b || xi >= e || rank == 0) continue;
-                        const uint32_t ad = (((rec >> kSegRecShift) & (KW - 1)) << kHllP) | ((rec >> 6) & 0x3fffu);
-                        if (dense) {
-                            if (seg_lds_max(reinterpret_cast<uint32_t *>(win + (ad & ~3u)), (ad & 3u) * 8, rank))
-                                dirty[ad >> 7] = 1;
-                        } else {
-                            uint32_t *w = reinterpret_cast<uint32_t *>(g + (ad & ~3u));
-                            part_reg_max(w, (ad & 3u) * 8, rank, *w);
-                        }
+                for (uint32_t c = 0; c < RPT; c++) {
+                    const uint32_t rank = rec[c] & 63u;
+                    if (rank == 0) continue;
+                    const uint32_t ad = (((rec[c] >> kSegRecShift) & (KW - 1)) << kHllP) | ((rec[c] >> 6) & 0x3fffu);
+                    if (dense) {
+                        if (seg_lds_max(reinterpret_cast<uint32_t *>(win + (ad & ~3u)), (ad & 3u) * 8, rank))
+                            dirty[ad >> 7] = 1;
+                    } else {
+                        uint32_t *w = reinterpret_cast<uint32_t *>(g + (ad & ~3u));
+                        part_reg_max(w, (ad & 3u) * 8, rank, *w);
                     }
                 }
             }
             p0 += btot;
-            lds_barrier();  // rbase / rlen / rpre are rewritten by the next batch of runs
         }
+        lds_barrier();  // every raise in LDS done
         if (cut) {
             // a slice of a cut window: the whole LDS copy, merged by k_seg_m
             part_u32x4 *dst = reinterpret_cast<part_u32x4 *>(S.copies + size_t(copy) * WB);
 #pragma unroll
             for (uint32_t i = 0; i < NPC; i++) dst[i * 1024 + tid] = reinterpret_cast<const part_u32x4 *>(win)[i * 1024 + tid];
-            lds_barrier();
         } else if (dense) {
-            // the lines that rose, stored back whole
+            // (4) the lines that rose, stored back whole
 #pragma unroll
             for (uint32_t i = 0; i < NPC; i++) {
                 const uint32_t j = i * 1024 + tid;
                 if (j < npc && dirty[j >> 3])
                     reinterpret_cast<part_u32x4 *>(g)[j] = reinterpret_cast<const part_u32x4 *>(win)[j];
             }
-            lds_barrier();  // the next window's image overwrites win
         }
+        lds_barrier();  // win, dirty, rb, rp and hdr are rewritten by the next window
     }
 }
 

@@ -257,6 +257,118 @@ class ShardedSketch:
         return torch.cat([g.cpu() for g in gathered]).numpy()[:G].astype(np.uint64)
 
 
+    # ---- planned queries: keys named by their global index in a KeyMap,
+    # the name -> slot resolution done once (plan), the query itself only
+    # device work and one collective (C5's rankings,
+    # attendance_analysis.py:87-97 in PFCOUNT form, and the campus PFMERGE)
+    def plan(self, keymap: KeyMap, groups: Sequence) -> dict:
+        """This rank's part of every group of global key indices: the local
+        slots of the keys it owns, groups padded to a multiple of world (the
+        reduce_scatter split).  Slots and offsets are kept on the device too."""
+        import torch
+        G = len(groups)
+        per = -(-G // self.world) if G else 0
+        own, loc = keymap.owner, keymap.local
+        parts, goffs = [], [0]
+        for g in groups:
+            g = np.asarray(g, np.int64)
+            m = g[own[g] == self.rank] if g.size else g
+            parts.append(loc[m].astype(np.uint32))
+            goffs.append(goffs[-1] + int(m.size))
+        goffs += [goffs[-1]] * (per * self.world - G)
+        slots = np.concatenate(parts) if parts else np.zeros(0, np.uint32)
+        dev = self.ops.device
+        return {"G": G, "per": per, "slots": slots, "goffs": np.asarray(goffs, np.uint32),
+                "slots_dev": torch.from_numpy(slots.view(np.int32) if slots.size else np.zeros(1, np.int32)).to(dev),
+                "goffs_dev": torch.from_numpy(np.asarray(goffs, np.uint32).view(np.int32)).to(dev)}
+
+    def rollup_planned(self, plan: dict) -> np.ndarray:
+        """rollup() of a plan: one union count per group.  One rank: the
+        fused per-group K2 (merge + estimator, device arrays); N ranks: K3
+        per group into a [groups, 16384] tensor, reduce_scatter MAX (RCCL),
+        K2 estimator on this rank's share, all_gather of the counts."""
+        import torch
+        G, per = plan["G"], plan["per"]
+        if self.solo:
+            out = torch.zeros(max(1, G), dtype=torch.int64, device=self.ops.device)
+            if G:
+                self.client.ctx.call("ske_hll_pfcount_groups", C.c_void_p(plan["slots_dev"].data_ptr()),
+                                     C.c_void_p(plan["goffs_dev"].data_ptr()), G, C.c_void_p(out.data_ptr()), 1)
+            return out[:G].cpu().numpy().astype(np.uint64)
+        t = torch.zeros((per * self.world, HLL_REGISTERS), dtype=torch.uint8, device=self.ops.device)
+        if per:
+            self.torch_sync()
+            self.client.ctx.call("ske_hll_merge_groups_dev", plan["slots"].ctypes.data_as(C.c_void_p),
+                                 plan["goffs"].ctypes.data_as(C.c_void_p), per * self.world,
+                                 C.c_void_p(t.data_ptr()))
+        if self.use_reduce_scatter:
+            mine = torch.empty((per, HLL_REGISTERS), dtype=t.dtype, device=t.device)
+            self.dist.reduce_scatter_tensor(mine, t, op=self._max(), group=self.group)
+        else:
+            self._all_reduce(t, self._max())
+            mine = t[self.rank * per:(self.rank + 1) * per].contiguous()
+        local = torch.from_numpy(self.ops.count_raw(mine).astype(np.int64))
+        if self.use_reduce_scatter:
+            local = local.to(t.device)
+        gathered = [torch.zeros_like(local) for _ in range(self.world)]
+        self.dist.all_gather(gathered, local, group=self.group)
+        return torch.cat([g.cpu() for g in gathered]).numpy()[:G].astype(np.uint64)
+
+    def pfcount_each_planned(self, keymap: KeyMap, gidx: np.ndarray) -> np.ndarray:
+        """PFCOUNT of every key of gidx (global indices): each rank counts its
+        own keys (K2 per key, device arrays), all_reduce SUM of the counts."""
+        import torch
+        gidx = np.asarray(gidx, np.int64)
+        mine = np.nonzero(keymap.owner[gidx] == self.rank)[0]
+        dev = self.ops.device
+        counts = torch.zeros(max(1, gidx.size), dtype=torch.int64, device=dev)
+        if mine.size:
+            sl = torch.from_numpy(keymap.local[gidx[mine]].astype(np.uint32).view(np.int32)).to(dev)
+            out = torch.zeros(mine.size, dtype=torch.int64, device=dev)
+            self.client.ctx.call("ske_hll_pfcount_each", C.c_void_p(sl.data_ptr()), int(mine.size),
+                                 C.c_void_p(out.data_ptr()), 1)
+            counts[torch.from_numpy(mine).to(dev)] = out
+        if not self.solo:
+            self._all_reduce_sum(counts)
+        return counts[:gidx.size].cpu().numpy().astype(np.uint64)
+
+    def pfmerge_planned(self, keymap: KeyMap, gidx: np.ndarray, scratch_slot: int) -> tuple:
+        """The campus PFMERGE of every key of gidx: each rank merges its own
+        keys into `scratch_slot` (cleared first; the two-level K3), the
+        16 KiB rows are max-reduced (all_reduce MAX) and counted.  Returns
+        (PFCOUNT of the union, the union's registers as a uint8 tensor)."""
+        import torch
+        gidx = np.asarray(gidx, np.int64)
+        mine = gidx[keymap.owner[gidx] == self.rank]
+        src = np.ascontiguousarray(keymap.local[mine].astype(np.uint32))
+        ctx = self.client.ctx
+        ctx.call("ske_hll_clear", int(scratch_slot))
+        if src.size:
+            ctx.call("ske_hll_pfmerge", int(scratch_slot), src.ctypes.data_as(C.c_void_p), int(src.size))
+        p, nb = C.c_void_p(), C.c_uint64()
+        ctx.call("ske_hll_slab", C.byref(p), C.byref(nb))
+        row = torch.empty((1, HLL_REGISTERS), dtype=torch.uint8, device=self.ops.device)
+        self.torch_sync()
+        ctx.call("ske_memcpy", C.c_void_p(row.data_ptr()), C.c_void_p(p.value + int(scratch_slot) * HLL_REGISTERS),
+                 HLL_REGISTERS, 3)
+        self._all_reduce(row, self._max())
+        return int(self.ops.count_raw(row)[0]), row
+
+    def torch_sync(self):
+        import torch
+        if self.ops.device.type == "cuda":
+            torch.cuda.synchronize(self.ops.device)
+
+    def _all_reduce_sum(self, t):
+        if self.use_reduce_scatter or t.device.type == "cpu":
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+            return t
+        h = t.cpu()
+        self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM, group=self.group)
+        t.copy_(h)
+        return t
+
+
 class SwipeExchange:
     """Swipes that arrive NOT partitioned by key owner ("if
     input is not pre-partitioned, use one alltoallv per batch").
