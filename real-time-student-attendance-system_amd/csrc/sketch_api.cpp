@@ -826,7 +826,7 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
         return SKE_OK;
     }
     if (!strcmp(name, "seg_klog")) {  // keys per window 2^klog
-        if (value != 2 && value != 3) return SKE_EINVAL;
+        if (value < 0 || value > 3) return SKE_EINVAL;
         c->seg.klog = int(value);
         return SKE_OK;
     }
@@ -1535,6 +1535,13 @@ int ske_diag_set_pb_stamp_buffer(ske_ctx *c, void *dev_ptr) {
 int ske_diag_set_k1_stamp_buffer(ske_ctx *c, void *dev_ptr) {
     if (!c) return SKE_EINVAL;
     HIPCHK(c, ske::set_k1_stamp_buffer(dev_ptr));
+    return SKE_OK;
+}
+#endif
+#ifdef SKE_SEG_STAMPS
+int ske_diag_set_seg_stamp_buffer(ske_ctx *c, void *dev_ptr) {
+    if (!c) return SKE_EINVAL;
+    HIPCHK(c, ske::set_seg_stamp_buffer(dev_ptr));
     return SKE_OK;
 }
 #endif

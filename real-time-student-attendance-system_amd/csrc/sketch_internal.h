@@ -98,6 +98,7 @@ hipError_t launch_swipes_lds(const K1Args &A, bool hll, int tile, int cus, hipSt
 hipError_t k1_lds_setup();
 hipError_t set_k1_stamp_buffer(void *p);  // -DSKE_STAMPS diagnostic build only
 hipError_t set_pb_stamp_buffer(void *p);  // -DSKE_STAMPS diagnostic build only
+hipError_t set_seg_stamp_buffer(void *p);  // -DSKE_SEG_STAMPS diagnostic build only
 
 // sketch_ingest.hip -- JSON event decode and key-slot resolution (device columns)
 struct IngestCols {
@@ -145,7 +146,7 @@ struct SegOpts {
     int mode = -1;                  // -1 auto, 0 never (pass C), 1 whenever the chain and slab allow
     uint32_t density_x100 = 200;    // auto: a batch's swipes per 128-B line of the slab, x100
     uint32_t dense_min_x100 = 100;  // a window is staged in LDS from this many records per line, x100
-    int klog = 3;                   // keys per window: 2^klog (3: 128 KiB of LDS, 2: 64 KiB)
+    int klog = 3;                   // keys per window: 2^klog (16 KiB each; 0..3)
 };
 // sizes the context scratch for batches of up to n swipes (no launch)
 // sub: swipes per sub-batch of the three passes (0: the default, 16M)

@@ -1140,8 +1140,6 @@ constexpr uint32_t kSegMaxWpb = 512;                        // windows per bucke
 constexpr uint32_t kSegChunk = 8192;                        // records per level-2 chunk
 constexpr uint32_t kSegMaxRuns = kPSub / kSegRunSw;         // 2048 runs per sub-batch
 constexpr uint32_t kSegRecShift = 20;                       // record: slot-in-bucket above bit 20
-constexpr uint32_t kSegEPairs = 1024;                       // E: (sub-batch, chunk) runs staged at once
-constexpr uint32_t kSegSlice = 65536;                       // E: records per block and window (hot windows are cut)
 
 struct SegArgs {
     uint32_t *r1;     // [nruns][kSegRunSw] level-1 records of a sub-batch, bucket-sorted per run
@@ -1394,10 +1392,10 @@ __device__ __forceinline__ bool seg_lds_max(uint32_t *w, uint32_t sh, uint32_t r
     return false;
 }
 
-// The window pass.  A window whose records exceed kSegSlice (a hot key's:
+// The window pass.  A window whose records exceed its slice (a hot key's:
 // at the 8-way shard the hottest lecture's day keys take ~1.8 M records of
 // one window per step) is cut into slices so that no block reads more than
-// kSegSlice records: pass E1 (QUEUE = false) takes every window's first
+// slice of records (seg_slice): pass E1 (QUEUE = false) takes every window's first
 // slice and queues the others; E2 (QUEUE = true) takes the queued slices;
 // each slice of a cut window raises its own LDS copy of the window, stored
 // whole to a copy buffer, and M (k_seg_m) stores the byte max of the copies.
@@ -1411,25 +1409,67 @@ __device__ __forceinline__ bool seg_lds_max(uint32_t *w, uint32_t sh, uint32_t r
 // prefix per thread, all 16 loads in flight), raises them in LDS and (4)
 // stores the risen lines.  A window with fewer than dense_min records is
 // raised in place instead (its register loads are dropped).
-constexpr uint32_t kSegCbLds = 2048;  // cb words kept in LDS (nsub * (nb1 + 1)); more: read from L2
+// Diagnostic per-item stamps of the window pass (-DSKE_SEG_STAMPS builds only;
+// tools/stamps/run_seg_stamps.py): thread 0 records s_memrealtime (100 MHz)
+// at 5 points of every window / queued slice, its record and run counts and
+// its block and XCD, into a side buffer no output depends on.
+#ifdef SKE_SEG_STAMPS
+__device__ unsigned long long *ske_seg_stamp_buf;
+hipError_t set_seg_stamp_buffer(void *p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(ske_seg_stamp_buf), &p, sizeof(void *));
+}
+#define SEG_STAMP(slot, k, v)                                                                  \
+    do {                                                                                       \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+        unsigned long long t_;                                                                 \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+        if (threadIdx.x == 0 && ske_seg_stamp_buf) {                                           \
+            ske_seg_stamp_buf[size_t(slot) * 8 + (k)] = t_;                                    \
+            if ((k) == 4) {                                                                    \
+                ske_seg_stamp_buf[size_t(slot) * 8 + 5] = (v);                                 \
+                ske_seg_stamp_buf[size_t(slot) * 8 + 6] =                                      \
+                    blockIdx.x | (uint64_t(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15) << 32); \
+            }                                                                                  \
+        }                                                                                      \
+    } while (0)
+#else
+hipError_t set_seg_stamp_buffer(void *) { return hipErrorNotSupported; }
+#define SEG_STAMP(slot, k, v) \
+    do {                      \
+    } while (0)
+#endif
+// Block shape per window size: windows of 2^KLOG keys (16 KiB each) in
+// blocks of T threads, BPC blocks resident per CU (LDS: the window + its
+// staging), so that small windows keep more windows in flight per CU.
+template <int KLOG> struct SegE {
+    static constexpr uint32_t T = KLOG >= 2 ? 1024 : (KLOG == 1 ? 512 : 256);
+    static constexpr uint32_t BPC = KLOG >= 3 ? 1 : (KLOG == 2 ? 2 : (KLOG == 1 ? 4 : 8));
+    static constexpr uint32_t WPS = T / 64 * BPC / 4;  // waves per SIMD (launch bounds)
+    static constexpr uint32_t RPT = KLOG >= 3 ? 16 : 8;  // records per thread per round
+    static constexpr uint32_t EP = KLOG == 2 ? 512 : T;  // runs staged at once
+    static constexpr uint32_t CBL = KLOG >= 3 ? 2048 : (KLOG == 2 ? 1024 : (KLOG == 1 ? 512 : 256));
+};
+__host__ __device__ constexpr uint32_t seg_slice(uint32_t klog) { return 16384u << (klog < 2 ? klog : 2); }
+
 template <int KLOG, bool QUEUE>
-__global__ void __launch_bounds__(1024, KLOG >= 3 ? 4 : 8) k_seg_e(const PartArgs A, const SegArgs S) {
-    constexpr uint32_t KW = 1u << KLOG, WB = KW << kHllP, NPC = WB / 16 / 1024;  // 16-B pieces per thread
-    constexpr uint32_t NL = KW * (kHllRegs / 128);                                 // 128-B lines
-    // (windows of 4 keys: two blocks per CU, so under 80 KiB of LDS and 64 VGPRs)
-    constexpr uint32_t RPT = KLOG >= 3 ? 16 : 8;               // records per thread per round
-    constexpr uint32_t EP = KLOG >= 3 ? kSegEPairs : kSegEPairs / 2;
-    constexpr uint32_t CBL = KLOG >= 3 ? kSegCbLds : kSegCbLds / 2;
+__global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const PartArgs A, const SegArgs S) {
+    using E = SegE<KLOG>;
+    constexpr uint32_t T = E::T;
+    constexpr uint32_t KW = 1u << KLOG, WB = KW << kHllP, NPC = WB / 16 / T;  // 16-B pieces per thread
+    constexpr uint32_t NL = KW * (kHllRegs / 128);                              // 128-B lines
+    constexpr uint32_t RPT = E::RPT, EP = E::EP, CBL = E::CBL;
+    constexpr uint32_t SLICE = seg_slice(KLOG);
     __shared__ __attribute__((aligned(16))) uint8_t win[WB];
     __shared__ uint8_t dirty[NL];
     __shared__ uint32_t rb[EP], rp[EP + 1];
     __shared__ uint32_t cbs[CBL];
-    __shared__ uint32_t spre[65], ws[16], hdr[2];
+    __shared__ uint32_t spre[65], ws[T / 64], hdr[2];
     const uint32_t tid = threadIdx.x;
     const uint32_t wpb = 1u << S.wlog, cbw = S.nsub * (S.nb1 + 1);
     const bool cbl = cbw <= CBL;
     if (cbl)
-        for (uint32_t j = tid; j < cbw; j += 1024) cbs[j] = S.cb[j];
+        for (uint32_t j = tid; j < cbw; j += T) cbs[j] = S.cb[j];
     const uint32_t *cbp = cbl ? cbs : S.cb;
     lds_barrier();
     const uint32_t nitems = QUEUE ? S.q[0] : S.nwin;
@@ -1443,6 +1483,9 @@ __global__ void __launch_bounds__(1024, KLOG >= 3 ? 4 : 8) k_seg_e(const PartArg
         } else {
             wi = it;
         }
+        const uint32_t stamp = QUEUE ? S.nwin + it : wi;
+        (void)stamp;
+        SEG_STAMP(stamp, 0, 0);
         const uint32_t h = wi >> S.wlog, w2 = wi & (wpb - 1);
         const uint32_t slot0 = wi << KLOG;
         const uint32_t nk = A.nslots - slot0 < KW ? A.nslots - slot0 : KW;
@@ -1452,7 +1495,7 @@ __global__ void __launch_bounds__(1024, KLOG >= 3 ? 4 : 8) k_seg_e(const PartArg
         part_u32x4 v[NPC];
 #pragma unroll
         for (uint32_t i = 0; i < NPC; i++) {
-            const uint32_t j = i * 1024 + tid;
+            const uint32_t j = i * T + tid;
             v[i] = j < npc ? reinterpret_cast<const part_u32x4 *>(g)[j] : part_u32x4{0, 0, 0, 0};
         }
         // (2) runs: pair x = (sub-batch s, chunk q of bucket h in s), in that
@@ -1478,20 +1521,23 @@ __global__ void __launch_bounds__(1024, KLOG >= 3 ? 4 : 8) k_seg_e(const PartArg
         uint32_t nrec = 0, nrec0 = 0;
         for (uint32_t x0 = 0; x0 < np; x0 += EP) {
             uint32_t base = 0, len = 0, t;
-            if (x0 + tid < np) len = run_of(x0 + tid, base);
+            if (tid < EP && x0 + tid < np) len = run_of(x0 + tid, base);
             const uint32_t ex = seg_scan(len, ws, t);
-            if (x0 == 0 && tid < EP) {
-                rb[tid] = base;
-                rp[tid] = ex;
+            if (x0 == 0) {
+                nrec0 = t;  // every thread: the first batch's total
+                if (tid < EP) {
+                    rb[tid] = base;
+                    rp[tid] = ex;
+                }
                 if (tid == 0) rp[np < EP ? np : EP] = t;
-                nrec0 = t;
             }
             nrec += t;
         }
+        SEG_STAMP(stamp, 1, 0);
         if (nrec == 0) continue;  // block-uniform
-        if (!QUEUE && nrec > kSegSlice) {
+        if (!QUEUE && nrec > SLICE) {
             // a hot window: cut into slices, the others queued for E2
-            const uint32_t nsl = (nrec + kSegSlice - 1) / kSegSlice;
+            const uint32_t nsl = (nrec + SLICE - 1) / SLICE;
             if (tid == 0) {
                 uint32_t base = atomicAdd(&S.q[1], nsl);
                 if (base + nsl > S.ccap) {
@@ -1507,13 +1553,13 @@ __global__ void __launch_bounds__(1024, KLOG >= 3 ? 4 : 8) k_seg_e(const PartArg
             copy = hdr[0];
         }
         const bool cut = copy != 0xffffffffu;
-        const uint32_t lo = cut ? sl * kSegSlice : 0;
-        const uint32_t hi = cut ? (nrec - lo < kSegSlice ? nrec : lo + kSegSlice) : nrec;
+        const uint32_t lo = cut ? sl * SLICE : 0;
+        const uint32_t hi = cut ? (nrec - lo < SLICE ? nrec : lo + SLICE) : nrec;
         const bool dense = cut || nrec >= S.dense_min;
         if (dense) {
-            for (uint32_t j = tid; j < NL; j += 1024) dirty[j] = 0;
+            for (uint32_t j = tid; j < NL; j += T) dirty[j] = 0;
 #pragma unroll
-            for (uint32_t i = 0; i < NPC; i++) reinterpret_cast<part_u32x4 *>(win)[i * 1024 + tid] = v[i];
+            for (uint32_t i = 0; i < NPC; i++) reinterpret_cast<part_u32x4 *>(win)[i * T + tid] = v[i];
         }
         // (3) records [lo, hi) of the concatenated runs, RPT consecutive ones
         // per thread and round; runs staged kSegEPairs at a time
@@ -1532,9 +1578,10 @@ __global__ void __launch_bounds__(1024, KLOG >= 3 ? 4 : 8) k_seg_e(const PartArg
                 if (tid == 0) rp[nx] = btot;
             }
             lds_barrier();  // (the window's LDS image is complete here too)
+            if (x0 == 0) SEG_STAMP(stamp, 2, 0);
             // this batch's records [p0, p0 + btot) of the window; ours: [lo, hi)
             const uint32_t f_lo = lo > p0 ? lo - p0 : 0, f_hi = hi - p0 < btot ? hi - p0 : btot;
-            for (uint32_t f0 = f_lo + tid * RPT; f0 - tid * RPT < f_hi; f0 += 1024 * RPT) {
+            for (uint32_t f0 = f_lo + tid * RPT; f0 - tid * RPT < f_hi; f0 += T * RPT) {
                 uint32_t rec[RPT];
                 if (f0 < f_hi) {
                     uint32_t j = seg_last_le(rp, nx, f0);
@@ -1568,21 +1615,23 @@ __global__ void __launch_bounds__(1024, KLOG >= 3 ? 4 : 8) k_seg_e(const PartArg
             p0 += btot;
         }
         lds_barrier();  // every raise in LDS done
+        SEG_STAMP(stamp, 3, 0);
         if (cut) {
             // a slice of a cut window: the whole LDS copy, merged by k_seg_m
             part_u32x4 *dst = reinterpret_cast<part_u32x4 *>(S.copies + size_t(copy) * WB);
 #pragma unroll
-            for (uint32_t i = 0; i < NPC; i++) dst[i * 1024 + tid] = reinterpret_cast<const part_u32x4 *>(win)[i * 1024 + tid];
+            for (uint32_t i = 0; i < NPC; i++) dst[i * T + tid] = reinterpret_cast<const part_u32x4 *>(win)[i * T + tid];
         } else if (dense) {
             // (4) the lines that rose, stored back whole
 #pragma unroll
             for (uint32_t i = 0; i < NPC; i++) {
-                const uint32_t j = i * 1024 + tid;
+                const uint32_t j = i * T + tid;
                 if (j < npc && dirty[j >> 3])
                     reinterpret_cast<part_u32x4 *>(g)[j] = reinterpret_cast<const part_u32x4 *>(win)[j];
             }
         }
         lds_barrier();  // win, dirty, rb, rp and hdr are rewritten by the next window
+        SEG_STAMP(stamp, 4, uint64_t(nrec) | (uint64_t(np) << 32) | (uint64_t(dense) << 63));
     }
 }
 
@@ -1708,7 +1757,7 @@ struct SegPlan {
     uint32_t s1, wlog, klog, nb1, nwin, maxch, nsub, dense_min;
 };
 static bool seg_plan(uint32_t nslots, uint64_t n, uint32_t sub, const SegOpts &so, SegPlan *P) {
-    if (nslots == 0 || n == 0 || (so.klog != 2 && so.klog != 3)) return false;
+    if (nslots == 0 || n == 0 || so.klog < 0 || so.klog > 3) return false;
     const uint32_t klog = uint32_t(so.klog);
     const uint32_t nwin = uint32_t((uint64_t(nslots) + (1u << klog) - 1) >> klog);
     uint32_t wlog = 0;
@@ -1753,10 +1802,10 @@ static hipError_t seg_scratch(const SegPlan &P, uint32_t sub, uint64_t n, Scratc
     if (e == hipSuccess)
         S->o2 = (uint32_t *)scratch_get(scr, 37, size_t(P.nsub) * P.maxch * ((1u << P.wlog) + 1) * 4, &e);
     if (e == hipSuccess) S->cb = (uint32_t *)scratch_get(scr, 38, size_t(P.nsub) * (P.nb1 + 1) * 4, &e);
-    // the window pass's cut windows: a cut window has > kSegSlice records and
-    // ceil(records / kSegSlice) < 2 records / kSegSlice slices, so 2 n /
-    // kSegSlice copies, queue entries and cut windows always suffice
-    const uint32_t ccap = uint32_t(2 * ((n + kSegSlice - 1) / kSegSlice) + 2);
+    // the window pass's cut windows: a cut window has > slice records and
+    // ceil(records / slice) < 2 records / slice slices, so 2 n / slice
+    // copies, queue entries and cut windows always suffice
+    const uint32_t ccap = uint32_t(2 * ((n + seg_slice(P.klog) - 1) / seg_slice(P.klog)) + 2);
     const size_t wb = size_t(1) << (P.klog + kHllP);
     if (e == hipSuccess) S->q = (uint32_t *)scratch_get(scr, 39, 16, &e);
     if (e == hipSuccess) S->qitems = (uint4 *)scratch_get(scr, 42, size_t(ccap) * 16, &e);
@@ -1892,14 +1941,18 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             if (hook) hook(hook_user, 4, 0, st);
             e = hipMemsetAsync(S.q, 0, 16, st);
             if (e != hipSuccess) return e;
-            if (P.klog >= 3) {
-                hipLaunchKernelGGL((k_seg_e<3, false>), dim3(unsigned(cus)), dim3(1024), 0, st, A, S);
-                hipLaunchKernelGGL((k_seg_e<3, true>), dim3(unsigned(cus)), dim3(1024), 0, st, A, S);
-                hipLaunchKernelGGL(k_seg_m<3>, dim3(unsigned(cus)), dim3(1024), 0, st, A, S);
-            } else {
-                hipLaunchKernelGGL((k_seg_e<2, false>), dim3(unsigned(cus) * 2), dim3(1024), 0, st, A, S);
-                hipLaunchKernelGGL((k_seg_e<2, true>), dim3(unsigned(cus) * 2), dim3(1024), 0, st, A, S);
-                hipLaunchKernelGGL(k_seg_m<2>, dim3(unsigned(cus)), dim3(1024), 0, st, A, S);
+            switch (P.klog) {
+#define SEG_E_LAUNCH(K)                                                                                  \
+    case K:                                                                                              \
+        hipLaunchKernelGGL((k_seg_e<K, false>), dim3(unsigned(cus) * SegE<K>::BPC), dim3(SegE<K>::T), 0, st, A, S); \
+        hipLaunchKernelGGL((k_seg_e<K, true>), dim3(unsigned(cus) * SegE<K>::BPC), dim3(SegE<K>::T), 0, st, A, S);  \
+        hipLaunchKernelGGL(k_seg_m<K>, dim3(unsigned(cus)), dim3(1024), 0, st, A, S);                    \
+        break;
+                SEG_E_LAUNCH(0)
+                SEG_E_LAUNCH(1)
+                SEG_E_LAUNCH(2)
+                SEG_E_LAUNCH(3)
+#undef SEG_E_LAUNCH
             }
             if (hook) hook(hook_user, 4, 1, st);
             e = hipGetLastError();

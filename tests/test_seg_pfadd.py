@@ -57,6 +57,9 @@ def _oracle(orc, engine, w, p, batches):
     (2, 100, 0),            # windows of 4 keys (two blocks per CU)
     (3, 0, 1 << 18),        # 5 sub-batches feed one window pass
     (2, 50, 3 * 1024 + 5),  # sub-batches of 4 tiles (rounded), odd split
+    (1, 100, 0),            # windows of 2 keys (512-thread blocks)
+    (0, 100, 0),            # windows of 1 key (256-thread blocks)
+    (0, 0, 1 << 18),        # 1-key windows, 5 sub-batches, all staged
 ])
 def test_seg_forced_small(engine, orc, klog, dense_min, sub):
     from rtsas_amd.engine import DeviceBuffer
@@ -81,11 +84,14 @@ def test_seg_forced_small(engine, orc, klog, dense_min, sub):
     assert np.array_equal(engine.registers_all(w.n_keys), regs)
 
 
-@pytest.mark.parametrize("nkeys", [1, 9, 4097, 20_000])
-def test_seg_key_counts(engine, orc, nkeys):
+@pytest.mark.parametrize("nkeys,n,klog", [(1, 700_001, 3), (9, 700_001, 3), (4097, 700_001, 3),
+                                           (20_000, 700_001, 3), (1, 12_000_000, 2), (3, 9_000_000, 3),
+                                           (20_000, 700_001, 0), (3, 9_000_000, 0), (4097, 700_001, 1)])
+def test_seg_key_counts(engine, orc, nkeys, n, klog):
     """Slabs of 1 key (one bucket, one window), 9 (a partial window), 4097
     (a partial last bucket) and 20 000 (512-bucket cap: s1 grows), uniform
-    keys, forced on."""
+    keys, forced on; one key under 12 M swipes (a window of > 1024 runs --
+    staged in batches -- cut into ~165 slices), three under 9 M."""
     from rtsas_amd import synthetic
     from rtsas_amd.engine import DeviceBuffer
     w = synthetic.WORKLOADS["c3"]
@@ -96,7 +102,7 @@ def test_seg_key_counts(engine, orc, nkeys):
     engine.preload(0, p, w.n_members)
     engine.hll_reserve(w.n_keys)
     engine.set_option("hll_seg", 1)
-    n = 700_001
+    engine.set_option("seg_klog", klog)
     b = engine.swipe_batch(p, 0, n)
     out = DeviceBuffer(engine.ctx, n)
     engine.swipes(0, b, out)
