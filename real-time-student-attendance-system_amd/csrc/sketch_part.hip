@@ -1150,8 +1150,9 @@ struct SegArgs {
     uint32_t *o2;     // [nsub][maxch][wpb + 1] window w's start in chunk q
     uint32_t *cb;     // [nsub][nb1 + 1] first chunk of bucket h in sub-batch s (prefix)
     uint32_t nruns;   // level-1 runs of this sub-batch
-    uint32_t nb1;     // level-1 buckets (slot >> s1)
-    uint32_t s1;      // slot bits below the bucket (<= 12)
+    uint32_t nb1;     // level-1 buckets: 2^b1, window W = slot >> klog in bucket W & (nb1 - 1)
+    uint32_t b1;      // log2(nb1)
+    uint32_t s1;      // bits of a record's slot-in-bucket: (W >> b1) << klog | slot & (2^klog - 1) (<= 12)
     uint32_t wlog;    // windows per bucket = 1 << wlog
     uint32_t klog;    // keys per window = 1 << klog
     uint32_t s;       // this sub-batch's index in the call
@@ -1205,7 +1206,7 @@ __global__ void __launch_bounds__(1024, 8) k_seg_c1(const PartArgs A, const SegA
     for (uint32_t j = tid; j < kSegRunSw; j += 1024) mark[j] = 0;
     const uint32_t npieces = A.nunits * kSegRunTiles;  // 16-B lists of one run
     const __amdgpu_buffer_rsrc_t rfl = part_rsrc(A.flist, A.nunits * A.fl_stride * kPbLanes * 2);
-    const uint32_t smask = (1u << S.s1) - 1;
+    const uint32_t kmask = (1u << S.klog) - 1, bmask = S.nb1 - 1;
     lds_barrier();  // marks cleared before any run sets one
     for (uint32_t r = blockIdx.x; r < S.nruns; r += gridDim.x) {
         const uint32_t t0 = r * kSegRunTiles;
@@ -1259,8 +1260,9 @@ __global__ void __launch_bounds__(1024, 8) k_seg_c1(const PartArgs A, const SegA
                 if (sl[u] >= A.nslots) {
                     atomicOr(A.err, 1u);
                 } else {
-                    const uint32_t b = sl[u] >> S.s1;
-                    rec[u] = ((sl[u] & smask) << kSegRecShift) | ((hv[u] & 0x3fffu) << 6) | (hv[u] >> 16);
+                    const uint32_t w = sl[u] >> S.klog, b = w & bmask;
+                    const uint32_t sib = ((w >> S.b1) << S.klog) | (sl[u] & kmask);
+                    rec[u] = (sib << kSegRecShift) | ((hv[u] & 0x3fffu) << 6) | (hv[u] >> 16);
                     pos[u] = (b << 16) | atomicAdd(&cnt[b], 1u);
                 }
             }
@@ -1448,7 +1450,6 @@ template <int KLOG> struct SegE {
     static constexpr uint32_t WPS = T / 64 * BPC / 4;  // waves per SIMD (launch bounds)
     static constexpr uint32_t RPT = KLOG >= 3 ? 16 : 8;  // records per thread per round
     static constexpr uint32_t EP = KLOG == 2 ? 512 : T;  // runs staged at once
-    static constexpr uint32_t CBL = KLOG >= 3 ? 2048 : (KLOG == 2 ? 1024 : (KLOG == 1 ? 512 : 256));
 };
 __host__ __device__ constexpr uint32_t seg_slice(uint32_t klog) { return 16384u << (klog < 2 ? klog : 2); }
 
@@ -1458,83 +1459,114 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
     constexpr uint32_t T = E::T;
     constexpr uint32_t KW = 1u << KLOG, WB = KW << kHllP, NPC = WB / 16 / T;  // 16-B pieces per thread
     constexpr uint32_t NL = KW * (kHllRegs / 128);                              // 128-B lines
-    constexpr uint32_t RPT = E::RPT, EP = E::EP, CBL = E::CBL;
+    constexpr uint32_t RPT = E::RPT, EP = E::EP;
     constexpr uint32_t SLICE = seg_slice(KLOG);
     __shared__ __attribute__((aligned(16))) uint8_t win[WB];
     __shared__ uint8_t dirty[NL];
     __shared__ uint32_t rb[EP], rp[EP + 1];
-    __shared__ uint32_t cbs[CBL];
-    __shared__ uint32_t spre[65], ws[T / 64], hdr[2];
+    __shared__ uint32_t spre[2][65], cq0[2][64], ws[T / 64], hdr[2];
     const uint32_t tid = threadIdx.x;
-    const uint32_t wpb = 1u << S.wlog, cbw = S.nsub * (S.nb1 + 1);
-    const bool cbl = cbw <= CBL;
-    if (cbl)
-        for (uint32_t j = tid; j < cbw; j += T) cbs[j] = S.cb[j];
-    const uint32_t *cbp = cbl ? cbs : S.cb;
-    lds_barrier();
+    const uint32_t nb1m = S.nb1 - 1;  // buckets: a power of two, window W in bucket W & nb1m
     const uint32_t nitems = QUEUE ? S.q[0] : S.nwin;
-    for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
-        uint32_t wi, sl = 0, copy = 0xffffffffu;
+    // Items (E1: windows, E2: queued slices) go round robin over the blocks.
+    // Each item's layout -- its bucket's chunk counts per sub-batch (spre:
+    // prefix, cq0: the first chunk; nsub <= 64), double-buffered by item
+    // parity -- its first EP runs and its window's registers are fetched in
+    // phases while the previous item's records are raised and its lines
+    // stored:
+    //   P1  the bucket's chunk columns and the window's registers (loads);
+    //   P2  the column prefix (scan), then the item's first EP runs (loads);
+    //   P3  the runs' prefix (scan) and record count, when the item starts.
+    // (Buckets interleave windows, so a hot key's windows fall in different
+    // buckets and every bucket has about the same chunks: a window's runs
+    // rarely exceed EP; more are counted and staged in batches.)
+    uint32_t cq = 0, cc = 0;                // P1: this thread's sub-batch column
+    uint32_t pbase = 0, plen = 0, pnp = 0;  // P2: this thread's run, the item's runs
+    part_u32x4 v[NPC];
+    auto item = [&](uint32_t it, uint32_t &wi, uint32_t &sl, uint32_t &copy) {
+        wi = it;
+        sl = 0;
+        copy = 0xffffffffu;
         if (QUEUE) {
             const uint4 e = S.qitems[it];
             wi = e.x;
             sl = e.y;
             copy = e.z;
-        } else {
-            wi = it;
         }
+    };
+    auto p1 = [&](uint32_t wi) {
+        const uint32_t h = wi & nb1m;
+        if (tid < S.nsub) {
+            cq = S.cb[size_t(tid) * (S.nb1 + 1) + h];
+            cc = S.cb[size_t(tid) * (S.nb1 + 1) + h + 1];
+        }
+        const uint32_t slot0 = wi << KLOG;
+        const uint32_t nk = A.nslots - slot0 < KW ? A.nslots - slot0 : KW;
+        const part_u32x4 *g = reinterpret_cast<const part_u32x4 *>(A.regs + (size_t(slot0) << kHllP));
+#pragma unroll
+        for (uint32_t i = 0; i < NPC; i++) {
+            const uint32_t j = i * T + tid;
+            v[i] = j < (nk << (kHllP - 4)) ? g[j] : part_u32x4{0, 0, 0, 0};
+        }
+    };
+    // run x of window column w2 of the bucket staged in buffer pb
+    const uint32_t orow = (1u << S.wlog) + 1;
+    auto run_of = [&](uint32_t pb, uint32_t x, uint32_t w2, uint32_t &base) -> uint32_t {
+        const uint32_t s = seg_last_le(spre[pb], S.nsub, x);
+        const size_t row = size_t(s) * S.maxch + cq0[pb][s] + (x - spre[pb][s]);
+        const uint32_t *o = S.o2 + row * orow + w2;
+        const uint32_t b = o[0];
+        base = uint32_t(row * kSegChunk + b);  // < 2^32: the host plan checks nsub * maxch * kSegChunk
+        return o[1] - b;
+    };
+    auto p2 = [&](uint32_t pb, uint32_t wi) {  // block-uniform; buffer pb is free
+        const uint32_t c = tid < S.nsub ? cc - cq : 0u;
+        const uint32_t ex = seg_scan(c, ws, pnp);
+        if (tid < S.nsub) {
+            spre[pb][tid] = ex;
+            cq0[pb][tid] = cq;
+        }
+        lds_barrier();
+        plen = 0;
+        if (tid < EP && tid < pnp) plen = run_of(pb, tid, wi >> S.b1, pbase);
+    };
+    uint32_t it = blockIdx.x, par = 0;
+    uint32_t wi_n = 0, sl_n = 0, copy_n = 0;
+    if (it < nitems) {
+        item(it, wi_n, sl_n, copy_n);
+        p1(wi_n);
+        p2(0, wi_n);
+    }
+    for (; it < nitems; it += gridDim.x, par ^= 1) {
+        const uint32_t wi = wi_n, sl = sl_n;
+        uint32_t copy = copy_n;
+        const uint32_t np = pnp;
         const uint32_t stamp = QUEUE ? S.nwin + it : wi;
         (void)stamp;
         SEG_STAMP(stamp, 0, 0);
-        const uint32_t h = wi >> S.wlog, w2 = wi & (wpb - 1);
+        const uint32_t w2 = wi >> S.b1;
         const uint32_t slot0 = wi << KLOG;
         const uint32_t nk = A.nslots - slot0 < KW ? A.nslots - slot0 : KW;
         uint8_t *g = A.regs + (size_t(slot0) << kHllP);
         const uint32_t npc = nk << (kHllP - 4);  // the window's 16-B pieces in the slab
-        // (1) the window's registers, in flight while its run table is read
-        part_u32x4 v[NPC];
-#pragma unroll
-        for (uint32_t i = 0; i < NPC; i++) {
-            const uint32_t j = i * T + tid;
-            v[i] = j < npc ? reinterpret_cast<const part_u32x4 *>(g)[j] : part_u32x4{0, 0, 0, 0};
-        }
-        // (2) runs: pair x = (sub-batch s, chunk q of bucket h in s), in that
-        // order; spre = prefix of the sub-batches' chunk counts (nsub <= 64)
-        uint32_t np;
+        // P3: the record count (the first batch of runs stays staged)
+        uint32_t nrec, nrec0;
         {
-            uint32_t c = 0;
-            if (tid < S.nsub) c = cbp[tid * (S.nb1 + 1) + h + 1] - cbp[tid * (S.nb1 + 1) + h];
-            const uint32_t ex = seg_scan(c, ws, np);
-            if (tid < S.nsub) spre[tid] = ex;
-        }
-        lds_barrier();
-        auto run_of = [&](uint32_t x, uint32_t &base) -> uint32_t {
-            const uint32_t s = seg_last_le(spre, S.nsub, x);
-            const uint32_t q = cbp[s * (S.nb1 + 1) + h] + (x - spre[s]);
-            const size_t row = size_t(s) * S.maxch + q;
-            const uint32_t *o = S.o2 + row * (wpb + 1) + w2;
-            const uint32_t b = o[0];
-            base = uint32_t(row * kSegChunk + b);  // < 2^32: the host plan checks nsub * maxch * kSegChunk
-            return o[1] - b;
-        };
-        // the record count (the first batch of runs is kept staged)
-        uint32_t nrec = 0, nrec0 = 0;
-        for (uint32_t x0 = 0; x0 < np; x0 += EP) {
-            uint32_t base = 0, len = 0, t;
-            if (tid < EP && x0 + tid < np) len = run_of(x0 + tid, base);
-            const uint32_t ex = seg_scan(len, ws, t);
-            if (x0 == 0) {
-                nrec0 = t;  // every thread: the first batch's total
-                if (tid < EP) {
-                    rb[tid] = base;
-                    rp[tid] = ex;
-                }
-                if (tid == 0) rp[np < EP ? np : EP] = t;
+            const uint32_t ex = seg_scan(plen, ws, nrec0);
+            if (tid < EP) {
+                rb[tid] = pbase;
+                rp[tid] = ex;
             }
-            nrec += t;
+            if (tid == 0) rp[np < EP ? np : EP] = nrec0;
+            nrec = nrec0;
+            for (uint32_t x0 = EP; x0 < np; x0 += EP) {  // (more than EP runs: count the rest)
+                uint32_t base = 0, len = 0, t;
+                if (tid < EP && x0 + tid < np) len = run_of(par, x0 + tid, w2, base);
+                (void)seg_scan(len, ws, t);
+                nrec += t;
+            }
         }
         SEG_STAMP(stamp, 1, 0);
-        if (nrec == 0) continue;  // block-uniform
         if (!QUEUE && nrec > SLICE) {
             // a hot window: cut into slices, the others queued for E2
             const uint32_t nsl = (nrec + SLICE - 1) / SLICE;
@@ -1555,30 +1587,37 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
         const bool cut = copy != 0xffffffffu;
         const uint32_t lo = cut ? sl * SLICE : 0;
         const uint32_t hi = cut ? (nrec - lo < SLICE ? nrec : lo + SLICE) : nrec;
-        const bool dense = cut || nrec >= S.dense_min;
+        const bool dense = nrec > 0 && (cut || nrec >= S.dense_min);
         if (dense) {
             for (uint32_t j = tid; j < NL; j += T) dirty[j] = 0;
 #pragma unroll
             for (uint32_t i = 0; i < NPC; i++) reinterpret_cast<part_u32x4 *>(win)[i * T + tid] = v[i];
         }
-        // (3) records [lo, hi) of the concatenated runs, RPT consecutive ones
-        // per thread and round; runs staged kSegEPairs at a time
+        lds_barrier();  // the window's LDS image and its first runs are staged
+        // P1 of the next item: its loads fly while this item's records are raised
+        const uint32_t nit = it + gridDim.x;
+        if (nit < nitems) {
+            item(nit, wi_n, sl_n, copy_n);
+            p1(wi_n);
+        }
+        SEG_STAMP(stamp, 2, 0);
+        // records [lo, hi) of the concatenated runs, RPT consecutive ones per
+        // thread and round; runs staged EP at a time
         for (uint32_t x0 = 0, p0 = 0; x0 < np && p0 < hi; x0 += EP) {
             const uint32_t nx = np - x0 < EP ? np - x0 : EP;
             uint32_t btot = nrec0;
-            if (x0 > 0) {  // (a window with more than kSegEPairs runs: restage)
+            if (x0 > 0) {  // (a window with more than EP runs: restage)
                 lds_barrier();
                 uint32_t base = 0, len = 0;
-                if (tid < nx) len = run_of(x0 + tid, base);
+                if (tid < nx) len = run_of(par, x0 + tid, w2, base);
                 const uint32_t ex = seg_scan(len, ws, btot);
                 if (tid < nx) {
                     rb[tid] = base;
                     rp[tid] = ex;
                 }
                 if (tid == 0) rp[nx] = btot;
+                lds_barrier();
             }
-            lds_barrier();  // (the window's LDS image is complete here too)
-            if (x0 == 0) SEG_STAMP(stamp, 2, 0);
             // this batch's records [p0, p0 + btot) of the window; ours: [lo, hi)
             const uint32_t f_lo = lo > p0 ? lo - p0 : 0, f_hi = hi - p0 < btot ? hi - p0 : btot;
             for (uint32_t f0 = f_lo + tid * RPT; f0 - tid * RPT < f_hi; f0 += T * RPT) {
@@ -1614,15 +1653,18 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
             }
             p0 += btot;
         }
-        lds_barrier();  // every raise in LDS done
+        lds_barrier();  // every raise in LDS done; rb / rp free
         SEG_STAMP(stamp, 3, 0);
+        // P2 of the next item (its layout into the other buffer), its runs'
+        // loads flying while this item's lines are stored
+        if (nit < nitems) p2(par ^ 1, wi_n);
         if (cut) {
             // a slice of a cut window: the whole LDS copy, merged by k_seg_m
             part_u32x4 *dst = reinterpret_cast<part_u32x4 *>(S.copies + size_t(copy) * WB);
 #pragma unroll
             for (uint32_t i = 0; i < NPC; i++) dst[i * T + tid] = reinterpret_cast<const part_u32x4 *>(win)[i * T + tid];
         } else if (dense) {
-            // (4) the lines that rose, stored back whole
+            // the lines that rose, stored back whole
 #pragma unroll
             for (uint32_t i = 0; i < NPC; i++) {
                 const uint32_t j = i * T + tid;
@@ -1630,7 +1672,7 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
                     reinterpret_cast<part_u32x4 *>(g)[j] = reinterpret_cast<const part_u32x4 *>(win)[j];
             }
         }
-        lds_barrier();  // win, dirty, rb, rp and hdr are rewritten by the next window
+        lds_barrier();  // win, dirty and hdr are rewritten by the next item
         SEG_STAMP(stamp, 4, uint64_t(nrec) | (uint64_t(np) << 32) | (uint64_t(dense) << 63));
     }
 }
@@ -1748,31 +1790,34 @@ static uint32_t part_sub(uint32_t sub_opt) {
 
 // the scratch before the first launch (so a graph recorded later holds it)
 // The segmented PFADD's geometry for a slab of nslots keys and a batch of n
-// swipes in sub-batches of `sub`: windows of 2^klog keys; the level-1 bucket
-// is slot >> s1 with 2^wlog windows each, wlog ~ log2(windows) / 2 so that
-// both levels' runs stay long (at C3: 98 buckets x 128 windows at 100 k keys,
-// 25 x 64 at the 8-way shard); false when the slab is too large for 512
-// buckets of 4096 keys.
+// swipes in sub-batches of `sub`: windows of 2^klog keys (W = slot >> klog);
+// 2^b1 level-1 buckets of 2^wlog windows each, window W in bucket W mod
+// 2^b1 (buckets interleave windows, so the consecutive windows of a hot
+// lecture's day keys fall in different buckets and every bucket carries
+// about the same records), b1 + wlog = ceil(log2(windows)) split evenly so
+// that both levels' runs stay long; false when the slab needs more than 2^9
+// buckets of 2^9 windows.
 struct SegPlan {
-    uint32_t s1, wlog, klog, nb1, nwin, maxch, nsub, dense_min;
+    uint32_t s1, b1, wlog, klog, nb1, nwin, maxch, nsub, dense_min;
 };
 static bool seg_plan(uint32_t nslots, uint64_t n, uint32_t sub, const SegOpts &so, SegPlan *P) {
     if (nslots == 0 || n == 0 || so.klog < 0 || so.klog > 3) return false;
     const uint32_t klog = uint32_t(so.klog);
     const uint32_t nwin = uint32_t((uint64_t(nslots) + (1u << klog) - 1) >> klog);
-    uint32_t wlog = 0;
-    while ((uint64_t(1) << (2 * wlog)) < nwin) wlog++;
-    uint32_t s1 = klog + wlog;
-    while (((uint64_t(nslots) + (uint64_t(1) << s1) - 1) >> s1) > kSegMaxB1) {
-        s1++;
-        wlog++;
+    uint32_t tb = 0;
+    while ((uint64_t(1) << tb) < nwin) tb++;
+    uint32_t wlog = (tb + 1) / 2, b1 = tb - wlog;
+    if (b1 > 9) {
+        b1 = 9;
+        wlog = tb - 9;
     }
-    if (wlog > 9 || s1 > 12) return false;
+    if (wlog > 9) return false;
     P->klog = klog;
     P->wlog = wlog;
-    P->s1 = s1;
+    P->b1 = b1;
+    P->s1 = klog + wlog;
     P->nwin = nwin;
-    P->nb1 = uint32_t((uint64_t(nslots) + (uint64_t(1) << s1) - 1) >> s1);
+    P->nb1 = 1u << b1;
     P->nsub = uint32_t((n + sub - 1) / sub);
     P->maxch = (sub + kSegChunk - 1) / kSegChunk + P->nb1;
     if (P->nsub > 64 || uint64_t(P->nsub) * P->maxch * kSegChunk >= (uint64_t(1) << 32)) return false;
@@ -1814,6 +1859,7 @@ static hipError_t seg_scratch(const SegPlan &P, uint32_t sub, uint64_t n, Scratc
     S->ccap = ccap;
     S->nb1 = P.nb1;
     S->s1 = P.s1;
+    S->b1 = P.b1;
     S->wlog = P.wlog;
     S->klog = P.klog;
     S->nsub = P.nsub;

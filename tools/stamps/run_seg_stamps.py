@@ -31,7 +31,7 @@ run = bench.Run(args, args.config, 1, 0, 0, torch.device("cuda", 0), dist)
 eng = run.engine
 lib = eng.ctx.lib
 lib.ske_diag_set_seg_stamp_buffer.argtypes = [C.c_void_p, C.c_void_p]
-buf = torch.zeros(1 << 19, dtype=torch.int64, device="cuda")
+buf = torch.zeros(1 << 21, dtype=torch.int64, device="cuda")
 eng.swipes(0, run.batches[0], run.out)  # warm slab
 torch.cuda.synchronize()
 lib.ske_diag_set_seg_stamp_buffer(eng.ctx.ptr, C.c_void_p(buf.data_ptr()))
@@ -55,6 +55,16 @@ for name, sel in (("all", np.ones(len(st), bool)),):
     q = lambda a: [float(np.percentile(a, p)) for p in (50, 90, 99, 100)]
     res[name] = {"count_us_p50_90_99_max": q(ph[:, 0]), "image_us": q(ph[:, 1]), "apply_us": q(ph[:, 2]),
                  "write_us": q(ph[:, 3]), "total_us": q(tot), "records": q(nrec), "runs": q(npairs)}
+# split: items of E1 (index < nwin) vs E2, and by run count (hot buckets)
+e2 = idx >= nwin_guess_e1 if False else None
+hot = npairs > 1024
+for name, sel in (("runs_le_1024", ~hot), ("runs_gt_1024", hot)):
+    if sel.any():
+        res[name] = {"items": int(sel.sum()), "sum_us": float(tot[sel].sum()),
+                     "total_us_p50_90_max": [float(np.percentile(tot[sel], p)) for p in (50, 90, 100)],
+                     "phases_mean_us": [float(x) for x in ph[sel].mean(axis=0)],
+                     "records_mean": float(nrec[sel].mean())}
+res["e1_end_us"] = float((st[idx < int(os.environ.get("NWIN", "1e12")), 4].max() - t0) / 100.0) if "NWIN" in os.environ else None
 per_block = np.bincount(block, weights=tot)
 res["busiest_block_sum_us"] = float(per_block.max())
 res["mean_block_sum_us"] = float(per_block[per_block > 0].mean())
