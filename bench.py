@@ -8,9 +8,12 @@ Zipf(1.1)-over-lectures x uniform-over-days stream of 8-digit ids with 10 %
 invalid swipes, and the HLL keys this rank owns (distributed.KeyMap:
 MurmurHash64A(key name) mod world over the 100k README-form key names; all
 of them at N = 1, ~12.5k per rank at N = 8).  One step = one K1 call over
-one resident batch of 16M swipes (answers written, PFADD of the valid ones):
-the partitioned K1, three kernels (sketch_part.hip: hash + probe records,
-LDS-slice probes, answers + register max).  `--config c2` runs C2 (1M
+one resident batch of 2^27 swipes per GPU (C3's 1B-swipe stream in 8 steps;
+answers written, PFADD of the valid ones): the partitioned K1 in even
+sub-batches of at most 16M swipes (sketch_part.hip: hash + probe records,
+LDS-slice probes, answers + the segmented PFADD's records and level-2 sort),
+then one window pass of the segmented PFADD over the slab (each key window
+staged in LDS, raised, its risen lines flushed).  `--config c2` runs C2 (1M
 swipes, the LDS K1).
 
 Inputs are generated on the GPU and resident in HBM before timing; every
@@ -67,6 +70,11 @@ METRIC = "swipes/sec (fused BF.EXISTS+PFADD) at 1/2/4/8 GPUs; % of HBM peak"
 PASS_NAMES = ["k1", "k_part_a", "k_part_b", "k_part_c", "k_seg_d", "k_seg_e"]
 PMC_ROUNDS = ["r05", "r04", "r03", "r02"]  # newest committed PMC summaries first
 VERIFY_KEYS = 64
+# swipes per GPU and step where it differs from the workload's own
+# step_swipes: C3 since round 5 takes 2^27 (its 1B-swipe stream in 8 steps;
+# the segmented PFADD streams each key window of the slab once per step, so
+# the step is sized to several register updates per slab line -- DESIGN.md §3)
+BENCH_STEP = {"c3": 1 << 27}
 
 
 def parse(argv=None):
@@ -648,7 +656,7 @@ class Run:
         # the probability mass of this rank's keys in the global stream
         self.mass = float(probs[mine].sum()) if probs is not None else mine.size / len(self.names)
         self.shares = "equal" if args.exchange else args.shares
-        self.n = n = rank_swipes(args.batch or w.step_swipes, self.mass, kw, self.shares)
+        self.n = n = rank_swipes(args.batch or BENCH_STEP.get(cfg, w.step_swipes), self.mass, kw, self.shares)
         self.engine = engine = SketchEngine(local)
         self.stream = stream = torch.cuda.Stream()  # shared by libsketch and torch
         torch.cuda.set_stream(stream)
@@ -942,7 +950,7 @@ class Run:
         a, tag = self.args, self.cfg
         if a.shard:
             tag += "_shard%d" % self.kw
-        if a.batch:
+        if a.batch and a.batch != BENCH_STEP.get(self.cfg, self.w.step_swipes):
             tag += "_b%dm" % (a.batch >> 20)
         return tag + ("_seg" if seg else "")
 

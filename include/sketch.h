@@ -299,9 +299,10 @@ int ske_swipes_variant(ske_ctx *ctx, uint32_t fid);
  * swipes per sub-batch, 0 = 16M), "pass_timing" (0/1); the partitioned K1's
  * segmented PFADD: "hll_seg" (-1 auto, 0 never, 1 whenever the
  * chain and slab allow), "seg_density" (auto: swipes per 128-B slab line at
- * which a batch is segmented, x100), "seg_dense_min" (records per window line
- * at which a window is staged in LDS, x100), "seg_klog" (2 or 3: keys per
- * window 4 or 8).  Any other name or an out-of-range value: SKE_EINVAL.  None
+ * which a batch is segmented, x100, default 600, doubled for a slab of at
+ * most 192 MB), "seg_dense_min" (records per window line at which a window
+ * is staged in LDS, x100), "seg_klog" (0..3: keys per window 1, 2, 4, 8;
+ * default 1).  Any other name or an out-of-range value: SKE_EINVAL.  None
  * changes an answer or a register. */
 int ske_set_option(ske_ctx *ctx, const char *name, int64_t value);
 /* Kernel timing for the benchmark's roofline: with option "pass_timing" = 1

@@ -144,9 +144,10 @@ bool part_supported(const ChainDev &ch);
 // "seg_density" and "seg_dense_min" (x100), "seg_klog".
 struct SegOpts {
     int mode = -1;                  // -1 auto, 0 never (pass C), 1 whenever the chain and slab allow
-    uint32_t density_x100 = 200;    // auto: a batch's swipes per 128-B line of the slab, x100
+    uint32_t density_x100 = 600;    // auto: a batch's swipes per 128-B line of the slab, x100 (x2 when the
+                                    // slab fits the Infinity Cache, where pass C's random requests are cheaper)
     uint32_t dense_min_x100 = 100;  // a window is staged in LDS from this many records per line, x100
-    int klog = 3;                   // keys per window: 2^klog (16 KiB each; 0..3)
+    int klog = 1;                   // keys per window: 2^klog (16 KiB each; 0..3)
 };
 // sizes the context scratch for batches of up to n swipes (no launch)
 // sub: swipes per sub-batch of the three passes (0: the default, 16M)

@@ -1448,7 +1448,7 @@ template <int KLOG> struct SegE {
     static constexpr uint32_t T = KLOG >= 2 ? 1024 : (KLOG == 1 ? 512 : 256);
     static constexpr uint32_t BPC = KLOG >= 3 ? 1 : (KLOG == 2 ? 2 : (KLOG == 1 ? 4 : 8));
     static constexpr uint32_t WPS = T / 64 * BPC / 4;  // waves per SIMD (launch bounds)
-    static constexpr uint32_t RPT = KLOG >= 3 ? 16 : 8;  // records per thread per round
+    static constexpr uint32_t RPT = KLOG >= 3 ? 16 : (KLOG == 2 ? 8 : 4);  // records per thread per round
     static constexpr uint32_t EP = KLOG == 2 ? 512 : T;  // runs staged at once
 };
 __host__ __device__ constexpr uint32_t seg_slice(uint32_t klog) { return 16384u << (klog < 2 ? klog : 2); }
@@ -1465,24 +1465,26 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
     __shared__ uint8_t dirty[NL];
     __shared__ uint32_t rb[EP], rp[EP + 1];
     __shared__ uint32_t spre[2][65], cq0[2][64], ws[T / 64], hdr[2];
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t nb1m = S.nb1 - 1;  // buckets: a power of two, window W in bucket W & nb1m
     const uint32_t nitems = QUEUE ? S.q[0] : S.nwin;
+    const __amdgpu_buffer_rsrc_t rr2 = part_rsrc(S.r2, S.nsub * S.maxch * kSegChunk * 4);
     // Items (E1: windows, E2: queued slices) go round robin over the blocks.
     // Each item's layout -- its bucket's chunk counts per sub-batch (spre:
     // prefix, cq0: the first chunk; nsub <= 64), double-buffered by item
     // parity -- its first EP runs and its window's registers are fetched in
     // phases while the previous item's records are raised and its lines
     // stored:
-    //   P1  the bucket's chunk columns and the window's registers (loads);
-    //   P2  the column prefix (scan), then the item's first EP runs (loads);
+    //   P1  the bucket's chunk columns (loads), while the records are raised;
+    //   P2  the column prefix (scan), then the item's first EP runs (loads),
+    //       while the lines are stored; then the window's registers by
+    //       LDS-DMA into `win`;
     //   P3  the runs' prefix (scan) and record count, when the item starts.
     // (Buckets interleave windows, so a hot key's windows fall in different
     // buckets and every bucket has about the same chunks: a window's runs
     // rarely exceed EP; more are counted and staged in batches.)
     uint32_t cq = 0, cc = 0;                // P1: this thread's sub-batch column
     uint32_t pbase = 0, plen = 0, pnp = 0;  // P2: this thread's run, the item's runs
-    part_u32x4 v[NPC];
     auto item = [&](uint32_t it, uint32_t &wi, uint32_t &sl, uint32_t &copy) {
         wi = it;
         sl = 0;
@@ -1500,13 +1502,20 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
             cq = S.cb[size_t(tid) * (S.nb1 + 1) + h];
             cc = S.cb[size_t(tid) * (S.nb1 + 1) + h + 1];
         }
+    };
+    // the window's registers into `win` by LDS-DMA (1 KiB per wave
+    // instruction, no VGPRs; bytes past the slab read as zero), waited for by
+    // the __syncthreads() before the records are raised
+    auto image = [&](uint32_t wi) {
         const uint32_t slot0 = wi << KLOG;
         const uint32_t nk = A.nslots - slot0 < KW ? A.nslots - slot0 : KW;
-        const part_u32x4 *g = reinterpret_cast<const part_u32x4 *>(A.regs + (size_t(slot0) << kHllP));
+        const __amdgpu_buffer_rsrc_t r = part_rsrc(A.regs + (size_t(slot0) << kHllP), nk << kHllP);
 #pragma unroll
         for (uint32_t i = 0; i < NPC; i++) {
-            const uint32_t j = i * T + tid;
-            v[i] = j < (nk << (kHllP - 4)) ? g[j] : part_u32x4{0, 0, 0, 0};
+            const uint32_t piece = i * (T / 64) + wave;  // 1 KiB pieces
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                r, (__attribute__((address_space(3))) void *)(win + piece * 1024), 16,
+                int(piece * 1024 + lane * 16), 0, 0, 0);
         }
     };
     // run x of window column w2 of the bucket staged in buffer pb
@@ -1536,6 +1545,7 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
         item(it, wi_n, sl_n, copy_n);
         p1(wi_n);
         p2(0, wi_n);
+        image(wi_n);
     }
     for (; it < nitems; it += gridDim.x, par ^= 1) {
         const uint32_t wi = wi_n, sl = sl_n;
@@ -1588,12 +1598,9 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
         const uint32_t lo = cut ? sl * SLICE : 0;
         const uint32_t hi = cut ? (nrec - lo < SLICE ? nrec : lo + SLICE) : nrec;
         const bool dense = nrec > 0 && (cut || nrec >= S.dense_min);
-        if (dense) {
+        if (dense)
             for (uint32_t j = tid; j < NL; j += T) dirty[j] = 0;
-#pragma unroll
-            for (uint32_t i = 0; i < NPC; i++) reinterpret_cast<part_u32x4 *>(win)[i * T + tid] = v[i];
-        }
-        lds_barrier();  // the window's LDS image and its first runs are staged
+        __syncthreads();  // the window's registers landed in LDS (vmcnt), its first runs staged
         // P1 of the next item: its loads fly while this item's records are raised
         const uint32_t nit = it + gridDim.x;
         if (nit < nitems) {
@@ -1601,8 +1608,7 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
             p1(wi_n);
         }
         SEG_STAMP(stamp, 2, 0);
-        // records [lo, hi) of the concatenated runs, RPT consecutive ones per
-        // thread and round; runs staged EP at a time
+        // records [lo, hi) of the concatenated runs, runs staged EP at a time
         for (uint32_t x0 = 0, p0 = 0; x0 < np && p0 < hi; x0 += EP) {
             const uint32_t nx = np - x0 < EP ? np - x0 : EP;
             uint32_t btot = nrec0;
@@ -1618,39 +1624,58 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
                 if (tid == 0) rp[nx] = btot;
                 lds_barrier();
             }
-            // this batch's records [p0, p0 + btot) of the window; ours: [lo, hi)
+            // this batch's records [p0, p0 + btot) of the window; ours: [lo, hi).
+            // A wave takes 64 * RPT consecutive records per round, lane l the
+            // ones at l + 64 c (coalesced loads); the run of the wave's first
+            // record is searched once and every lane walks on from it.
             const uint32_t f_lo = lo > p0 ? lo - p0 : 0, f_hi = hi - p0 < btot ? hi - p0 : btot;
-            for (uint32_t f0 = f_lo + tid * RPT; f0 - tid * RPT < f_hi; f0 += T * RPT) {
-                uint32_t rec[RPT];
-                if (f0 < f_hi) {
-                    uint32_t j = seg_last_le(rp, nx, f0);
-#pragma unroll
-                    for (uint32_t c = 0; c < RPT; c++) {
-                        const uint32_t f = f0 + c;
-                        rec[c] = 0;
-                        if (f < f_hi) {
-                            while (rp[j + 1] <= f) j++;
-                            rec[c] = S.r2[rb[j] + (f - rp[j])];
-                        }
-                    }
-                } else {
+            // (dense: the window's registers in LDS; sparse: in place, in HBM)
+            const __amdgpu_buffer_rsrc_t rgw = part_rsrc(g, npc * 16);
+            auto round = [&](auto dense_c) {
+                constexpr bool D = decltype(dense_c)::value;
+                for (uint32_t r0 = f_lo + wave * 64 * RPT; r0 - wave * 64 * RPT < f_hi; r0 += T * RPT) {
+                    uint32_t rec[RPT];
 #pragma unroll
                     for (uint32_t c = 0; c < RPT; c++) rec[c] = 0;
-                }
+                    if (r0 < f_hi) {  // wave-uniform
+                        uint32_t j = seg_last_le(rp, nx, r0);
 #pragma unroll
-                for (uint32_t c = 0; c < RPT; c++) {
-                    const uint32_t rank = rec[c] & 63u;
-                    if (rank == 0) continue;
-                    const uint32_t ad = (((rec[c] >> kSegRecShift) & (KW - 1)) << kHllP) | ((rec[c] >> 6) & 0x3fffu);
-                    if (dense) {
-                        if (seg_lds_max(reinterpret_cast<uint32_t *>(win + (ad & ~3u)), (ad & 3u) * 8, rank))
-                            dirty[ad >> 7] = 1;
-                    } else {
-                        uint32_t *w = reinterpret_cast<uint32_t *>(g + (ad & ~3u));
-                        part_reg_max(w, (ad & 3u) * 8, rank, *w);
+                        for (uint32_t c = 0; c < RPT; c++) {
+                            const uint32_t f = r0 + c * 64 + lane;
+                            if (f < f_hi) {
+                                while (rp[j + 1] <= f) j++;
+                                rec[c] = __builtin_amdgcn_raw_buffer_load_b32(rr2, (rb[j] + (f - rp[j])) * 4, 0, 0);
+                            }
+                        }
+                    }
+                    // the registers' words, all read before any CAS (a raise
+                    // is rare once the slab is warm)
+                    uint32_t old[RPT];
+#pragma unroll
+                    for (uint32_t c = 0; c < RPT; c++) {
+                        const uint32_t a = (((rec[c] >> kSegRecShift) & (KW - 1)) << kHllP) | ((rec[c] >> 6) & 0x3fffu);
+                        old[c] = 0xffffffffu;
+                        if (rec[c] & 63u)
+                            old[c] = D ? reinterpret_cast<const uint32_t *>(win)[a >> 2]
+                                       : __builtin_amdgcn_raw_buffer_load_b32(rgw, a & ~3u, 0, 0);
+                    }
+#pragma unroll
+                    for (uint32_t c = 0; c < RPT; c++) {
+                        const uint32_t a = (((rec[c] >> kSegRecShift) & (KW - 1)) << kHllP) | ((rec[c] >> 6) & 0x3fffu);
+                        const uint32_t rank = rec[c] & 63u, sh = (a & 3u) * 8;
+                        if (((old[c] >> sh) & 0xffu) >= rank) continue;
+                        if constexpr (D) {
+                            if (seg_lds_max(reinterpret_cast<uint32_t *>(win + (a & ~3u)), sh, rank)) dirty[a >> 7] = 1;
+                        } else {
+                            part_reg_max(reinterpret_cast<uint32_t *>(g + (a & ~3u)), sh, rank, old[c]);
+                        }
                     }
                 }
-            }
+            };
+            if (dense)
+                round(std::true_type{});
+            else
+                round(std::false_type{});
             p0 += btot;
         }
         lds_barrier();  // every raise in LDS done; rb / rp free
@@ -1673,6 +1698,7 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
             }
         }
         lds_barrier();  // win, dirty and hdr are rewritten by the next item
+        if (nit < nitems) image(wi_n);
         SEG_STAMP(stamp, 4, uint64_t(nrec) | (uint64_t(np) << 32) | (uint64_t(dense) << 63));
     }
 }
@@ -1831,7 +1857,10 @@ static bool seg_plan(uint32_t nslots, uint64_t n, uint32_t sub, const SegOpts &s
 static bool seg_use(const PartArgs &A, const SegOpts &so, uint32_t nslots, uint64_t n, uint32_t sub, SegPlan *P) {
     if (so.mode == 0 || !part_flist(A) || !seg_plan(nslots, n, sub, so, P)) return false;
     if (so.mode == 1) return true;
-    return n * 100 >= uint64_t(so.density_x100) * nslots * (kHllRegs / 128);
+    // break-evens measured at C3: ~5 swipes per line over a
+    // 1.6 GB slab, ~12 over a 205 MB one that the 256 MiB Infinity Cache holds
+    const uint64_t thr = uint64_t(so.density_x100) * ((uint64_t(nslots) << kHllP) <= (192ull << 20) ? 2 : 1);
+    return n * 100 >= thr * nslots * (kHllRegs / 128);
 }
 
 // the segmented PFADD's scratch (context slots 32-38)

@@ -279,3 +279,42 @@ def test_c3_bench_shard_one_gpu(engine, orc):
     assert np.array_equal(out.to_host(np.uint8, b.n), answers[0])
     got = engine.registers_all(w.n_keys)
     assert np.array_equal(got, regs)
+
+
+@pytest.mark.parametrize("world", [1, 8])
+def test_c3_bench_step_128m_segmented(engine, orc, world):
+    """C3 at bench.py's default step since round 5 (2^27 swipes per GPU: a
+    1B-swipe C3 stream in 8 steps), on one GPU's keys at N = 1 (100k Zipf
+    lecture-day keys, a 1.6 GB slab) and at N = 8 (synthetic.shard(c3, 8):
+    12.5k keys, 205 MB).  The auto choice takes the segmented PFADD at this
+    density (asserted through the pass timing kinds); every answer and every
+    register bit-exact vs the oracle (its multi-threaded per-event loop,
+    identical results to the sequential one)."""
+    import os
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import DeviceBuffer
+    w = synthetic.shard(synthetic.WORKLOADS["c3"], world)
+    p = _setup(engine, w)
+    n = 1 << 27
+    b = engine.swipe_batch(p, 0, n)
+    out = DeviceBuffer(engine.ctx, n)
+    engine.set_option("pass_timing", 1)
+    engine.pass_times(reset=True)
+    engine.swipes(0, b, out)
+    pt = engine.pass_times(reset=True)
+    engine.set_option("pass_timing", 0)
+    assert pt[5][1] == 1 and pt[4][1] == 8, pt  # one window pass, 8 sub-batches
+    chain = orc.Chain(w.bf_capacity, w.bf_error)
+    mb = engine.members_batch(p, 0, w.n_members)
+    mbuf, moffs, _ = mb.to_host()
+    mb.free()
+    chain.madd_packed(mbuf, moffs)
+    buf, offs, slot = b.to_host()
+    b.free()
+    regs = np.zeros((w.n_keys, 16384), np.uint8)
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    want, nvalid, _ = orc.process_swipes(chain, regs, slot.astype(np.uint32), buf, offs, threads=threads)
+    del buf, offs, slot
+    assert np.array_equal(out.to_host(np.uint8, n), want)
+    assert np.array_equal(engine.registers_all(w.n_keys), regs)
+    assert 0.85 < nvalid / n < 0.95

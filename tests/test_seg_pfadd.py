@@ -189,23 +189,29 @@ def test_seg_out_of_range_slot(engine, orc):
 
 
 def test_seg_auto_choice(engine):
-    """auto (-1): segmented from 2 swipes per slab line (seg_density 200);
-    the plan is the library's, visible through the pass timing kinds."""
+    """auto (-1): segmented from seg_density / 100 swipes per 128-B slab
+    line (default 6), twice that for a slab the Infinity Cache holds (this
+    one: 100 keys, 1.6 MB, 12 800 lines -> 153 600 swipes); the choice is the
+    library's, visible through the pass timing kinds."""
     from rtsas_amd.engine import DeviceBuffer
     w, p = _c3(engine, lectures=10, days=10)   # 100 keys = 12 800 lines
     out = DeviceBuffer(engine.ctx, 1 << 20)
     engine.set_option("pass_timing", 1)
-    for n, seg in ((20_000, False), (30_000, True)):
+
+    def seg_used(n):
         engine.pass_times(reset=True)
-        b = engine.swipe_batch(p, 0, n)
-        engine.swipes(0, b, out)
+        engine.swipes(0, engine.swipe_batch(p, 0, n), out)
         pt = engine.pass_times(reset=True)
-        assert (pt[5][1] > 0) == seg, (n, pt)
         assert pt[3][1] > 0
+        return pt[5][1] > 0
+
+    assert not seg_used(150_000) and seg_used(160_000)
+    engine.set_option("seg_density", 100)  # 2 per line (x2 on chip): 25 600
+    assert not seg_used(25_000) and seg_used(26_000)
     engine.set_option("hll_seg", 0)
-    engine.pass_times(reset=True)
-    engine.swipes(0, engine.swipe_batch(p, 0, 1 << 20), out)
-    assert engine.pass_times(reset=True)[5][1] == 0
+    assert not seg_used(1 << 20)
+    engine.set_option("hll_seg", 1)
+    assert seg_used(1000)
     engine.set_option("pass_timing", 0)
 
 
