@@ -1908,6 +1908,9 @@ hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, uint32
     if (e == hipSuccess && seg_use(A, so, nslots, n ? n : 1, sub, &P)) {
         SegArgs S{};
         e = seg_scratch(P, sub, n, scr, &S);
+        // scratch that cannot grow under a recorded graph: such a batch takes
+        // pass C instead (launch_swipes_part decides the same way)
+        if (e == hipErrorStreamCaptureUnsupported) e = hipSuccess;
     }
     return e;
 }
@@ -1952,9 +1955,15 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
         // the segmented PFADD (k_seg_*) for this batch, or pass C per sub-batch
         SegPlan P;
         SegArgs S{};
-        const bool seg = flist && seg_use(A, so, nslots, B.n, subj, &P);
+        bool seg = flist && seg_use(A, so, nslots, B.n, subj, &P);
         if (seg) {
             e = seg_scratch(P, subj, B.n, scr, &S);
+            // (recording a graph with scratch too small for this batch's
+            // segmented PFADD: the batch takes pass C, same answers and registers)
+            if (e == hipErrorStreamCaptureUnsupported) {
+                seg = false;
+                e = hipSuccess;
+            }
             if (e != hipSuccess) return e;
         }
         uint32_t si = 0;
