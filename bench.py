@@ -1042,33 +1042,45 @@ def main():
 
     run = Run(args, args.config, world, rank, local, dev, dist)
     elapsed, step_ms, host_enqueue = run.timed()
+    free_b, total_b = torch.cuda.mem_get_info(dev)
+    mem_used = float(total_b - free_b)  # the device's (all ranks on it: the rank's own on a node)
     cdev = dev if args.dist_backend == "nccl" else "cpu"
     my_elapsed = elapsed
     total_swipes = run.n
     shares = {"mode": run.shares, "swipes_per_step": [run.n], "key_mass": [run.mass],
-              "elapsed_s": [elapsed]}
+              "elapsed_s": [elapsed], "device_mem_used_GB": [mem_used / 1e9]}
     if world > 1:
         t = torch.tensor([elapsed, step_ms], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, step_ms = float(t[0]), float(t[1])
         # every rank's batch, key mass and wall time (the slowest bounds the job)
-        g = torch.zeros(3 * world, dtype=torch.float64, device=cdev)
-        g[3 * rank:3 * rank + 3] = torch.tensor([run.n, run.mass, my_elapsed], dtype=torch.float64)
+        g = torch.zeros(4 * world, dtype=torch.float64, device=cdev)
+        g[4 * rank:4 * rank + 4] = torch.tensor([run.n, run.mass, my_elapsed, mem_used], dtype=torch.float64)
         dist.all_reduce(g, op=dist.ReduceOp.SUM)
-        g = g.view(world, 3).cpu().tolist()
+        g = g.view(world, 4).cpu().tolist()
         total_swipes = int(sum(r[0] for r in g))
         shares = {"mode": run.shares, "swipes_per_step": [int(r[0]) for r in g],
-                  "key_mass": [r[1] for r in g], "elapsed_s": [r[2] for r in g]}
+                  "key_mass": [r[1] for r in g], "elapsed_s": [r[2] for r in g],
+                  "device_mem_used_GB": [r[3] / 1e9 for r in g],
+                  "device_mem_note": "hipMemGetInfo used bytes of each rank's device after timing (ranks "
+                                     "sharing a GPU in a rehearsal see their sum)"}
     mean_n = total_swipes / world
     shares.update({"rank_share_max": max(shares["swipes_per_step"]) / mean_n,
                    "rank_share_min": min(shares["swipes_per_step"]) / mean_n,
                    "slowest_rank": int(max(range(world), key=lambda r: shares["elapsed_s"][r]))})
     pt = run.replay_instrumented() if args.pass_replay else None
+    pt_rank = rank
     if world > 1 and pt is not None:
-        t = torch.tensor([ms for ms, _ in pt], dtype=torch.float64,
-                         device=dev if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        pt = [(float(t[i]), c) for i, (_, c) in enumerate(pt)]
+        # the per-pass times of the slowest rank (the one that bounds the
+        # job's time), every rank's gathered
+        k = len(pt)
+        t = torch.zeros(world * 2 * k, dtype=torch.float64, device=cdev)
+        t[rank * 2 * k:(rank + 1) * 2 * k] = torch.tensor([x for ms, c in pt for x in (ms, c)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        allp = t.view(world, k, 2).cpu().tolist()
+        pt_rank = shares["slowest_rank"]
+        pt = [(float(ms), int(c)) for ms, c in allp[pt_rank]]
+        shares["pass_ms_per_rank"] = [[ms / c if c else 0.0 for ms, c in r] for r in allp]
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = total_swipes * args.steps / elapsed
@@ -1086,7 +1098,7 @@ def main():
         "dtype": "u64",
         "data": "synthetic (device counter-based generator, seed %d)" % run.w.seed,
         "config": run.config(),
-        "roofline": run.roofline(pt, step_ms),
+        "roofline": {**run.roofline(pt, step_ms), "passes_of_rank": pt_rank},
         "preload_s": run.preload_s,
         "host_enqueue_us_per_step": host_enqueue * 1e6 / args.steps,
         "rank_shares": shares,

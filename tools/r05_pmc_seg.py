@@ -16,7 +16,7 @@ root, prefix = sys.argv[1], sys.argv[2]
 SKIP_SUB, SKIP_STEP = 16, 2
 plan = {"k_part_a": (["k_part_a3"], SKIP_SUB), "k_part_b": (["k_part_b"], SKIP_SUB),
         "k_part_c": (["k_seg_c1"], SKIP_SUB), "k_seg_d": (["k_seg_scan", "k_seg_d("], SKIP_SUB),
-        "k_seg_e": (["k_seg_eILi1ELb0", "k_seg_eILi1ELb1", "k_seg_mILi1"], SKIP_STEP)}
+        "k_seg_e": (["k_seg_e<1, false>", "k_seg_e<1, true>", "k_seg_m<1>"], SKIP_STEP)}
 for name, (kernels, skip) in plan.items():
     parts = {k: summarise(root, k, skip) for k in kernels}
     mean = {}
