@@ -555,9 +555,21 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
         const __amdgpu_buffer_rsrc_t rdst = part_rsrc(A.rec + size_t(t) * A.stride, A.stride * 4);
         // (a piece past the records reads the last piece instead: an LDS read
         // past srec would be undefined behaviour, from which the compiler may
-        // infer a bound on tid for the rest of the kernel)
+        // infer a bound on tid for the rest of the kernel -- round 4 had one:
+        // the unclamped index read past srec for the last pieces, and the
+        // partitioned-K1 answers of some A/B builds were wrong; the
+        // 2048-counter case of tests/test_k1_partitioned.py pins the fix)
         const part_u32x4 *src = reinterpret_cast<const part_u32x4 *>(srec);
         constexpr uint32_t kLast = kRecWords / 4 - 1;
+        static_assert(kRecWords % 4 == 0 && kCo * kT >= kLast + 1, "the copy-out covers srec in 16-B pieces");
+        static_assert([] {  // every piece index the copy-out reads is inside srec
+            for (uint32_t c = 0; c < kCo; c++)
+                for (uint32_t t = 0; t < kT; t++) {
+                    const uint32_t j = c * kT + t;
+                    if (((c + 1) * kT <= kLast + 1 ? j : (j < kLast ? j : kLast)) > kLast) return false;
+                }
+            return true;
+        }(), "copy-out LDS index bound");
 #pragma unroll
         for (uint32_t c = 0; c < kCo; c++) {
             const uint32_t j = c * kT + tid;
