@@ -830,6 +830,11 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
         c->seg.klog = int(value);
         return SKE_OK;
     }
+    if (!strcmp(name, "rec_groups")) {  // pass A's records in the group layout: -1 auto, 0 per-tile runs, 1 on
+        if (value < -1 || value > 1) return SKE_EINVAL;
+        c->seg.rec_groups = int(value);
+        return SKE_OK;
+    }
     if (!strcmp(name, "k1_grid")) {
         if (value < 0 || value > 65535) return SKE_EINVAL;
         c->k1_grid = int(value);

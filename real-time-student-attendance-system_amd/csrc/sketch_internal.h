@@ -148,6 +148,11 @@ struct SegOpts {
                                     // slab fits the Infinity Cache, where pass C's random requests are cheaper)
     uint32_t dense_min_x100 = 100;  // a window is staged in LDS from this many records per line, x100
     int klog = 1;                   // keys per window: 2^klog (16 KiB each; 0..3)
+    // option "rec_groups": pass A's probe records in the group layout (a
+    // unit's runs of 8 tiles adjacent; one-link k = 11 chains under 1024
+    // slices): 1 whenever the chain allows; -1 auto and 0: per-tile runs
+    // (the group layout costs pass A more than it saves pass B)
+    int rec_groups = -1;
 };
 // sizes the context scratch for batches of up to n swipes (no launch)
 // sub: swipes per sub-batch of the three passes (0: the default, 16M)

@@ -49,6 +49,7 @@
 // Placement of blocks on XCDs is a speed matter only; every (tile, slice) run
 // is read by exactly one block, and fail marks are only ever set.
 #include <algorithm>
+#include <cmath>
 #include <type_traits>
 
 #include "sketch_common.h"
@@ -100,6 +101,10 @@ struct PartArgs {
     uint32_t fixed_w, n, stride, ntiles, nslices, nlinks, ksum, nslots, fail_stride, off_stride;
     uint16_t *flist;       // [nunits][fl_stride][kPbLanes] fail lists (pass B -> pass C), or nullptr
     uint32_t nunits, fl_stride;
+    // group layout (gcap != 0; k_part_a3 / k_part_b<2, 4, true, true>): the
+    // runs of a unit over a group of 8 tiles adjacent in rec[group][unit][gcap],
+    // a run that does not fit at its tile's place in rec[govf + tile * stride]
+    uint32_t gcap, govf;
     PartLink link[kPMaxLinks];
 };
 
@@ -120,9 +125,11 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // is placement for speed only: every tile of a group is handled by exactly one
 // block of the group, whichever XCD it runs on.
 constexpr uint32_t kPGroups = 8;
+// (group edges on multiples of 8 tiles: pass B's rounds and the group layout's
+// 8-tile groups never straddle two XCD groups)
 __device__ __forceinline__ void part_group(uint32_t ntiles, uint32_t x, uint32_t &t0, uint32_t &t1) {
-    t0 = uint32_t(uint64_t(ntiles) * x / kPGroups);
-    t1 = uint32_t(uint64_t(ntiles) * (x + 1) / kPGroups);
+    t0 = uint32_t(uint64_t(ntiles) * x / kPGroups) & ~7u;
+    t1 = x + 1 == kPGroups ? ntiles : uint32_t(uint64_t(ntiles) * (x + 1) / kPGroups) & ~7u;
 }
 
 // Bit (pos & 31) of w: v_bfe_u32 reads only its offset operand's low 5 bits,
@@ -393,14 +400,21 @@ constexpr uint32_t kOORa = 0x80000000u;  // a buffer offset past every range: lo
 #ifndef SKE_PA_WAIT_LAST
 #define SKE_PA_WAIT_LAST 1  // round 4 A/B: pass A 0.226-0.230 -> 0.225 ms
 #endif
-template <int KM, uint32_t kCnt>
+// GL: the group layout (PartArgs::gcap).  A block takes whole groups of 8
+// consecutive tiles, one tile after the other, and keeps each of its units'
+// place in the group's region in a register; every run starts on a 16-B
+// piece (padded to 4 records in LDS and in the region), so the copy-out stays
+// one 16-B store per piece, to the place an LDS map gives the piece's unit.
+template <int KM, uint32_t kCnt, bool GL = false>
 __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two blocks per CU
     constexpr uint32_t kT = 512;
     constexpr uint32_t kU = 1024 / kT, kTile = 1024;
     constexpr uint32_t kPer = kCnt / kT;  // counters per thread: kPer / 2 whole pairs
-    constexpr uint32_t kRecWords = kTile * KM;  // (the sink's records land past the copy-out)
+    // (the sink's records land past the copy-out; GL: a unit's run padded to 4)
+    constexpr uint32_t kRecWords = kTile * KM + (GL ? 4 * (kCnt / 2) : 0);
     constexpr uint32_t kCo = (kRecWords / 4 + kT - 1) / kT;  // 16-B copy-out pieces per thread
-    static_assert(kCnt % (2 * kT) == 0 && 4u * kTile * KM < 65536u,
+    constexpr uint32_t kMap = GL ? kRecWords / 4 : 1;        // GL: a piece's place - its LDS place
+    static_assert(kCnt % (2 * kT) == 0 && 4u * kRecWords < 65536u,
                   "whole pairs per thread; a rank * 4 below bit 16; starts fit 16 bits");
     // one LDS object, counters first: it sits at LDS address 0, so a probe's
     // counter address is its slice field shifted and added to the parity's
@@ -408,6 +422,7 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
     struct __attribute__((aligned(16))) Lds {
         uint32_t cnt[2 * kCnt];
         uint32_t srec[kRecWords];
+        uint32_t dmap[kMap];
         uint32_t swsum[kT / 64];
         uint32_t stot;
     };
@@ -441,12 +456,20 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
     uint32_t gt0, gt1;
     part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
     const uint32_t tstep = gridDim.x / kPGroups;
+    // this block's tiles: every tstep-th of its group's (GL: every tstep-th
+    // group of 8 tiles, its tiles in order; gt0 is a multiple of 8)
+    const uint32_t tfirst = GL ? gt0 + 8 * (blockIdx.x / kPGroups) : gt0 + blockIdx.x / kPGroups;
+    auto tnext = [&](uint32_t t) {
+        if constexpr (GL) return (t & 7u) != 7u && t + 1 < gt1 ? t + 1 : (t & ~7u) + 8 * tstep;
+        else return t + tstep;
+    };
     const __amdgpu_buffer_rsrc_t rbytes = part_rsrc(A.bytes, 0xfffffff0u);
     const PartLink &L = A.link[0];
     uint32_t nb_[kU], ne_[kU];
     PartId it[kU];
+    uint32_t gofs[kPer / 2] = {};  // GL: this thread's units' places in the current group
     {
-        const uint32_t t = gt0 + blockIdx.x / kPGroups;
+        const uint32_t t = tfirst;
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++) {
             offsets(t < gt1 ? t : gt0, u, nb_[u], ne_[u]);
@@ -468,7 +491,7 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
         const uint32_t cb = par * kCnt;
         const uint32_t pb = cb * 4;  // the parity's byte base, above (kCnt - 1) * 4
         uint32_t rv[kU][KM], rp[kU][KM];
-        const uint32_t tn = t + tstep < gt1 ? t + tstep : t;
+        const uint32_t tn = tnext(t) < gt1 ? tnext(t) : t;
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++) offsets(tn, u, nb_[u], ne_[u]);
         const bool full = (t + 1) * kTile <= A.n;  // block-uniform
@@ -521,7 +544,7 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
             v[j] = (cnt[c] - (c << 18)) >> 2;
         }
 #pragma unroll
-        for (uint32_t j = 0; j < kPer; j += 2) s += v[j] + v[j + 1];
+        for (uint32_t j = 0; j < kPer; j += 2) s += GL ? (v[j] + v[j + 1] + 3) & ~3u : v[j] + v[j + 1];
         const uint32_t incl = part_wave_scan(s);
         if (lane == 63) swsum[wave] = incl;
         lds_barrier();
@@ -530,12 +553,24 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
 #pragma unroll
         for (uint32_t j = 0; j < kPer; j += 2) {
             const uint32_t g = tid * kPer + j, c = cb + g, un = g / 2, n2 = v[j] + v[j + 1];
-            __builtin_amdgcn_raw_buffer_store_b32(run | (n2 << 16), roff, un < nunits ? (un * A.off_stride + t) * 4 : kOORa,
-                                                  0, 0);  // pass B's run: start | count << 16
+            uint32_t W = run | (n2 << 16);  // pass B's run: start | count << 16
+            if constexpr (GL) {
+                // the unit's next place in the group's region, or (it does not
+                // fit) its LDS place in the tile's overflow row: bit 31
+                const uint32_t p4 = (n2 + 3) & ~3u;
+                if ((t & 7u) == 0) gofs[j / 2] = 0;
+                const bool fits = gofs[j / 2] + p4 <= A.gcap;
+                const uint32_t dst = fits ? ((t >> 3) * nunits + un) * A.gcap + gofs[j / 2] : A.govf + t * A.stride + run;
+                W = fits ? gofs[j / 2] | (n2 << 16) : W | 0x80000000u;
+                if (fits) gofs[j / 2] += p4;
+                if (un < nunits)
+                    for (uint32_t p = run / 4; p < (run + p4) / 4; p++) lds.dmap[p] = dst - run;
+            }
+            __builtin_amdgcn_raw_buffer_store_b32(W, roff, un < nunits ? (un * A.off_stride + t) * 4 : kOORa, 0, 0);
             if (g == sink) stot = run;
             cnt[c] = 4 * run - (c << 18);
             cnt[c + 1] = 4 * (run + v[j]) - ((c + 1) << 18);
-            run += n2;
+            run += GL ? (n2 + 3) & ~3u : n2;
         }
         lds_barrier();
 #pragma unroll
@@ -552,7 +587,8 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
         const uint32_t total = stot;
         // a fixed number of 16-B pieces per thread (those past the tile's
         // total go out of range)
-        const __amdgpu_buffer_rsrc_t rdst = part_rsrc(A.rec + size_t(t) * A.stride, A.stride * 4);
+        const __amdgpu_buffer_rsrc_t rdst =
+            GL ? part_rsrc(A.rec, (A.govf + A.ntiles * A.stride) * 4) : part_rsrc(A.rec + size_t(t) * A.stride, A.stride * 4);
         // (a piece past the records reads the last piece instead: an LDS read
         // past srec would be undefined behaviour, from which the compiler may
         // infer a bound on tid for the rest of the kernel -- round 4 had one:
@@ -574,12 +610,13 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
         for (uint32_t c = 0; c < kCo; c++) {
             const uint32_t j = c * kT + tid;
             const uint32_t jr = (c + 1) * kT <= kLast + 1 ? j : (j < kLast ? j : kLast);
+            const uint32_t at = GL ? (j * 4 + lds.dmap[jr]) * 4 : j * 16;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, src[jr]),
-                                                   rdst, j * 4 < total ? j * 16 : kOORa, 0, nt_aux<4>());
+                                                   rdst, j * 4 < total ? at : kOORa, 0, nt_aux<4>());
         }
     };
     uint32_t par = 0;
-    for (uint32_t t = gt0 + blockIdx.x / kPGroups; t < gt1; t += tstep, par ^= 1) tile(t, par);
+    for (uint32_t t = tfirst; t < gt1; t = tnext(t), par ^= 1) tile(t, par);
 }
 
 // ---------------------------------------------------------------------------
@@ -661,8 +698,11 @@ hipError_t set_pb_stamp_buffer(void *p) {
 #ifndef SKE_PB_SPLIT
 #define SKE_PB_SPLIT 2
 #endif
-template <int SP, int R = 2 * SP, bool FL = false>  // R: 16-byte pieces per lane and run (runs of SP slices)
+// GL (FL only): the group layout -- a run's start is its place in the (tile
+// group, unit) region, or (bit 31 of its run word) in the tile's overflow row
+template <int SP, int R = 2 * SP, bool FL = false, bool GL = false>  // R: 16-byte pieces per lane and run (runs of SP slices)
 __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const PartArgs A) {
+    static_assert(!GL || FL, "the group layout is pass A3's");
     PB_STAMP(0);
     const uint32_t tmask = (1u << kPTileLog) - 1;
     __shared__ __attribute__((aligned(16))) uint8_t img[kPSliceBytes * SP];
@@ -694,7 +734,7 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t k = lane / kPbLanes, qq = lane % kPbLanes;
     constexpr uint32_t kWaves = kPbBlock / 64, kStep = kWaves * kPbGroup;
-    const __amdgpu_buffer_rsrc_t rrec = part_rsrc(A.rec, A.ntiles * A.stride * 4);
+    const __amdgpu_buffer_rsrc_t rrec = part_rsrc(A.rec, ((GL ? A.govf : 0) + A.ntiles * A.stride) * 4);
     const __amdgpu_buffer_rsrc_t roff = part_rsrc(A.off, (A.nslices + 1) * A.off_stride * 4);
     const __amdgpu_buffer_rsrc_t rfl = part_rsrc(A.flist, FL ? A.nunits * A.fl_stride * kPbLanes * 2 : 0);
     uint32_t *q = fq[wave];
@@ -745,7 +785,11 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
         auto load_be8 = [&](uint32_t tg0, uint32_t &B, uint32_t &E) {
             const uint32_t t = tg0 + (lane / kPbGroup) * kStep + lane % kPbGroup;
             const bool in = t < tb;
-            if constexpr (FL) {
+            if constexpr (GL) {  // B keeps the overflow bit 31
+                const uint32_t W = __builtin_amdgcn_raw_buffer_load_b32(roff, in ? (orow + t) * 4 : kOOR, 0, nt_aux<1>());
+                B = W & 0x8000ffffu;
+                E = (W & 0xffffu) + ((W >> 16) & 0x7fffu);
+            } else if constexpr (FL) {
                 const uint32_t W = __builtin_amdgcn_raw_buffer_load_b32(roff, in ? (orow + t) * 4 : kOOR, 0, nt_aux<1>());
                 B = W & 0xffffu;
                 E = B + (W >> 16);
@@ -758,9 +802,15 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
         // its start: every piece is one whole line (one request, not two)
         // (one byte offset per lane; piece c adds 128 c, an immediate of the
         // load; a piece past the run's end goes out of range)
+        // the word where tile t's run of this unit is placed from (GL: its
+        // group region, or with bit 31 of b its overflow row)
+        auto row = [&](uint32_t t, uint32_t b) {
+            if constexpr (GL) return (b >> 31) ? A.govf + t * A.stride : ((t >> 3) * A.nunits + unit) * A.gcap;
+            else return t * A.stride;
+        };
         auto load_recs = [&](uint32_t tg, uint32_t b, uint32_t e, uint4 (&r)[R]) {
-            const uint32_t i0 = (b & ~31u) + qq * 4;
-            const uint32_t v0 = ((tg + k) * A.stride + i0) * 4;
+            const uint32_t i0 = (b & (GL ? 0xffe0u : ~31u)) + qq * 4;
+            const uint32_t v0 = (row(tg + k, b) + i0) * 4;
             const int32_t left = int32_t(e) - int32_t(i0);
 #pragma unroll
             for (uint32_t c = 0; c < R; c++)
@@ -787,7 +837,8 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
             load_recs(tg + kStep, b1, e1, rn);
             // the (up to) 4R records of this lane: piece c starts at record
             // lo_c = s0 + c*32 + qq*4; bit j of vm: record j in [bc, ec)
-            const uint32_t s0 = bc & ~31u;
+            const uint32_t bw = GL ? bc & 0xffffu : bc;  // (GL: without the overflow bit)
+            const uint32_t s0 = bw & ~31u;
             uint32_t rec[4 * R];
 #pragma unroll
             for (uint32_t c = 0; c < R; c++) {
@@ -806,7 +857,7 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
             uint32_t vm = 0;
 #pragma unroll
             for (uint32_t c = 0; c < R; c++) vm |= part_bfm(clamp4(dh - int32_t(32 * c)), 4 * c);
-            vm &= ~part_bfm(clamp4(int32_t(bc) - int32_t(lo0)), 0);
+            vm &= ~part_bfm(clamp4(int32_t(bw) - int32_t(lo0)), 0);
             // bit set in the image: its 32-bit word, bit (offset & 31); with
             // slice pairs the record's parity bit selects the image half
             const uint32_t *img32 = reinterpret_cast<const uint32_t *>(img);
@@ -896,7 +947,7 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                 __builtin_amdgcn_wave_barrier();
             }
             if (ec - s0 > 32 * R) {  // rare: a long run
-                const uint32_t base = (tg + k) * A.stride;
+                const uint32_t base = row(tg + k, bc);
                 for (uint32_t i = s0 + 32 * R + qq; i < ec; i += kPbLanes) {
                     const uint32_t rr = __builtin_amdgcn_raw_buffer_load_b32(rrec, (base + i) * 4, 0, 0);
                     const uint32_t o = FL ? (rr & 0xfffffu)
@@ -1799,16 +1850,41 @@ bool part_supported(const ChainDev &ch) {
     return part_plan(ch, &A);
 }
 
+// The group layout's geometry (k_part_a3<11, 1024, true>): a (group of 8
+// tiles, unit) region holds the unit's expected records of the group plus
+// six standard deviations, the runs' padding and a line; the overflow rows
+// after the regions take k_part_a3's padded LDS layout (stride 13 312).
+// False when the layout does not apply or its offsets would pass 2^31 bytes.
+// Only on request (rec_groups 1): at C3 it moves pass B 0.195 -> 0.183 ms
+// and pass A 0.226 -> 0.388 ms per 16 M sub-batch -- a run's edge lines are
+// written by two tiles, partial-line writes.
+static bool part_glayout(PartArgs *A, const SegOpts &so, uint32_t ntiles_max) {
+    A->gcap = A->govf = 0;
+    if (so.rec_groups != 1 || !part_flist(*A) || A->nunits >= 512) return false;
+    const double d = double(A->link[0].d);
+    const double share = std::min(d, double(2 * kPSliceBits)) / d;  // of the largest unit
+    const double mu = 8.0 * 1024 * A->ksum * share;
+    const uint64_t cap = (uint64_t(mu + 6 * std::sqrt(mu) + 8 * 3 + 32) + 31) & ~uint64_t(31);
+    const uint64_t stride = ((1024u * 11 + 4 * (1024 / 2)) + 31) & ~31u;
+    const uint64_t govf = uint64_t((ntiles_max + 7) / 8) * A->nunits * cap;
+    if (cap >= 65536 || (govf + uint64_t(ntiles_max) * stride) * 4 >= (uint64_t(1) << 31)) return false;
+    A->gcap = uint32_t(cap);
+    A->govf = uint32_t(govf);
+    A->stride = uint32_t(stride);
+    return true;
+}
+
 // the scratch of a sub-batch of up to `sub` swipes (context scratch slots
 // 28-31 and 44: probe records, run boundaries, fail bytes, HLL words, and the
 // fail lists of one-link chains)
-static hipError_t part_scratch(PartArgs *A, uint64_t n, uint32_t sub, Scratch *scr) {
+static hipError_t part_scratch(PartArgs *A, uint64_t n, uint32_t sub, const SegOpts &so, Scratch *scr) {
     const uint32_t m = n < sub ? uint32_t(n) : sub;
     const uint32_t ntiles_max = (m + kPaBlock - 1) / kPaBlock;
     const uint32_t fstride = (m + 255) & ~255u;
     A->off_stride = (ntiles_max + 15) & ~15u;
     hipError_t e = hipSuccess;
-    A->rec = (uint32_t *)scratch_get(scr, 28, size_t(ntiles_max) * A->stride * 4, &e);
+    part_glayout(A, so, ntiles_max);
+    A->rec = (uint32_t *)scratch_get(scr, 28, (size_t(A->govf) + size_t(ntiles_max) * A->stride) * 4, &e);
     if (e == hipSuccess) A->off = (uint32_t *)scratch_get(scr, 29, size_t(A->off_stride) * (A->nslices + 1) * 4, &e);
     if (e == hipSuccess) A->fail = (uint8_t *)scratch_get(scr, 30, size_t(fstride) * A->nlinks, &e);
     if (e == hipSuccess) A->hllw = (uint32_t *)scratch_get(scr, 31, size_t(m) * 4, &e);
@@ -1915,7 +1991,7 @@ hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, uint32
     PartArgs A{};
     if (!part_plan(ch, &A)) return hipErrorInvalidValue;
     const uint32_t sub = part_sub(sub_opt);
-    hipError_t e = part_scratch(&A, n ? n : 1, sub, scr);
+    hipError_t e = part_scratch(&A, n ? n : 1, sub, so, scr);
     SegPlan P;
     if (e == hipSuccess && seg_use(A, so, nslots, n ? n : 1, sub, &P)) {
         SegArgs S{};
@@ -1938,7 +2014,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
     uint64_t nmax = 0;
     for (uint32_t j = 0; j < nb; j++) nmax = bt[j].n > nmax ? bt[j].n : nmax;
     if (nmax == 0) return hipSuccess;
-    hipError_t e = part_scratch(&A, nmax, sub, scr);
+    hipError_t e = part_scratch(&A, nmax, sub, so, scr);
     if (e != hipSuccess) return e;
     A.regs = regs;
     A.nslots = nslots;
@@ -1989,7 +2065,9 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             A.slot = B.slot + s0;
             A.out = B.out ? B.out + s0 : nullptr;
             if (hook) hook(hook_user, 0, 0, st);
-            if (flist && A.nunits < 512)  // C3/C5: 152 pairs, two counters per thread
+            if (A.gcap)  // the group layout (C3/C5 by default)
+                hipLaunchKernelGGL((k_part_a3<11, 1024, true>), dim3(g2), dim3(512), 0, st, A);
+            else if (flist && A.nunits < 512)  // C3/C5: 152 pairs, two counters per thread
                 hipLaunchKernelGGL((k_part_a3<11, 1024>), dim3(g2), dim3(512), 0, st, A);
             else if (flist)
                 hipLaunchKernelGGL((k_part_a3<11, 2048>), dim3(g2), dim3(512), 0, st, A);
@@ -1999,7 +2077,9 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
                 hipLaunchKernelGGL(k_part_a<22>, dim3(ga), dim3(kPaBlock), 0, st, A);
             if (hook) hook(hook_user, 0, 1, st);
             if (hook) hook(hook_user, 1, 0, st);
-            if (flist)
+            if (A.gcap)
+                hipLaunchKernelGGL((k_part_b<2, 4, true, true>), dim3(gb), dim3(kPbBlock), 0, st, A);
+            else if (flist)
                 hipLaunchKernelGGL((k_part_b<2, 4, true>), dim3(gb), dim3(kPbBlock), 0, st, A);
             else if (pairs)
                 hipLaunchKernelGGL(k_part_b<2>, dim3(gb), dim3(kPbBlock), 0, st, A);
