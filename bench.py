@@ -101,7 +101,9 @@ def parse(argv=None):
     ap.add_argument("--exchange", type=int, default=0,
                     help="1 = unpartitioned input: every rank's batches span ALL keys and a step "
                          "routes them to the key owners with all_to_all_single "
-                         "(distributed.SwipeExchange), runs K1 there and returns the answers")
+                         "(distributed.SwipeExchange), runs K1 there and returns the answers; "
+                         "step j+1's routing and forward exchange overlap step j's K1 (2 = the "
+                         "one-stream form, for A/B)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="library option (ske_set_option), e.g. k1_grid=128; repeatable")
     ap.add_argument("--persistent", type=int, default=-1,
@@ -715,9 +717,12 @@ class Run:
                     __cuda_array_interface__ = {"shape": shape, "typestr": typestr, "data": (ptr, False),
                                                 "version": 3, "strides": None}
                 return torch.as_tensor(_V(), device=dev)
-            self.ex = SwipeExchange(rank, world, engine_k1(engine), self.km, engine=engine, sink_slots=self.sinks)
-            self.xviews = [(tview(b.bytes.ptr, (n, self.width), "|u1"), tview(b.slot.ptr, (n,), "<i4"))
-                           for b in self.batches]
+            self.ex = SwipeExchange(rank, world, engine_k1(engine), self.km, engine=engine, sink_slots=self.sinks,
+                                    overlap=args.exchange != 2)
+            # (the ids' view keeps the batch buffer's padding in its storage:
+            # K1 may read past the last id)
+            self.xviews = [(tview(b.bytes.ptr, (n * self.width + 64,), "|u1")[:n * self.width].view(n, self.width),
+                            tview(b.slot.ptr, (n,), "<i4")) for b in self.batches]
 
     # ---- steps
     def step(self, j):
@@ -768,6 +773,10 @@ class Run:
                 s_.wait_stream(self.stream)
             for j in range(a.steps):
                 self.step(a.warmup + j)
+            if self.ex is not None:
+                # the pipelined exchange's last return half, and the timed
+                # stream waits for its streams (inside the timed region)
+                self.ex.flush()
             e.set_stream(self.stream.cuda_stream)
             for s_ in self.streams[1:]:
                 self.stream.wait_stream(s_)
@@ -1107,7 +1116,7 @@ def main():
     if run.ex is not None:
         # cap_rows_per_peer / slack_used: what the timed steps were enqueued
         # with; slack_next: what settle() adapted it to for later batches
-        line["exchange"] = {**run.ex.stats, "slack_next": run.ex.slack}
+        line["exchange"] = {**run.ex.stats, "slack_next": run.ex.slack, "pipelined": run.ex.overlap}
     if (args.rollup if args.rollup >= 0 else args.config == "c5") and not args.shard and run.w_all.zipf_lectures:
         line["rollup"] = checked(rollup_bench, run, dist)
     if world == 1 and args.host_fed and not run.lds_k1:

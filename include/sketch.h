@@ -255,6 +255,15 @@ int ske_route_swipes_cap_async(ske_ctx *ctx, const uint8_t *ids, uint32_t width,
                                uint32_t world, const uint32_t *key_route, uint32_t nkeys, uint32_t cap,
                                const uint32_t *sink_slots, uint8_t *send_ids, uint32_t *send_slots, uint32_t *pos,
                                uint32_t *counts);
+/* The routing of a one-rank world, where the exchange is the identity (K1
+ * reads the batch in place, answers come in input order): out_slots[i] = the
+ * local slot of global key gkey[i] from key_route (as above), or 0xffffffff
+ * for a key past the table or owned by no rank < world (K1 reports it as
+ * SKE_ERANGE).  key_route NULL (world 1 only): the identity table of a
+ * one-rank key map, slot = gkey for gkey < nkeys (< 2^26).  Device arrays,
+ * enqueue only. */
+int ske_route_slots_async(ske_ctx *ctx, const uint32_t *gkey, uint64_t n, const uint32_t *key_route, uint32_t nkeys,
+                          uint32_t world, uint32_t *out_slots);
 /* out[i] = answers[pos[i]]: the owners' BF.EXISTS answers, received back in
  * send order, into input order (enqueue only). */
 int ske_route_return_async(ske_ctx *ctx, const uint8_t *answers, const uint32_t *pos, uint64_t n,

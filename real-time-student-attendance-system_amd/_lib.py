@@ -126,6 +126,7 @@ SIGNATURES = {
     "ske_route_swipes_cap_async": (C.c_int, [_CTX, _u8p, C.c_uint32, _u32p, C.c_uint64, C.c_uint32, _u32p,
                                              C.c_uint32, C.c_uint32, _u32p, _u8p, _u32p, _u32p, _u32p]),
     "ske_route_return_async": (C.c_int, [_CTX, _u8p, _u32p, C.c_uint64, _u8p]),
+    "ske_route_slots_async": (C.c_int, [_CTX, _u32p, C.c_uint64, _u32p, C.c_uint32, C.c_uint32, _u32p]),
     "ske_swipes_stats": (C.c_int, [_CTX, C.c_uint32, _u8p, _u32p, C.c_uint64,
                                    C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "ske_swipes_variant": (C.c_int, [_CTX, C.c_uint32]),

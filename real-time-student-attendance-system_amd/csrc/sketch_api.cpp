@@ -59,6 +59,15 @@ struct Staged {
 
 }  // namespace
 
+// The last use of a group of context scratch slots: a use on another stream
+// first waits for it (scratch_user_begin below).
+struct ScratchUse {
+    hipEvent_t done = nullptr;
+    hipStream_t stream = nullptr;
+    unsigned long long cap = 0;  // capture id of stream's last scratch use (0: none)
+    bool pending = false;        // that use is not yet covered by done (recorded lazily)
+};
+
 struct ske_ctx {
     int device = 0;
     int cus = 256;
@@ -87,10 +96,8 @@ struct ske_ctx {
     uint8_t *zero16 = nullptr;  // 16 zero bytes on the device
     // the XCD-partitioned K1 keeps per-launch state in the context scratch:
     // a launch on another stream first waits for the previous one
-    hipEvent_t xr_done = nullptr;
-    hipStream_t xr_stream = nullptr;
-    unsigned long long xr_cap = 0;  // capture id of xr_stream's last scratch use (0: none)
-    bool xr_pending = false;        // that use is not yet covered by xr_done (recorded lazily)
+    ScratchUse xr;  // K1 (and every scratch user but routing)
+    ScratchUse rt;  // routing (slot 40 / 41 only): ordered among routing calls, not behind K1
     // executable graphs alive (recorded, not yet freed): they hold pointers to
     // the scratch and the register slab, so neither may be reallocated
     void *hook_arg = nullptr;  // launch_swipes_part's pass hook state
@@ -350,10 +357,10 @@ int k1_variant(const ske_ctx *c, const ChainDev &ch) {
 // reverse (the caller synchronises before recording a graph, as
 // engine.capture does; ske_graph_launch records the event after a replay).
 //
-// xr_done is recorded lazily: only when a use on another stream needs it (or
+// A ScratchUse's done event is recorded lazily: only when a use on another stream needs it (or
 // ske_set_stream leaves the stream), not after every call -- a marker packet
 // per call costs ~6 us of GPU time between back-to-back steps.  Recording it
-// later on xr_stream still covers the last use (it covers everything enqueued
+// later on its stream still covers the last use (it covers everything enqueued
 // there so far).  A stream whose capture state changed since that use needs
 // no wait: recording a graph starts from a synchronised stream.
 static unsigned long long capture_id(hipStream_t st, hipError_t *e) {
@@ -363,48 +370,51 @@ static unsigned long long capture_id(hipStream_t st, hipError_t *e) {
     return cs == hipStreamCaptureStatusActive ? cid : 0;
 }
 
-// cover xr_stream's last scratch use by xr_done (false: no wait is needed)
-static int xr_flush(ske_ctx *c, bool *covered) {
+// cover u.stream's last scratch use by u.done (false: no wait is needed)
+static int xr_flush(ske_ctx *c, ScratchUse &u, bool *covered) {
     *covered = false;
-    if (!c->xr_stream) return SKE_OK;
-    if (!c->xr_pending) {
+    if (!u.stream) return SKE_OK;
+    if (!u.pending) {
         *covered = true;
         return SKE_OK;
     }
     hipError_t e = hipSuccess;
-    const unsigned long long now = capture_id(c->xr_stream, &e);
+    const unsigned long long now = capture_id(u.stream, &e);
     HIPCHK(c, e);
-    c->xr_pending = false;
-    if (now != c->xr_cap) {
-        c->xr_stream = nullptr;
+    u.pending = false;
+    if (now != u.cap) {
+        u.stream = nullptr;
         return SKE_OK;
     }
-    HIPCHK(c, hipEventRecord(c->xr_done, c->xr_stream));
+    HIPCHK(c, hipEventRecord(u.done, u.stream));
     *covered = true;
     return SKE_OK;
 }
 
-int scratch_user_begin(ske_ctx *c, unsigned long long *cid_out) {
-    if (!c->xr_done) HIPCHK(c, hipEventCreateWithFlags(&c->xr_done, hipEventDisableTiming));
+static int scratch_user_begin(ske_ctx *c, unsigned long long *cid_out, ScratchUse &u) {
+    if (!u.done) HIPCHK(c, hipEventCreateWithFlags(&u.done, hipEventDisableTiming));
     hipError_t e = hipSuccess;
     const unsigned long long cid = capture_id(c->st, &e);
     HIPCHK(c, e);
-    if (c->xr_stream && c->xr_stream != c->st && c->xr_cap == cid) {
+    if (u.stream && u.stream != c->st && u.cap == cid) {
         bool covered = false;
-        const int rc = xr_flush(c, &covered);
+        const int rc = xr_flush(c, u, &covered);
         if (rc) return rc;
-        if (covered) HIPCHK(c, hipStreamWaitEvent(c->st, c->xr_done, 0));
+        if (covered) HIPCHK(c, hipStreamWaitEvent(c->st, u.done, 0));
     }
     *cid_out = cid;
     return SKE_OK;
 }
 
-int scratch_user_end(ske_ctx *c, unsigned long long cid) {
-    c->xr_stream = c->st;
-    c->xr_cap = cid;
-    c->xr_pending = true;
+static int scratch_user_end(ske_ctx *c, unsigned long long cid, ScratchUse &u) {
+    u.stream = c->st;
+    u.cap = cid;
+    u.pending = true;
     return SKE_OK;
 }
+
+int scratch_user_begin(ske_ctx *c, unsigned long long *cid_out) { return scratch_user_begin(c, cid_out, c->xr); }
+int scratch_user_end(ske_ctx *c, unsigned long long cid) { return scratch_user_end(c, cid, c->xr); }
 
 // scratch that cannot grow (a graph is being recorded, or alive) -> SKE_EBUSY
 int scratch_error(ske_ctx *c, hipError_t e) {
@@ -688,7 +698,8 @@ int ske_close(ske_ctx *c) {
     stager_delete(c->hs);
     if (c->err) (void)hipFree(c->err);
     if (c->zero16) (void)hipFree(c->zero16);
-    if (c->xr_done) (void)hipEventDestroy(c->xr_done);
+    if (c->xr.done) (void)hipEventDestroy(c->xr.done);
+    if (c->rt.done) (void)hipEventDestroy(c->rt.done);
     for (auto &m : c->marks) {
         (void)hipEventDestroy(m.a);
         (void)hipEventDestroy(m.b);
@@ -715,11 +726,12 @@ int ske_set_stream(ske_ctx *c, void *stream) {
     hipStream_t next = stream ? (hipStream_t)stream : c->own;
     // leaving the stream of the last scratch use: cover it now, while the
     // stream is known to be alive
-    if (next != c->st && c->xr_pending && c->xr_stream == c->st) {
-        bool covered = false;
-        const int rc = xr_flush(c, &covered);
-        if (rc) return rc;
-    }
+    for (ScratchUse *u : {&c->xr, &c->rt})
+        if (next != c->st && u->pending && u->stream == c->st) {
+            bool covered = false;
+            const int rc = xr_flush(c, *u, &covered);
+            if (rc) return rc;
+        }
     c->st = next;
     return SKE_OK;
 }
@@ -1374,9 +1386,9 @@ int ske_route_swipes(ske_ctx *c, const uint8_t *ids, uint32_t width, const uint3
     uint32_t *tot = e == hipSuccess ? (uint32_t *)scratch_get(c->scratch, 41, size_t(world) * 4, &e) : nullptr;
     if (e != hipSuccess) return scratch_error(c, e);
     unsigned long long cid = 0;
-    const int rc = scratch_user_begin(c, &cid);  // an async routing call on another stream finishes first
+    const int rc = scratch_user_begin(c, &cid, c->rt);  // an async routing call on another stream finishes first
     if (rc) return rc;
-    scratch_user_end(c, cid);
+    scratch_user_end(c, cid, c->rt);
     HIPCHK(c, launch_route(ids, width, gkey, n, world, key_owner, key_local, nkeys, send_ids, send_slots, pos,
                            hist, tot, c->st));
     uint32_t h[64];
@@ -1398,19 +1410,30 @@ int ske_route_swipes_cap_async(ske_ctx *c, const uint8_t *ids, uint32_t width, c
     hipError_t e = hipSuccess;
     uint32_t *hist = (uint32_t *)scratch_get(c->scratch, 40, route_hist_words(n, world) * 4 + 4, &e);
     if (e != hipSuccess) return scratch_error(c, e);
-    // the histogram is context scratch (slot 40): a routing call on another
-    // stream waits for this one's kernels (scratch_user_begin/end)
+    // the histogram is context scratch (slot 40, no K1 uses it): a routing
+    // call on another stream waits for this one's kernels, a K1 does not --
+    // the next batch's routing runs beside this batch's K1
+    // (distributed.SwipeExchange's pipelined form)
     unsigned long long cid = 0;
-    const int rc = scratch_user_begin(c, &cid);
+    const int rc = scratch_user_begin(c, &cid, c->rt);
     if (rc) return rc;
     const hipError_t le = launch_route_cap(ids, width, gkey, n, world, key_route, nkeys, cap, sink_slots, send_ids,
                                            send_slots, pos, hist, counts, c->cus, c->st);
     if (le != hipSuccess) {
         c->last_hip = std::string("launch_route_cap: ") + hipGetErrorString(le);
-        scratch_user_end(c, cid);
+        scratch_user_end(c, cid, c->rt);
         return SKE_EHIP;
     }
-    return scratch_user_end(c, cid);
+    return scratch_user_end(c, cid, c->rt);
+}
+
+int ske_route_slots_async(ske_ctx *c, const uint32_t *gkey, uint64_t n, const uint32_t *key_route, uint32_t nkeys,
+                          uint32_t world, uint32_t *out_slots) {
+    if (!c || world == 0 || world > 64 || (n && (!gkey || !out_slots)) || (!key_route && world != 1) ||
+        (!key_route && nkeys > 0x3ffffffu))
+        return SKE_EINVAL;
+    HIPCHK(c, launch_route_slots(gkey, n, key_route, nkeys, world, out_slots, c->cus, c->st));
+    return SKE_OK;
 }
 
 int ske_route_return_async(ske_ctx *c, const uint8_t *answers, const uint32_t *pos, uint64_t n, uint8_t *out) {
@@ -1974,23 +1997,25 @@ int ske_capture_end(ske_ctx *c, void **graph_out) {
 int ske_graph_launch(ske_ctx *c, void *graph) {
     if (!c || !graph) return SKE_EINVAL;
     // a direct scratch use on another stream before the replay
-    if (c->xr_done && c->xr_stream && c->xr_stream != c->st && c->xr_cap == 0) {
-        bool covered = false;
-        const int rc = xr_flush(c, &covered);
-        if (rc) return rc;
-        if (covered) HIPCHK(c, hipStreamWaitEvent(c->st, c->xr_done, 0));
-    }
+    for (ScratchUse *u : {&c->xr, &c->rt})
+        if (u->done && u->stream && u->stream != c->st && u->cap == 0) {
+            bool covered = false;
+            const int rc = xr_flush(c, *u, &covered);
+            if (rc) return rc;
+            if (covered) HIPCHK(c, hipStreamWaitEvent(c->st, u->done, 0));
+        }
     HIPCHK(c, hipGraphLaunch(hipGraphExec_t(graph), c->st));
     // a replay may hold scratch users (the partitioned / XCD-partitioned K1):
     // a later direct launch on another stream waits for it.  Two replays of
     // graphs holding scratch users on different streams are not ordered by
     // this; replay such graphs on one stream.
-    if (c->xr_done) {
-        HIPCHK(c, hipEventRecord(c->xr_done, c->st));
-        c->xr_stream = c->st;
-        c->xr_cap = 0;
-        c->xr_pending = false;
-    }
+    for (ScratchUse *u : {&c->xr, &c->rt})
+        if (u->done) {
+            HIPCHK(c, hipEventRecord(u->done, c->st));
+            u->stream = c->st;
+            u->cap = 0;
+            u->pending = false;
+        }
     return SKE_OK;
 }
 

@@ -91,6 +91,8 @@ hipError_t launch_route_cap(const uint8_t *ids, uint32_t width, const uint32_t *
                             uint32_t *sslot, uint32_t *pos, uint32_t *hist, uint32_t *tot, int cus, hipStream_t st);
 hipError_t launch_route_return(const uint8_t *ans, const uint32_t *pos, uint64_t n, uint8_t *out, int cus,
                                hipStream_t st);
+hipError_t launch_route_slots(const uint32_t *gkey, uint64_t n, const uint32_t *kroute, uint32_t nkeys,
+                              uint32_t world, uint32_t *out, int cus, hipStream_t st);
 
 // fills A's chain fields; false when the chain does not fit this variant
 bool k1_lds_plan(const ChainDev &ch, K1Args *A);

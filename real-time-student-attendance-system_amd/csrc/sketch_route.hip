@@ -323,6 +323,53 @@ hipError_t launch_route_cap(const uint8_t *ids, uint32_t width, const uint32_t *
     return hipGetLastError();
 }
 
+// The exchange at world 1 is the identity: K1 reads the batch in place and
+// answers in input order, so only the keys are mapped -- out[i] = the local
+// slot of gkey[i] (route word & 2^26 - 1), or kNoSlot for a key past the
+// table or owned by no rank of this world (K1 then reports it as SKE_ERANGE,
+// as the routed forms do).  8 B per swipe + the table gather (a random L2
+// read per swipe: 0.52 ms per 2^27 swipes); kroute == nullptr is the
+// identity table of a one-rank key map (KeyMap: local slot = the key's index
+// in the universe), no gather: 8 B per swipe, streamed.
+__device__ __forceinline__ uint32_t route_slot1(uint32_t g, const uint32_t *kroute, uint32_t nkeys, uint32_t world) {
+    if (!kroute) return g < nkeys ? g : kNoSlot;
+    const uint32_t kr = g < nkeys ? kroute[g] : 0xffffffffu;
+    return kr != 0xffffffffu && (kr >> 26) < world ? kr & 0x3ffffffu : kNoSlot;
+}
+__global__ void __launch_bounds__(256) k_route_slots1(const uint32_t *gkey, uint64_t n, const uint32_t *kroute,
+                                                      uint32_t nkeys, uint32_t world, uint32_t *out) {
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256)
+        out[i] = route_slot1(gkey[i], kroute, nkeys, world);
+}
+__global__ void __launch_bounds__(256) k_route_slots(const uint32_t *gkey, uint64_t n, const uint32_t *kroute,
+                                                     uint32_t nkeys, uint32_t world, uint32_t *out) {
+    const uint64_t n4 = n / 4;
+    for (uint64_t q = uint64_t(blockIdx.x) * 256 + threadIdx.x; q < n4; q += uint64_t(gridDim.x) * 256) {
+        const uint4 g = reinterpret_cast<const uint4 *>(gkey)[q];
+        reinterpret_cast<uint4 *>(out)[q] =
+            make_uint4(route_slot1(g.x, kroute, nkeys, world), route_slot1(g.y, kroute, nkeys, world),
+                       route_slot1(g.z, kroute, nkeys, world), route_slot1(g.w, kroute, nkeys, world));
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+        const uint64_t i = n4 * 4 + threadIdx.x;
+        out[i] = route_slot1(gkey[i], kroute, nkeys, world);
+    }
+}
+
+hipError_t launch_route_slots(const uint32_t *gkey, uint64_t n, const uint32_t *kroute, uint32_t nkeys,
+                              uint32_t world, uint32_t *out, int cus, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    // four keys per thread when both arrays are 16-B aligned, else one
+    const bool v4 = !(reinterpret_cast<uintptr_t>(gkey) & 15) && !(reinterpret_cast<uintptr_t>(out) & 15);
+    const uint64_t g = ((v4 ? n / 4 : n) + 255) / 256;
+    const unsigned grid = unsigned(g < 1 ? 1 : g < uint64_t(cus) * 8 ? g : uint64_t(cus) * 8);
+    if (v4)
+        hipLaunchKernelGGL(k_route_slots, dim3(grid), dim3(256), 0, st, gkey, n, kroute, nkeys, world, out);
+    else
+        hipLaunchKernelGGL(k_route_slots1, dim3(grid), dim3(256), 0, st, gkey, n, kroute, nkeys, world, out);
+    return hipGetLastError();
+}
+
 // four answers per thread: one 16-B load of positions, one 4-B store (pos
 // and out 16-B / 4-B aligned, checked by the host; else one per thread)
 __global__ void __launch_bounds__(256) k_route_return(const uint8_t *ans, const uint32_t *pos, uint64_t n,

@@ -86,6 +86,8 @@ class KeyMap:
             self.local[idx] = bases[r] + np.arange(idx.size, dtype=np.uint32)
             self._mine.append(idx)
         self._dev = {}
+        # one rank, no base: local slot = universe index
+        self.identity = self.world == 1 and bases[0] == 0
 
     def __len__(self):
         return len(self.names)
@@ -395,7 +397,7 @@ class SwipeExchange:
     """
 
     def __init__(self, rank: int, world: int, k1, keymap: KeyMap, group=None, engine=None,
-                 sink_slots=None, slack: float = 0.15):
+                 sink_slots=None, slack: float = 0.15, overlap: bool = True):
         import torch
         import torch.distributed as dist
         assert keymap.world == world, "the key map was built for another world size"
@@ -418,6 +420,13 @@ class SwipeExchange:
         self.pending = []
         self._free_pinned = []
         self.stats = {"batches": 0, "redone": 0, "max_share": 0.0}
+        # swipes_async on a device with an engine: the pipelined form (routing
+        # and the forward all_to_all of batch j+1 on a stream of their own
+        # while batch j's K1 runs; see _swipes_async_pipelined)
+        self.overlap = bool(overlap)
+        self._pipe = None          # two parities of send / receive rows
+        self._pipe_j = 0
+        self._pipe_back = None     # the batch whose return half is not yet issued
 
     def capacity(self, n_max: int) -> int:
         """Rows per peer of the equal-split exchange for batches of at most
@@ -544,6 +553,10 @@ class SwipeExchange:
         cap = self.capacity(n if n_max is None else n_max)
         assert n <= (n if n_max is None else n_max)
         dev = ids.device
+        if self.solo and self.engine is not None and ids.is_cuda:
+            return self._swipes_async_solo(ids, gkeys, n, w, cap)
+        if self.overlap and self.engine is not None and ids.is_cuda:
+            return self._swipes_async_pipelined(ids, gkeys, n, w, cap)
         if self.engine is not None and ids.is_cuda:
             send_ids, send_slots, pos, counts = self._route_cap_native(ids, gkeys, cap)
         else:
@@ -589,6 +602,7 @@ class SwipeExchange:
         because some owner overflowed its capacity on some rank; adapts the
         slack to the largest owner share seen (the same on every rank)."""
         torch = self.torch
+        self.flush()
         pend, self.pending = self.pending, []
         if not pend:
             return 0
@@ -622,6 +636,167 @@ class SwipeExchange:
             self.slack = max(0.02, gshare - 1.0 + 0.03)
         return redo
 
+    # ---- one rank: the exchange is the identity
+    def _swipes_async_solo(self, ids, gkeys, n, w, cap):
+        """World 1 (no process group): every key is this rank's, so nothing
+        is sorted, sent or gathered back -- the keys are mapped to local
+        slots (ske_route_slots_async, 8 B per swipe) and K1 reads the ids in
+        place, answering in input order.  (K1 may read up to 16 bytes past
+        the last id: ids whose storage ends at the last id are copied into a
+        padded buffer first.)"""
+        torch = self.torch
+        dev = ids.device
+        ids = ids.contiguous()
+        end = ids.storage_offset() * ids.element_size() + n * w
+        if ids.untyped_storage().nbytes() - end < 16:
+            pad = torch.empty(n * w + 16, dtype=torch.uint8, device=dev)
+            pad[:n * w].view(n, w).copy_(ids)
+            ids = pad[:n * w].view(n, w)
+        g32 = gkeys.to(torch.int32).contiguous()
+        # a one-rank key map is the identity (local slot = universe index):
+        # no table, the kernel only checks the range
+        kroute = None if getattr(self.keymap, "identity", False) else self.keymap.route_table(dev)
+        slots = torch.empty(max(1, n), dtype=torch.int32, device=dev)
+        eng = self.engine
+        prev = eng.get_stream()
+        try:
+            eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+            eng.ctx.call("ske_route_slots_async", C.c_void_p(g32.data_ptr()), n,
+                         C.c_void_p(None if kroute is None else kroute.data_ptr()),
+                         len(self.keymap), self.world, C.c_void_p(slots.data_ptr()))
+        finally:
+            eng.set_stream(prev)
+        self.stats["cap_rows_per_peer"] = cap
+        self.stats["slack_used"] = self.slack
+        ans = self.k1(ids, slots[:n]).to(torch.uint8)
+        self.pending.append({"ids": ids, "gkeys": gkeys, "ans": ans, "counts": torch.tensor([n], dtype=torch.int32),
+                             "ev": None, "cap": cap, "n": n})
+        return ans
+
+    # ---- the pipelined form of swipes_async (VERDICT r04 #5)
+    #
+    # Three streams besides the caller's: R (routing, the forward
+    # all_to_all_single of ids and slots), K (K1), B (the answers'
+    # all_to_all_single back, the gather into input order).  Batch j:
+    #
+    #   caller: event "inputs ready"        R: wait it; wait rows[j % 2] free;
+    #   route j; counts -> pinned host; forward a2a j     K: wait R; K1 j
+    #   (batch j-1's return half is issued here, AFTER batch j's forward
+    #   all_to_all: collectives of one process group run in issue order, so a
+    #   return of j-1 issued first would hold j's forward behind K1 j-1)
+    #   B (issued with batch j+1 or by flush): wait K1 j; a2a back; gather;
+    #   event "rows[j % 2] free"
+    #
+    # so batch j+1's routing and forward exchange run while batch j's K1 does,
+    # and two parities of send / receive rows keep them apart.  The answers
+    # are final after settle() (as in the one-stream form); flush() issues
+    # the last return half and makes the caller's stream wait for all three
+    # streams without a host synchronisation.
+    def _pipe_rows(self, dev, rows, w, n):
+        """the two parities of rows for `rows` send rows of w bytes and a
+        batch of n swipes (pos holds one entry per swipe: n exceeds rows when
+        a capacity below the owners' shares is asked for)"""
+        torch = self.torch
+        if self._pipe is not None and self._pipe_key == (rows, w, dev) and self._pipe[0]["pos"].numel() >= n:
+            return self._pipe
+        self.flush()
+        if self._pipe is not None:
+            torch.cuda.current_stream(dev).synchronize()  # (old rows: nothing may still use them)
+        solo = self.world == 1
+
+        def parity():
+            return {"send_ids": torch.empty(rows * w + 16, dtype=torch.uint8, device=dev),
+                    "send_slots": torch.empty(rows, dtype=torch.int32, device=dev),
+                    "pos": torch.empty(max(1, rows, n), dtype=torch.int32, device=dev),
+                    "counts": torch.empty(self.world, dtype=torch.int32, device=dev),
+                    "r_flat": None if solo else torch.zeros(rows * w + 16, dtype=torch.uint8, device=dev),
+                    "r_slots": None if solo else torch.empty(rows, dtype=torch.int32, device=dev),
+                    "back": None if solo else torch.empty(rows, dtype=torch.uint8, device=dev),
+                    "free": None}
+        if not hasattr(self, "_pipe_streams") or self._pipe_streams[0].device != dev:
+            # (the return half on K1's stream, or the routing stream at high
+            # priority, measured no different at N = 1: profiles/r05_exchange_overlap.txt)
+            self._pipe_streams = tuple(torch.cuda.Stream(dev) for _ in range(3))
+        self._pipe = [parity(), parity()]
+        self._pipe_key = (rows, w, dev)
+        return self._pipe
+
+    def _swipes_async_pipelined(self, ids, gkeys, n, w, cap):
+        torch = self.torch
+        dev = ids.device
+        rows = self.world * cap
+        pipe = self._pipe_rows(dev, rows, w, n)
+        sr, sk, sb = self._pipe_streams
+        caller = torch.cuda.current_stream(dev)
+        ready = torch.cuda.Event()
+        ready.record(caller)
+        B = pipe[self._pipe_j % 2]
+        self._pipe_j += 1
+        self.stats["cap_rows_per_peer"] = cap
+        self.stats["slack_used"] = self.slack
+        sr.wait_event(ready)
+        if B["free"] is not None:
+            sr.wait_event(B["free"])
+        with torch.cuda.stream(sr):
+            send_ids, send_slots, pos, counts = self._route_cap_native(ids, gkeys, cap, bufs=B)
+            host = self._free_pinned.pop() if self._free_pinned else \
+                torch.empty(self.world, dtype=torch.int32, pin_memory=True)
+            host.copy_(counts, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(sr)
+            if self.world == 1:
+                r_ids, r_slots = send_ids, send_slots
+            else:
+                self._a2a(B["r_flat"][:rows * w], send_ids.reshape(-1), None, None)
+                self._a2a(B["r_slots"], send_slots, None, None)
+                r_ids, r_slots = B["r_flat"][:rows * w].view(rows, w), B["r_slots"]
+            fwd = torch.cuda.Event()
+            fwd.record(sr)
+        self._issue_back()  # batch j-1's return half, behind batch j's forward exchange
+        sk.wait_event(fwd)
+        with torch.cuda.stream(sk):
+            r_ans = self.k1(r_ids, r_slots)
+            done = torch.cuda.Event()
+            done.record(sk)
+        ans = torch.empty(n, dtype=torch.uint8, device=dev)
+        self._pipe_back = {"B": B, "r_ans": r_ans, "done": done, "n": n, "ans": ans, "rows": rows}
+        self.pending.append({"ids": ids, "gkeys": gkeys, "ans": ans, "counts": host, "ev": ev, "cap": cap, "n": n})
+        return ans
+
+    def _issue_back(self):
+        p, self._pipe_back = self._pipe_back, None
+        if p is None:
+            return
+        torch = self.torch
+        sr, sk, sb = self._pipe_streams
+        B = p["B"]
+        sb.wait_event(p["done"])
+        with torch.cuda.stream(sb):
+            if self.world == 1:
+                back = p["r_ans"]
+            else:
+                back = B["back"]
+                self._a2a(back, p["r_ans"], None, None)
+            self._gather(back, B["pos"], p["n"], ans=p["ans"])
+            free = torch.cuda.Event()
+            free.record(sb)
+        B["free"] = free
+        # (the allocator may hand these out again only after stream B's use)
+        p["r_ans"].record_stream(sb)
+        p["ans"].record_stream(sb)
+
+    def flush(self):
+        """Issue the pipelined form's last return half and make the caller's
+        stream wait for the exchange's streams (no host synchronisation):
+        after it, work on the caller's stream sees every answer."""
+        if self._pipe is None:
+            return
+        self._issue_back()
+        torch = self.torch
+        caller = torch.cuda.current_stream(self._pipe_key[2])
+        for s_ in self._pipe_streams:
+            caller.wait_stream(s_)
+
     def _route_cap_torch(self, ids, gkeys, cap):
         torch = self.torch
         n, w = ids.shape
@@ -643,7 +818,7 @@ class SwipeExchange:
         pos[order] = row
         return send_ids, send_slots, pos, counts
 
-    def _route_cap_native(self, ids, gkeys, cap):
+    def _route_cap_native(self, ids, gkeys, cap, bufs=None):
         torch = self.torch
         n, w = ids.shape
         dev = ids.device
@@ -651,10 +826,17 @@ class SwipeExchange:
         g32 = gkeys.to(torch.int32).contiguous()
         kroute = self.keymap.route_table(dev)
         rows = self.world * cap
-        send_ids = torch.empty(rows * w + 16, dtype=torch.uint8, device=dev)  # + K1's readable tail
-        send_slots = torch.empty(rows, dtype=torch.int32, device=dev)
-        pos = torch.empty(max(1, n), dtype=torch.int32, device=dev)
-        counts = torch.empty(self.world, dtype=torch.int32, device=dev)
+        if bufs is None:
+            send_ids = torch.empty(rows * w + 16, dtype=torch.uint8, device=dev)  # + K1's readable tail
+            send_slots = torch.empty(rows, dtype=torch.int32, device=dev)
+            pos = torch.empty(max(1, n), dtype=torch.int32, device=dev)
+            counts = torch.empty(self.world, dtype=torch.int32, device=dev)
+        else:
+            send_ids, send_slots, pos, counts = bufs["send_ids"], bufs["send_slots"], bufs["pos"], bufs["counts"]
+            # (the kernels write n positions, rows ids and slots, world counts)
+            if (send_ids.numel() < rows * w + 16 or send_slots.numel() < rows or pos.numel() < max(1, n)
+                    or counts.numel() < self.world):
+                raise ValueError("SwipeExchange: routing rows smaller than the batch")
         if not hasattr(self, "_sink_dev"):
             self._sink_dev = torch.from_numpy(self.sink.view(np.int32)).to(dev)
         eng = self.engine
@@ -670,11 +852,12 @@ class SwipeExchange:
             eng.set_stream(prev)
         return send_ids[:rows * w].view(rows, w), send_slots, pos, counts
 
-    def _gather(self, back, pos, n):
+    def _gather(self, back, pos, n, ans=None):
         """answers of the send rows back into input order"""
         torch = self.torch
         if self.engine is not None and back.is_cuda:
-            ans = torch.empty(n, dtype=torch.uint8, device=back.device)
+            if ans is None:
+                ans = torch.empty(n, dtype=torch.uint8, device=back.device)
             eng = self.engine
             prev = eng.get_stream()
             try:

@@ -67,20 +67,23 @@ def main(out_dir, mode="exact"):
     ids = torch.from_numpy(buf[:n * width].reshape(n, width).copy()).cuda()
     slots = torch.from_numpy(slot.astype(np.int64)).cuda()
     k1 = engine_k1(eng)
+    # async*: the pipelined form (routing of batch j+1 beside K1 of batch j,
+    # two parities of rows) unless "serial" (one stream)
     ex = SwipeExchange(rank, world, k1, km, engine=eng, sink_slots=sinks,
-                       slack=-0.6 if mode == "async_overflow" else world - 1.0)
+                       slack=-0.6 if mode == "async_overflow" else world - 1.0, overlap="serial" not in mode)
     force = os.environ.get("WORKER_FORCE_COLLECTIVES") == "1"  # world 1: collectives still called
     if force:
         ex.solo = False
     if mode == "exact":
         ans = ex.swipes(ids, slots)
     else:
-        h = N // 2  # n_max: no rank's half-slice is longer
-        a0 = ex.swipes_async(ids[:h], slots[:h], n_max=h)
-        a1 = ex.swipes_async(ids[h:], slots[h:], n_max=h)
+        # async_many: 5 batches (each parity of rows reused), of uneven sizes
+        nb = 5 if "many" in mode else 2
+        h = -(-N // nb)  # n_max: no rank's slice of a batch is longer
+        parts = [ex.swipes_async(ids[j * h:(j + 1) * h], slots[j * h:(j + 1) * h], n_max=h) for j in range(nb)]
         redone = ex.settle()
-        assert (redone == 2) == (mode == "async_overflow"), (mode, redone, ex.stats)
-        ans = torch.cat([a0, a1])
+        assert (redone == nb) == (mode == "async_overflow"), (mode, redone, ex.stats)
+        ans = torch.cat(parts)
     torch.cuda.synchronize()
     eng.sync()
     sk = ShardedSketch(client, rank, world)

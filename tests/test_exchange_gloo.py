@@ -242,3 +242,14 @@ def test_exchange_one_rank_no_group(orc):
         want, _, _ = orc.process_swipes(chain, want_regs, gkey.astype(np.uint32), flat, offs)
         assert np.array_equal(ans.numpy(), want.astype(np.uint8)), mode
         assert np.array_equal(regs[km.local[np.arange(len(names))]], want_regs), mode
+
+
+def test_keymap_identity_flag():
+    """KeyMap.identity (SwipeExchange's world-1 form then maps keys without a
+    table): one rank and no base only, and then local == universe index."""
+    from rtsas_amd.distributed import KeyMap
+    nm = [f"k{i}" for i in range(50)]
+    km = KeyMap(nm, 1)
+    assert km.identity and km.local.tolist() == list(range(50))
+    assert not KeyMap(nm, 1, base=3).identity
+    assert not KeyMap(nm, 2).identity

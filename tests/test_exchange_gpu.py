@@ -20,12 +20,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 @pytest.mark.parametrize("world,mode,backend", [(2, "exact", "gloo"), (3, "exact", "gloo"), (2, "async", "gloo"),
                                                 (3, "async", "gloo"), (2, "async_overflow", "gloo"),
-                                                (1, "exact", "nccl"), (1, "async", "nccl")])
+                                                (3, "async_many", "gloo"), (2, "async_serial", "gloo"),
+                                                (1, "exact", "nccl"), (1, "async", "nccl"),
+                                                (1, "async_many", "nccl")])
 def test_exchange_on_device_equals_oracle(orc, engine, tmp_path, world, mode, backend):
     """mode exact: SwipeExchange.swipes (the host reads the routing counts);
     async: swipes_async over two batches (ske_route_swipes_cap_async, equal
     splits of a capacity that cannot overflow, padding into each rank's sink
-    slot) then settle(); async_overflow: a capacity below the owners' shares,
+    slot) then settle(), in the pipelined form (batch j+1's routing and
+    forward exchange on their own stream beside batch j's K1, two parities
+    of rows); async_many: five batches (each parity reused); async_serial:
+    the one-stream form; async_overflow: a capacity below the owners' shares,
     so settle() re-runs both batches with exact splits.  backend nccl: RCCL
     (one GPU holds one RCCL rank: world 1, with the collectives forced on --
     the device all_to_all_single / all_reduce / reduce_scatter_tensor /
@@ -113,3 +118,57 @@ def test_route_cap_layout(engine, slack, world):
         rr = np.unique(ps)
         have = key(rr, ssl[rr], sid.view(np.uint64).ravel()[rr])
         assert np.isin(have, want).all()
+
+
+@pytest.mark.parametrize("padded,base", [(True, 0), (False, 0), (True, 2)])
+def test_solo_exchange_identity_vs_oracle(orc, engine, padded, base):
+    """World 1 without a process group: SwipeExchange.swipes_async is the
+    identity -- keys mapped to local slots by ske_route_slots_async (base 0:
+    the identity table, no gather; base 2: the key map's route table), K1 on
+    the ids in place (padded: their storage has bytes past the last id; else
+    they are copied into a padded buffer first), answers in input order over
+    3 ragged batches; a global key past the universe gets its BF.EXISTS
+    answer, its PFADD dropped and reported as SKE_ERANGE.  Answers and
+    registers == the oracle."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from exchange_worker import NK, names, workload
+    from rtsas_amd._lib import SketchLibError, SKE_ERANGE
+    from rtsas_amd.distributed import KeyMap, SwipeExchange, engine_k1
+    w = workload()
+    engine.reserve(0, w.bf_error, w.bf_capacity)
+    p = engine.gen_params(w)
+    engine.preload(0, p, w.n_members)
+    km = KeyMap(names(), 1, base=base)
+    assert km.identity == (base == 0)
+    engine.hll_reserve(base + NK + 1)
+    ex = SwipeExchange(0, 1, engine_k1(engine), km, engine=engine, sink_slots=[base + NK])
+    chain = orc.Chain(w.bf_capacity, w.bf_error)
+    mb = engine.members_batch(p, 0, w.n_members).to_host()
+    chain.madd_packed(mb[0], mb[1])
+    regs = np.zeros((base + NK + 1, 16384), np.uint8)
+    start, outs, want = 0, [], []
+    for j, n in enumerate([100_003, 1, 77_777]):
+        buf, offs, slot = engine.swipe_batch(p, start, n).to_host()
+        start += n
+        width = int(offs[1] - offs[0])
+        raw = np.zeros(n * width + (64 if padded else 0), np.uint8)
+        raw[:n * width] = buf[:n * width]
+        ids = torch.from_numpy(raw).cuda()[:n * width].view(n, width)
+        g = slot.astype(np.int64)
+        if j == 2:
+            g[4321] = NK + 5  # past the universe
+        outs.append(ex.swipes_async(ids, torch.from_numpy(g).cuda()))
+        sl = slot.astype(np.uint32) + np.uint32(base)
+        if j == 2:
+            sl[4321] = base + NK  # the oracle's spare row (not compared)
+        v, _, _ = orc.process_swipes(chain, regs, sl, buf, offs)
+        want.append(v)
+    assert ex.settle() == 0
+    torch.cuda.synchronize()
+    with pytest.raises(SketchLibError) as ei:
+        engine.check_errors()
+    assert ei.value.code == SKE_ERANGE
+    for o, v in zip(outs, want):
+        assert np.array_equal(o.cpu().numpy(), v.astype(np.uint8))
+    assert np.array_equal(engine.registers_all(base + NK), regs[:base + NK])
