@@ -10,7 +10,7 @@ MurmurHash64A(key name) mod world over the 100k README-form key names; all
 of them at N = 1, ~12.5k per rank at N = 8).  One step = one K1 call over
 one resident batch of 2^27 swipes per GPU (C3's 1B-swipe stream in 8 steps;
 answers written, PFADD of the valid ones): the partitioned K1 in even
-sub-batches of at most 16M swipes (sketch_part.hip: hash + probe records,
+sub-batches of at most 32M swipes (sketch_part.hip: hash + probe records,
 LDS-slice probes, answers + the segmented PFADD's records and level-2 sort),
 then one window pass of the segmented PFADD over the slab (each key window
 staged in LDS, raised, its risen lines flushed).  `--config c2` runs C2 (1M
@@ -212,6 +212,16 @@ def chain_geometry(engine, fid=0):
         engine.ctx.call("ske_bf_link_info", fid, i, C.byref(li))
         out.append((int(li.bits), int(li.hashes)))
     return out
+
+
+def part_sub_default(geom):
+    """The partitioned K1's default sub-batch (sketch_part.hip part_sub): the
+    largest, at most 2^25 swipes, whose probe records (tiles of 1024 swipes,
+    k-sum * 1024 4-B records per tile rounded to 32) fit a 2^31-byte range."""
+    ksum = sum(k for _, k in geom)
+    stride = ((ksum << 10) + 31) & ~31
+    tiles = ((1 << 31) - 1) // (stride * 4)
+    return min(1 << 25, tiles // 8 * 8 * 1024)
 
 
 def oracle_chain(engine, orc, w, p):
@@ -856,10 +866,11 @@ class Run:
         cus = self.torch.cuda.get_device_properties(self.dev).multi_processor_count
         seg = bool(pt) and len(pt) > 5 and pt[5][1] > 0
         # per launch of the per-sub-batch kernels: one sub-batch (bench batches
-        # are cut into even sub-batches of at most 16M swipes)
-        nsub = -(-n // (a.part_sub or (1 << 24)))
+        # are cut into even sub-batches of at most part_sub_default swipes)
+        geom = chain_geometry(self.engine)
+        nsub = -(-n // (a.part_sub or part_sub_default(geom)))
         alg = pass_bytes(n / nsub, self.nvalid / nsub, self.probes / nsub, self.width, self.fixed,
-                         chain_geometry(self.engine), lds_k1=self.lds_k1,
+                         geom, lds_k1=self.lds_k1,
                          slab_bytes=(self.nslots if seg else self.nslots + VERIFY_KEYS) * 16384, cus=cus,
                          seg=seg, nsub=nsub)
         passes = {}

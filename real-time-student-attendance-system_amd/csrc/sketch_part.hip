@@ -71,7 +71,7 @@ constexpr uint32_t kPcBlock = 256;            // k_part_c (fail bytes)
 constexpr uint32_t kPcFlBlock = SKE_PC_BLOCK;  // k_part_c_fl (fail lists)
 constexpr uint32_t kPSliceMask = kPSliceBits - 1;
 constexpr uint32_t kPSliceBytes = kPSliceBits / 8;  // 64 KiB
-constexpr uint32_t kPSub = 1u << 24;                // swipes per sub-batch (passes A-B-C)
+constexpr uint32_t kPSub = 1u << 25;                // swipes per sub-batch (passes A-B-C), at most
 constexpr uint32_t kPbGroup = 8;                    // tiles a pass-B wave reads at once
 constexpr uint32_t kPbLanes = 64 / kPbGroup;        // lanes per tile run
 constexpr uint32_t kPTileLog = 10;                  // swipes per tile = 1 << kPTileLog
@@ -173,17 +173,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t part_rsrc(const void *p, uint3
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, int(nbytes), 0x00020000);
 }
 
-// Streams read or written once take the non-temporal policy (`nt`): pass B's
-// probe records always; SKE_NT bits select the rest -- 1 pass B's run
-// boundaries, 2 pass A's ids and offsets, 4 pass A's record copy-out, 8 pass
-// A's HLL words and fail bytes, 16 pass C's streams (fail bytes, slots, HLL
-// words, answers), 32 pass C's register pre-check loads.  Measured at C3 (A/B,
+// Streams read or written once take the non-temporal policy (`nt`); SKE_NT
+// bits select them -- 1 pass B's run boundaries, 2 pass A's ids and offsets,
+// 4 pass A's record copy-out, 8 pass A's HLL words and fail bytes, 16 pass
+// C's streams (fail bytes, slots, HLL words, answers), 32 pass C's register
+// pre-check loads, 64 pass B's probe records.  Measured at C3 (A/B,
 // two alternations): records nt: pass B 0.276 -> 0.260 ms; + bits 1|2|4:
 // 0.25 ms; bits 8 and 16 neutral to slightly slower; bit 32 makes pass C
 // 0.39 -> 0.59 ms (the raising CAS no longer finds its line near).  Default 7.
 // (Round 4, final kernels: 15 and 23 within 0.1 % of 7, profiles/r04_ab_nt.txt.)
+// Bit 64 (pass B's records) was always on before round 5.
 #ifndef SKE_NT
-#define SKE_NT 7
+#define SKE_NT 71
 #endif
 typedef uint32_t part_u32x4 __attribute__((ext_vector_type(4)));
 template <int BIT, class T> __device__ __forceinline__ T nt_ld(const T *p) {
@@ -815,7 +816,7 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
 #pragma unroll
             for (uint32_t c = 0; c < R; c++)
                 r[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     rrec, (left > int32_t(32 * c) ? v0 : kOOR) + 128 * c, 0, 2));
+                                                     rrec, (left > int32_t(32 * c) ? v0 : kOOR) + 128 * c, 0, nt_aux<64>()));
         };
         uint32_t tg = ta + wave * kPbGroup;
         uint32_t Bc, Ec, Bn, En;  // boundaries of rounds [8q, 8q + 8) and of the 8 after
@@ -1201,7 +1202,7 @@ constexpr uint32_t kSegRunSw = kSegRunTiles << kPTileLog;  // 8192 swipes
 constexpr uint32_t kSegMaxB1 = 512;                         // level-1 buckets
 constexpr uint32_t kSegMaxWpb = 512;                        // windows per bucket
 constexpr uint32_t kSegChunk = 8192;                        // records per level-2 chunk
-constexpr uint32_t kSegMaxRuns = kPSub / kSegRunSw;         // 2048 runs per sub-batch
+constexpr uint32_t kSegMaxRuns = kPSub / kSegRunSw;         // 4096 runs per sub-batch
 constexpr uint32_t kSegRecShift = 20;                       // record: slot-in-bucket above bit 20
 
 struct SegArgs {
@@ -1356,18 +1357,25 @@ __global__ void __launch_bounds__(1024) k_seg_scan(const SegArgs S) {
     const uint32_t *oa = S.o1 + size_t(h) * kSegMaxRuns, *ob = oa + kSegMaxRuns;
     uint32_t *pp = S.p1 + size_t(h) * (kSegMaxRuns + 1);
     uint32_t *cs = S.cst + size_t(h) * (kSegMaxRuns + 1);
-    const uint32_t r0 = 2 * tid, r1 = 2 * tid + 1;  // nruns <= 2048
-    const uint32_t c0 = r0 < S.nruns ? ob[r0] - oa[r0] : 0u;
-    const uint32_t c1 = r1 < S.nruns ? ob[r1] - oa[r1] : 0u;
+    constexpr uint32_t kPer = kSegMaxRuns / 1024;  // runs per thread (nruns <= kSegMaxRuns)
+    uint32_t c[kPer], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t r = kPer * tid + j;
+        c[j] = r < S.nruns ? ob[r] - oa[r] : 0u;
+        sum += c[j];
+    }
     uint32_t total;
-    const uint32_t a0 = seg_scan(c0 + c1, ws, total);
-    const uint32_t a1 = a0 + c0;
-    if (r0 < S.nruns) pp[r0] = a0;
-    if (r1 < S.nruns) pp[r1] = a1;
+    uint32_t a = seg_scan(sum, ws, total);
     if (tid == 0) pp[S.nruns] = total;
-    // a run holds <= 8192 records: at most one chunk starts inside it
-    for (uint32_t q = (a0 + kSegChunk - 1) / kSegChunk; q * kSegChunk < a0 + c0; q++) cs[q] = r0;
-    for (uint32_t q = (a1 + kSegChunk - 1) / kSegChunk; q * kSegChunk < a1 + c1; q++) cs[q] = r1;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t r = kPer * tid + j;
+        if (r < S.nruns) pp[r] = a;
+        // a run holds <= 8192 records: at most one chunk starts inside it
+        for (uint32_t q = (a + kSegChunk - 1) / kSegChunk; q * kSegChunk < a + c[j]; q++) cs[q] = r;
+        a += c[j];
+    }
 }
 
 __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
@@ -1896,10 +1904,15 @@ static hipError_t part_scratch(PartArgs *A, uint64_t n, uint32_t sub, const SegO
     return e;
 }
 
-static uint32_t part_sub(uint32_t sub_opt) {
-    uint32_t sub = sub_opt ? sub_opt : kPSub;
+// swipes per sub-batch: the option, or the largest (kPSub) whose probe
+// records stay within a 2^31-byte buffer range (k_part_b's rsrc; KM 22
+// chains: 23 831 tiles)
+static uint32_t part_sub(uint32_t sub_opt, const PartArgs &A) {
+    const uint64_t tiles = ((uint64_t(1) << 31) - 1) / (uint64_t(A.stride) * 4);
+    const uint32_t cap = uint32_t(std::min<uint64_t>(kPSub, tiles / 8 * 8 * kPaBlock));
+    uint32_t sub = sub_opt ? sub_opt : cap;
     sub = (sub + kPaBlock - 1) / kPaBlock * kPaBlock;
-    return sub < kPaBlock ? kPaBlock : (sub > kPSub ? kPSub : sub);
+    return sub < kPaBlock ? kPaBlock : (sub > cap ? cap : sub);
 }
 
 // the scratch before the first launch (so a graph recorded later holds it)
@@ -1990,7 +2003,7 @@ hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub_opt, uint32
                         Scratch *scr) {
     PartArgs A{};
     if (!part_plan(ch, &A)) return hipErrorInvalidValue;
-    const uint32_t sub = part_sub(sub_opt);
+    const uint32_t sub = part_sub(sub_opt, A);
     hipError_t e = part_scratch(&A, n ? n : 1, sub, so, scr);
     SegPlan P;
     if (e == hipSuccess && seg_use(A, so, nslots, n ? n : 1, sub, &P)) {
@@ -2010,7 +2023,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
                               const SegOpts &so, hipStream_t st, PassHook hook, void *hook_user) {
     PartArgs A{};
     if (!part_plan(ch, &A)) return hipErrorInvalidValue;
-    const uint32_t sub = part_sub(sub_opt);
+    const uint32_t sub = part_sub(sub_opt, A);
     uint64_t nmax = 0;
     for (uint32_t j = 0; j < nb; j++) nmax = bt[j].n > nmax ? bt[j].n : nmax;
     if (nmax == 0) return hipSuccess;

@@ -289,13 +289,16 @@ def test_c3_bench_step_128m_segmented(engine, orc, world):
     12.5k keys, 205 MB).  The auto choice takes the segmented PFADD at this
     density (asserted through the pass timing kinds); every answer and every
     register bit-exact vs the oracle (its multi-threaded per-event loop,
-    identical results to the sequential one)."""
+    identical results to the sequential one).  N = 1 in the default
+    sub-batches (4 of 2^25 swipes), N = 8 in sub-batches of 2^24 (8)."""
     import os
     from rtsas_amd import synthetic
     from rtsas_amd.engine import DeviceBuffer
     w = synthetic.shard(synthetic.WORKLOADS["c3"], world)
     p = _setup(engine, w)
     n = 1 << 27
+    sub = 0 if world == 1 else 1 << 24
+    engine.set_option("part_sub", sub)
     b = engine.swipe_batch(p, 0, n)
     out = DeviceBuffer(engine.ctx, n)
     engine.set_option("pass_timing", 1)
@@ -303,7 +306,8 @@ def test_c3_bench_step_128m_segmented(engine, orc, world):
     engine.swipes(0, b, out)
     pt = engine.pass_times(reset=True)
     engine.set_option("pass_timing", 0)
-    assert pt[5][1] == 1 and pt[4][1] == 8, pt  # one window pass, 8 sub-batches
+    nsub = 4 if sub == 0 else 8
+    assert pt[5][1] == 1 and pt[4][1] == nsub, pt  # one window pass, nsub sub-batches
     chain = orc.Chain(w.bf_capacity, w.bf_error)
     mb = engine.members_batch(p, 0, w.n_members)
     mbuf, moffs, _ = mb.to_host()
