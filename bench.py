@@ -896,6 +896,12 @@ class Run:
         # FETCH corrected for 16-B-per-lane streams where the summary says so)
         pmc, pmc_src = load_pmc(self.pmc_tag(seg), dom)
         traffic = None
+        if pmc is not None and passes and dom != "k1":
+            # a summary taken over launches of another size says nothing of these
+            # (summaries before round 5's 2^25 sub-batches covered 2^24 swipes)
+            per = n if dom == "k_seg_e" else n / nsub
+            if abs(pmc.get("swipes_per_launch", 1 << 24) - per) > 0.01 * per:
+                pmc, pmc_src = None, None
         if pmc is not None:
             # request-size-calibrated bytes where the summary has them (round 4:
             # every read request by its size, tools/fetchcal.hip), else FETCH+WRITE

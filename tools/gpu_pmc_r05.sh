@@ -15,4 +15,4 @@ for c in "${GROUPS_[@]}"; do
   echo "pmc [$c] rc=$rc"
   if [ $rc -ne 0 ]; then tail -3 gpurun_out/pmc_r05/$tag.log; exit $rc; fi
 done
-python tools/r05_pmc_seg.py gpurun_out/pmc_r05 gpurun_out/pmc_r05_
+python tools/r05_pmc_seg.py gpurun_out/pmc_r05 gpurun_out/pmc_r05_ || exit 1

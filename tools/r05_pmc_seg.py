@@ -2,8 +2,11 @@
 segmented PFADD) from tools/gpu_pmc_r05.sh's passes, named by bench.py's pass
 kinds: k_part_a, k_part_b, k_part_c (the segmented C1, k_seg_c1), k_seg_d
 (k_seg_scan + k_seg_d, per sub-batch), k_seg_e (window pass E1 + E2 + merge
-M, per step).  Warm-up dispatches are skipped (2 steps of 8 sub-batches).
-usage: python tools/r05_pmc_seg.py <pmc_root> <out_prefix>
+M, per step).  Warm-up dispatches are skipped (2 steps of NSUB sub-batches;
+env NSUB, default 4: 2^27 swipes in sub-batches of 2^25).  Every summary
+records the swipes one launch covers (env STEP_SWIPES / NSUB; the window pass:
+a step), so bench.py applies it only to launches of that size.
+usage: NSUB=4 STEP_SWIPES=134217728 python tools/r05_pmc_seg.py <pmc_root> <out_prefix>
 """
 import json
 import os
@@ -13,7 +16,9 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_summary import summarise  # noqa: E402
 
 root, prefix = sys.argv[1], sys.argv[2]
-SKIP_SUB, SKIP_STEP = 16, 2
+NSUB = int(os.environ.get("NSUB", "4"))
+STEP = int(os.environ.get("STEP_SWIPES", str(1 << 27)))
+SKIP_SUB, SKIP_STEP = 2 * NSUB, 2
 plan = {"k_part_a": (["k_part_a3"], SKIP_SUB), "k_part_b": (["k_part_b"], SKIP_SUB),
         "k_part_c": (["k_seg_c1"], SKIP_SUB), "k_seg_d": (["k_seg_scan", "k_seg_d("], SKIP_SUB),
         "k_seg_e": (["k_seg_e<1, false>", "k_seg_e<1, true>", "k_seg_m<1>"], SKIP_STEP)}
@@ -24,7 +29,8 @@ for name, (kernels, skip) in plan.items():
         for c, v in p["mean"].items():
             mean[c] = mean.get(c, 0.0) + v
     out = {"kernels": {k: p["kernel"] for k, p in parts.items()}, "per_kernel": parts, "mean": mean,
-           "what": "per launch of the pass (sum of its kernels' per-dispatch means)"}
+           "what": "per launch of the pass (sum of its kernels' per-dispatch means)",
+           "swipes_per_launch": STEP if skip == SKIP_STEP else STEP // NSUB}
     if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
         out["hbm_bytes_per_dispatch"] = (mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024
     if "TCC_EA0_RDREQ_128B_sum" in mean and "WRITE_SIZE" in mean:
