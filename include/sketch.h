@@ -312,7 +312,8 @@ int ske_swipes_variant(ske_ctx *ctx, uint32_t fid);
  * which a batch is segmented, x100, default 600, doubled for a slab of at
  * most 192 MB), "seg_dense_min" (records per window line at which a window
  * is staged in LDS, x100), "seg_klog" (0..3: keys per window 1, 2, 4, 8;
- * default 1); "rec_groups" (1: pass A writes a slice unit's probe
+ * default 1), "seg_b1" (-1 auto, 0..9: 2^b1 level-1 buckets); "rec_groups"
+ * (1: pass A writes a slice unit's probe
  * records of 8 consecutive tiles adjacently, for one-link k = 11 chains;
  * -1 auto and 0: per-tile runs, the faster form).  Any other name or an out-of-range value: SKE_EINVAL.  None
  * changes an answer or a register. */

@@ -842,6 +842,11 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
         c->seg.klog = int(value);
         return SKE_OK;
     }
+    if (!strcmp(name, "seg_b1")) {  // segmented PFADD: 2^b1 level-1 buckets, -1 auto
+        if (value < -1 || value > 9) return SKE_EINVAL;
+        c->seg.b1 = int(value);
+        return SKE_OK;
+    }
     if (!strcmp(name, "rec_groups")) {  // pass A's records in the group layout: -1 auto, 0 per-tile runs, 1 on
         if (value < -1 || value > 1) return SKE_EINVAL;
         c->seg.rec_groups = int(value);

@@ -155,6 +155,7 @@ struct SegOpts {
     // slices): 1 whenever the chain allows; -1 auto and 0: per-tile runs
     // (the group layout costs pass A more than it saves pass B)
     int rec_groups = -1;
+    int b1 = -1;  // option "seg_b1": 2^b1 level-1 buckets (-1: auto, seg_plan)
 };
 // sizes the context scratch for batches of up to n swipes (no launch)
 // sub: swipes per sub-batch of the three passes (0: the default, 16M)

@@ -1933,7 +1933,19 @@ static bool seg_plan(uint32_t nslots, uint64_t n, uint32_t sub, const SegOpts &s
     const uint32_t nwin = uint32_t((uint64_t(nslots) + (1u << klog) - 1) >> klog);
     uint32_t tb = 0;
     while ((uint64_t(1) << tb) < nwin) tb++;
-    uint32_t wlog = (tb + 1) / 2, b1 = tb - wlog;
+    // windows per bucket 2^wlog: at least half the window bits, and at least
+    // tb - 5 (2^25 sub-batches: level-2 sorts over more windows beat longer
+    // level-1 segments up to 2^9; profiles/r05_ab_seg_b1.txt: b1 7 at C3's
+    // 2^16 windows, 5 at the 8-way shard's 2^13)
+    uint32_t wlog = std::max((tb + 1) / 2, tb > 5 ? tb - 5 : 0u), b1 = tb - wlog;
+    if (wlog > 9) {
+        wlog = 9;
+        b1 = tb - 9;
+    }
+    if (so.b1 >= 0) {  // the option: level-1 buckets 2^b1 (windows per bucket 2^(tb - b1) <= 2^9)
+        b1 = uint32_t(so.b1) < tb ? uint32_t(so.b1) : tb;
+        wlog = tb - b1;
+    }
     if (b1 > 9) {
         b1 = 9;
         wlog = tb - 9;
