@@ -10,7 +10,7 @@ MurmurHash64A(key name) mod world over the 100k README-form key names; all
 of them at N = 1, ~12.5k per rank at N = 8).  One step = one K1 call over
 one resident batch of 2^27 swipes per GPU (C3's 1B-swipe stream in 8 steps;
 answers written, PFADD of the valid ones): the partitioned K1 in even
-sub-batches of at most 32M swipes (sketch_part.hip: hash + probe records,
+sub-batches of 2^25 swipes (sketch_part.hip: hash + probe records,
 LDS-slice probes, answers + the segmented PFADD's records and level-2 sort),
 then one window pass of the segmented PFADD over the slab (each key window
 staged in LDS, raised, its risen lines flushed).  `--config c2` runs C2 (1M
@@ -215,13 +215,14 @@ def chain_geometry(engine, fid=0):
 
 
 def part_sub_default(geom):
-    """The partitioned K1's default sub-batch (sketch_part.hip part_sub): the
-    largest, at most 2^25 swipes, whose probe records (tiles of 1024 swipes,
-    k-sum * 1024 4-B records per tile rounded to 32) fit a 2^31-byte range."""
+    """The partitioned K1's default sub-batch (sketch_part.hip part_sub): 2^25
+    swipes, or less where the probe records of one of the 8 XCD tile groups
+    (tiles of 1024 swipes, k-sum * 1024 4-B records per tile rounded to 32)
+    would pass a 2^31-byte range."""
     ksum = sum(k for _, k in geom)
     stride = ((ksum << 10) + 31) & ~31
     tiles = ((1 << 31) - 1) // (stride * 4)
-    return min(1 << 25, tiles // 8 * 8 * 1024)
+    return min(1 << 25, (tiles - 8) * 8 * 1024)
 
 
 def oracle_chain(engine, orc, w, p):

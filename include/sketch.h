@@ -305,8 +305,8 @@ int ske_swipes_variant(ske_ctx *ctx, uint32_t fid);
 /* Tuning options (no reference counterpart): "variant" (-1 auto, 0..3 as
  * above), "tile" (LDS K1 swipes per thread: 1, 2, 4, 8), "k1_grid" (LDS K1
  * blocks, 0 = one per CU), "k1_persistent" (0/1), "part_sub" (partitioned K1
- * swipes per sub-batch, at most 32M; 0 = the largest the chain's probe
- * records allow, 32M for k <= 11), "pass_timing" (0/1); the partitioned K1's
+ * swipes per sub-batch, at most 2^26; 0 = 2^25), "pass_timing" (0/1); the
+ * partitioned K1's
  * segmented PFADD: "hll_seg" (-1 auto, 0 never, 1 whenever the
  * chain and slab allow), "seg_density" (auto: swipes per 128-B slab line at
  * which a batch is segmented, x100, default 600, doubled for a slab of at

@@ -818,7 +818,7 @@ int ske_set_option(ske_ctx *c, const char *name, int64_t value) {
         return SKE_OK;
     }
     if (!strcmp(name, "part_sub")) {  // partitioned K1 sub-batch (swipes; 0 = default)
-        if (value < 0 || value > (int64_t(1) << 25)) return SKE_EINVAL;
+        if (value < 0 || value > (int64_t(1) << 26)) return SKE_EINVAL;
         c->part_sub = uint32_t(value);
         return SKE_OK;
     }

@@ -71,7 +71,7 @@ constexpr uint32_t kPcBlock = 256;            // k_part_c (fail bytes)
 constexpr uint32_t kPcFlBlock = SKE_PC_BLOCK;  // k_part_c_fl (fail lists)
 constexpr uint32_t kPSliceMask = kPSliceBits - 1;
 constexpr uint32_t kPSliceBytes = kPSliceBits / 8;  // 64 KiB
-constexpr uint32_t kPSub = 1u << 25;                // swipes per sub-batch (passes A-B-C), at most
+constexpr uint32_t kPSub = 1u << 26;                // swipes per sub-batch (passes A-B-C), at most
 constexpr uint32_t kPbGroup = 8;                    // tiles a pass-B wave reads at once
 constexpr uint32_t kPbLanes = 64 / kPbGroup;        // lanes per tile run
 constexpr uint32_t kPTileLog = 10;                  // swipes per tile = 1 << kPTileLog
@@ -735,7 +735,12 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t k = lane / kPbLanes, qq = lane % kPbLanes;
     constexpr uint32_t kWaves = kPbBlock / 64, kStep = kWaves * kPbGroup;
-    const __amdgpu_buffer_rsrc_t rrec = part_rsrc(A.rec, ((GL ? A.govf : 0) + A.ntiles * A.stride) * 4);
+    // the records of this block's tile group (per-tile layout; offsets from
+    // its first tile, so a 2^26-swipe sub-batch's 2.95 GB stay 32-bit), or
+    // of every group (the group layout: regions and overflow rows)
+    const size_t rbase = GL ? 0 : size_t(gt0) * A.stride;
+    const __amdgpu_buffer_rsrc_t rrec =
+        GL ? part_rsrc(A.rec, (A.govf + A.ntiles * A.stride) * 4) : part_rsrc(A.rec + rbase, (gt1 - gt0) * A.stride * 4);
     const __amdgpu_buffer_rsrc_t roff = part_rsrc(A.off, (A.nslices + 1) * A.off_stride * 4);
     const __amdgpu_buffer_rsrc_t rfl = part_rsrc(A.flist, FL ? A.nunits * A.fl_stride * kPbLanes * 2 : 0);
     uint32_t *q = fq[wave];
@@ -807,7 +812,7 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
         // group region, or with bit 31 of b its overflow row)
         auto row = [&](uint32_t t, uint32_t b) {
             if constexpr (GL) return (b >> 31) ? A.govf + t * A.stride : ((t >> 3) * A.nunits + unit) * A.gcap;
-            else return t * A.stride;
+            else return (t - gt0) * A.stride;
         };
         auto load_recs = [&](uint32_t tg, uint32_t b, uint32_t e, uint4 (&r)[R]) {
             const uint32_t i0 = (b & (GL ? 0xffe0u : ~31u)) + qq * 4;
@@ -1202,7 +1207,8 @@ constexpr uint32_t kSegRunSw = kSegRunTiles << kPTileLog;  // 8192 swipes
 constexpr uint32_t kSegMaxB1 = 512;                         // level-1 buckets
 constexpr uint32_t kSegMaxWpb = 512;                        // windows per bucket
 constexpr uint32_t kSegChunk = 8192;                        // records per level-2 chunk
-constexpr uint32_t kSegMaxRuns = kPSub / kSegRunSw;         // 4096 runs per sub-batch
+constexpr uint32_t kSegMaxRuns = kPSub / kSegRunSw;         // 8192 runs per sub-batch
+constexpr uint32_t kSegDStage = 2048;                       // D: runs of a chunk staged in LDS
 constexpr uint32_t kSegRecShift = 20;                       // record: slot-in-bucket above bit 20
 
 struct SegArgs {
@@ -1380,7 +1386,9 @@ __global__ void __launch_bounds__(1024) k_seg_scan(const SegArgs S) {
 
 __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
     __shared__ uint32_t tot[kSegMaxB1], cbl[kSegMaxB1 + 1];
-    __shared__ uint32_t spp[kSegMaxRuns + 1], sob[kSegMaxRuns];
+    // the chunk's runs' prefix and starts, staged when at most kSegDStage
+    // runs hold it (a chunk of a sparse bucket spanning more reads them in place)
+    __shared__ uint32_t spp[kSegDStage + 1], sob[kSegDStage];
     __shared__ uint32_t c2[kSegMaxWpb + 1];
     __shared__ __attribute__((aligned(16))) uint32_t sb[kSegChunk];
     __shared__ uint32_t ws[16];
@@ -1409,23 +1417,27 @@ __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
         const uint32_t ga = cs[c];
         const uint32_t gb = w1 < tot[h] ? cs[c + 1] + 1 : S.nruns;  // runs [ga, gb) hold [w0, w1)
         const uint32_t ng = gb - ga;
-        for (uint32_t j = tid; j <= ng; j += 1024) {
-            spp[j] = pp[ga + j];
-            if (j < ng) sob[j] = S.o1[size_t(h) * kSegMaxRuns + ga + j];
-        }
+        const bool staged = ng < kSegDStage;  // block-uniform
+        const uint32_t *gpp = pp + ga, *gob = S.o1 + size_t(h) * kSegMaxRuns + ga;
+        if (staged)
+            for (uint32_t j = tid; j <= ng; j += 1024) {
+                spp[j] = gpp[j];
+                if (j < ng) sob[j] = gob[j];
+            }
         if (tid <= wpb) c2[tid] = 0;
         lds_barrier();
+        const uint32_t *vpp = staged ? spp : gpp, *vob = staged ? sob : gob;
         // 8 consecutive records per thread: one search, then a walk
         uint32_t rec[8], pos[8];
         const uint32_t p0 = w0 + tid * 8;
-        uint32_t k = p0 < w1 ? seg_last_le(spp, ng, p0) : 0u;
+        uint32_t k = p0 < w1 ? seg_last_le(vpp, ng, p0) : 0u;
 #pragma unroll
         for (uint32_t j = 0; j < 8; j++) {
             const uint32_t p = p0 + j;
             rec[j] = 0;
             if (p < w1) {
-                while (spp[k + 1] <= p) k++;
-                rec[j] = S.r1[size_t(ga + k) * kSegRunSw + sob[k] + (p - spp[k])];
+                while (vpp[k + 1] <= p) k++;
+                rec[j] = S.r1[size_t(ga + k) * kSegRunSw + vob[k] + (p - vpp[k])];
             }
         }
 #pragma unroll
@@ -1904,13 +1916,17 @@ static hipError_t part_scratch(PartArgs *A, uint64_t n, uint32_t sub, const SegO
     return e;
 }
 
-// swipes per sub-batch: the option, or the largest (kPSub) whose probe
-// records stay within a 2^31-byte buffer range (k_part_b's rsrc; KM 22
-// chains: 23 831 tiles)
+// swipes per sub-batch: the option (at most the largest, kPSub, whose probe
+// records of one XCD tile group stay within a 2^31-byte buffer range --
+// k_part_b's rsrc, relative to the group's first tile; SKE_PB_SPLIT 1: of
+// all tiles -- 2^26 for every chain the plan takes), or kPSubDefault: 2^25
+// measured as fast as 2^26 at C3 and faster than 2^24 (profiles/r05_ab_subbatch.txt)
+constexpr uint32_t kPSubDefault = 1u << 25;
 static uint32_t part_sub(uint32_t sub_opt, const PartArgs &A) {
     const uint64_t tiles = ((uint64_t(1) << 31) - 1) / (uint64_t(A.stride) * 4);
-    const uint32_t cap = uint32_t(std::min<uint64_t>(kPSub, tiles / 8 * 8 * kPaBlock));
-    uint32_t sub = sub_opt ? sub_opt : cap;
+    const uint64_t span = SKE_PB_SPLIT == 1 ? tiles : (tiles - 8) * kPGroups;  // tiles a sub-batch may have
+    const uint32_t cap = uint32_t(std::min<uint64_t>(kPSub, span / 8 * 8 * kPaBlock));
+    uint32_t sub = sub_opt ? sub_opt : std::min(cap, kPSubDefault);
     sub = (sub + kPaBlock - 1) / kPaBlock * kPaBlock;
     return sub < kPaBlock ? kPaBlock : (sub > cap ? cap : sub);
 }
@@ -1957,9 +1973,14 @@ static bool seg_plan(uint32_t nslots, uint64_t n, uint32_t sub, const SegOpts &s
     P->s1 = klog + wlog;
     P->nwin = nwin;
     P->nb1 = 1u << b1;
-    P->nsub = uint32_t((n + sub - 1) / sub);
     P->maxch = (sub + kSegChunk - 1) / kSegChunk + P->nb1;
-    if (P->nsub > 64 || uint64_t(P->nsub) * P->maxch * kSegChunk >= (uint64_t(1) << 32)) return false;
+    // sub-batches per window pass: at most 64, and their level-2 records
+    // within a 2^31-byte buffer range (the window pass's record loads); a
+    // batch of more runs a window pass after every nsub of them
+    const uint64_t kmax = ((uint64_t(1) << 29) - 1) / (uint64_t(P->maxch) * kSegChunk);
+    const uint64_t ns = (n + sub - 1) / sub;
+    if (kmax == 0) return false;
+    P->nsub = uint32_t(std::min<uint64_t>(std::min<uint64_t>(ns, kmax), 64));
     const uint64_t dm = uint64_t(so.dense_min_x100) * ((uint64_t(1) << klog) * (kHllRegs / 128)) / 100;
     P->dense_min = dm < 1 ? 1u : (dm > 0xffffffffu ? 0xffffffffu : uint32_t(dm));
     return true;
@@ -1979,6 +2000,7 @@ static bool seg_use(const PartArgs &A, const SegOpts &so, uint32_t nslots, uint6
 // the segmented PFADD's scratch (context slots 32-38)
 static hipError_t seg_scratch(const SegPlan &P, uint32_t sub, uint64_t n, Scratch *scr, SegArgs *S) {
     const uint64_t m = n < sub ? n : sub;
+    const uint64_t mg = std::min<uint64_t>(n, uint64_t(P.nsub) * sub);  // swipes of one window pass
     hipError_t e = hipSuccess;
     S->r1 = (uint32_t *)scratch_get(scr, 32, size_t((m + kSegRunSw - 1) / kSegRunSw) * kSegRunSw * 4, &e);
     if (e == hipSuccess) S->o1 = (uint32_t *)scratch_get(scr, 33, size_t(P.nb1 + 1) * kSegMaxRuns * 4, &e);
@@ -1992,7 +2014,7 @@ static hipError_t seg_scratch(const SegPlan &P, uint32_t sub, uint64_t n, Scratc
     // the window pass's cut windows: a cut window has > slice records and
     // ceil(records / slice) < 2 records / slice slices, so 2 n / slice
     // copies, queue entries and cut windows always suffice
-    const uint32_t ccap = uint32_t(2 * ((n + seg_slice(P.klog) - 1) / seg_slice(P.klog)) + 2);
+    const uint32_t ccap = uint32_t(2 * ((mg + seg_slice(P.klog) - 1) / seg_slice(P.klog)) + 2);
     const size_t wb = size_t(1) << (P.klog + kHllP);
     if (e == hipSuccess) S->q = (uint32_t *)scratch_get(scr, 39, 16, &e);
     if (e == hipSuccess) S->qitems = (uint4 *)scratch_get(scr, 42, size_t(ccap) * 16, &e);
@@ -2079,6 +2101,31 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             }
             if (e != hipSuccess) return e;
         }
+        // every window of the slab once after each group of P.nsub
+        // sub-batches (the whole batch unless it is very large): E1 (first
+        // slices), E2 (queued slices of cut windows), M (cut windows merged)
+        auto window_pass = [&](uint32_t ns) -> hipError_t {
+            S.nsub = ns;
+            A.n = 0;
+            if (hook) hook(hook_user, 4, 0, st);
+            hipError_t we = hipMemsetAsync(S.q, 0, 16, st);
+            if (we != hipSuccess) return we;
+            switch (P.klog) {
+#define SEG_E_LAUNCH(K)                                                                                  \
+    case K:                                                                                              \
+        hipLaunchKernelGGL((k_seg_e<K, false>), dim3(unsigned(cus) * SegE<K>::BPC), dim3(SegE<K>::T), 0, st, A, S); \
+        hipLaunchKernelGGL((k_seg_e<K, true>), dim3(unsigned(cus) * SegE<K>::BPC), dim3(SegE<K>::T), 0, st, A, S);  \
+        hipLaunchKernelGGL(k_seg_m<K>, dim3(unsigned(cus)), dim3(1024), 0, st, A, S);                    \
+        break;
+                SEG_E_LAUNCH(0)
+                SEG_E_LAUNCH(1)
+                SEG_E_LAUNCH(2)
+                SEG_E_LAUNCH(3)
+#undef SEG_E_LAUNCH
+            }
+            if (hook) hook(hook_user, 4, 1, st);
+            return hipGetLastError();
+        };
         uint32_t si = 0;
         for (uint64_t s0 = 0; s0 < B.n; s0 += subj, si++) {
             const uint32_t ms = B.n - s0 < subj ? uint32_t(B.n - s0) : subj;
@@ -2113,7 +2160,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             if (hook) hook(hook_user, 1, 1, st);
             if (hook) hook(hook_user, 2, 0, st);
             if (seg) {
-                S.s = si;
+                S.s = si % P.nsub;
                 S.nruns = (A.ntiles + kSegRunTiles - 1) / kSegRunTiles;
                 hipLaunchKernelGGL(k_seg_c1, dim3(std::min(S.nruns, unsigned(cus) * 2)), dim3(1024), 0, st, A, S);
                 if (hook) hook(hook_user, 2, 1, st);
@@ -2133,31 +2180,10 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             if (!seg && hook) hook(hook_user, 2, 1, st);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
-        }
-        if (seg) {
-            // every window of the slab once, after the batch's sub-batches:
-            // E1 (first slices), E2 (queued slices of cut windows), M (cut
-            // windows merged)
-            A.n = 0;
-            if (hook) hook(hook_user, 4, 0, st);
-            e = hipMemsetAsync(S.q, 0, 16, st);
-            if (e != hipSuccess) return e;
-            switch (P.klog) {
-#define SEG_E_LAUNCH(K)                                                                                  \
-    case K:                                                                                              \
-        hipLaunchKernelGGL((k_seg_e<K, false>), dim3(unsigned(cus) * SegE<K>::BPC), dim3(SegE<K>::T), 0, st, A, S); \
-        hipLaunchKernelGGL((k_seg_e<K, true>), dim3(unsigned(cus) * SegE<K>::BPC), dim3(SegE<K>::T), 0, st, A, S);  \
-        hipLaunchKernelGGL(k_seg_m<K>, dim3(unsigned(cus)), dim3(1024), 0, st, A, S);                    \
-        break;
-                SEG_E_LAUNCH(0)
-                SEG_E_LAUNCH(1)
-                SEG_E_LAUNCH(2)
-                SEG_E_LAUNCH(3)
-#undef SEG_E_LAUNCH
+            if (seg && ((si + 1) % P.nsub == 0 || s0 + subj >= B.n)) {
+                e = window_pass(si % P.nsub + 1);
+                if (e != hipSuccess) return e;
             }
-            if (hook) hook(hook_user, 4, 1, st);
-            e = hipGetLastError();
-            if (e != hipSuccess) return e;
         }
     }
     return hipSuccess;

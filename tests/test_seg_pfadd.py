@@ -60,6 +60,7 @@ def _oracle(orc, engine, w, p, batches):
     (1, 100, 0),            # windows of 2 keys (512-thread blocks)
     (0, 100, 0),            # windows of 1 key (256-thread blocks)
     (0, 0, 1 << 18),        # 1-key windows, 5 sub-batches, all staged
+    (1, 100, 16384),        # 74 sub-batches: two window passes (64 + 10 sub-batches)
 ])
 def test_seg_forced_small(engine, orc, klog, dense_min, sub):
     from rtsas_amd.engine import DeviceBuffer
