@@ -585,6 +585,9 @@ def pass_bytes(n, nvalid, probes, width, fixed, geometry, lds_k1=False, slab_byt
     filter_bytes = sum(bits // 8 for bits, _ in geometry)
     rec = 4 * ksum * n
     ntiles = -(-n // 1024)
+    # fail bytes per swipe: one per link; none for the fail-list chains (one
+    # link, k = 11), whose overflow flags live in the HLL word's top byte
+    nfail = 0 if (len(geometry) == 1 and ksum == 11) else len(geometry)
     return {
         # one kernel: ids + offsets + slot + answer streamed, one sector per
         # RedisBloom probe, one sector read + one written per valid swipe
@@ -593,14 +596,14 @@ def pass_bytes(n, nvalid, probes, width, fixed, geometry, lds_k1=False, slab_byt
               n * (width + s_off + 4 + 1) + 64 * probes + 128 * nvalid,
         # the LDS K1 stages the filter into every block's LDS once per launch
         "k1_stage": filter_bytes * cus if lds_k1 else 0,
-        # ids + offsets in; probe records, run table, HLL word, fail byte out
-        "k_part_a": n * (width + s_off) + rec + 4 * (nslices + 1) * ntiles + 4 * n + n * len(geometry),
+        # ids + offsets in; probe records, run table, HLL word, fail bytes out
+        "k_part_a": n * (width + s_off) + rec + 4 * (nslices + 1) * ntiles + 4 * n + n * nfail,
         # probe records + their run boundaries in, the filter staged once
         "k_part_b": rec + 8 * nslices * ntiles + filter_bytes,
         # fail byte, HLL word, slot in, answer out; per valid swipe its register's
         # sector read + written (SURVEY §8d's 128·v, as the one-kernel K1 above),
         # or (seg) its 4-B record written
-        "k_part_c": n * (len(geometry) + 4 + 4 + 1) + (4 if seg else 128) * nvalid,
+        "k_part_c": n * (nfail + 4 + 4 + 1) + (4 if seg else 128) * nvalid,
         "k_seg_d": 8 * nvalid,
         "k_seg_e": 4 * nvalid * nsub + 2 * slab_bytes,
     }

@@ -23,12 +23,15 @@
 //                      counting-sorted by slice in LDS and written out as one
 //                      contiguous run per (tile, slice unit); off[slice][tile]
 //                      holds the run boundaries.  Also the HLL word (register
-//                      | rank << 16) and a cleared fail byte per swipe.
+//                      | rank << 16; one-link k = 11 chains: its top byte is
+//                      the swipe's overflow flag) and, for other chains, a
+//                      cleared fail byte per swipe.
 //   pass B             per slice unit (one slice, or a pair of a one-link
 //                      chain's adjacent slices), staged into LDS: the unit's
 //                      run of every tile in the block's range; a failing
 //                      probe's swipe goes to the tile's fail list (one-link
-//                      k = 11 chains) or sets its fail byte.
+//                      k = 11 chains; a full list's overflow sets the HLL
+//                      word's top byte) or sets its fail byte.
 //   pass C             per swipe: valid = no failed probe in some link; the
 //                      answer; register max (pre-check load, CAS).
 //
@@ -444,7 +447,6 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
     // the stores (the copy-out's memory round trip, once per tile).
     const __amdgpu_buffer_rsrc_t roffs = part_rsrc(A.offs, A.offs ? (A.n + 1) * 4 : 0u);
     const __amdgpu_buffer_rsrc_t rhllw = part_rsrc(A.hllw, A.n * 4);
-    const __amdgpu_buffer_rsrc_t rfail0 = part_rsrc(A.fail, A.n);
     const __amdgpu_buffer_rsrc_t roff = part_rsrc(A.off, nunits * A.off_stride * 4);
     auto offsets = [&](uint32_t t, uint32_t u, uint32_t &b, uint32_t &e) {
         const uint32_t i = t * kTile + u * kT + tid;
@@ -506,8 +508,8 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
             {
                 uint32_t idx, rank;
                 hll_patlen(hh, idx, rank);
+                // (its top byte is the swipe's overflow flag, set by pass B)
                 __builtin_amdgcn_raw_buffer_store_b32(idx | (rank << 16), rhllw, act ? i * 4 : kOORa, 0, nt_aux<8>());
-                __builtin_amdgcn_raw_buffer_store_b8(uint8_t(0), rfail0, act ? i : kOORa, 0, nt_aux<8>());
             }
             const uint32_t lu20 = lu << 20;
             ProbeWalk32 wk;
@@ -781,7 +783,12 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                 *reinterpret_cast<uint4 *>(img + (c * kPbBlock + threadIdx.x) * 16) = piece[c];
         }
         lds_barrier();
-        const __amdgpu_buffer_rsrc_t rfail = part_rsrc(A.fail + size_t(l) * A.fail_stride, A.fail_stride);
+        // failures that do not fit a fail list: a byte store of 1 (FL: into
+        // the top byte of the swipe's HLL word -- byte 4 i + 3, which pass A
+        // wrote 0 -- so pass A writes no fail bytes and C reads none)
+        const __amdgpu_buffer_rsrc_t rfail =
+            FL ? part_rsrc(A.hllw, A.n * 4) : part_rsrc(A.fail + size_t(l) * A.fail_stride, A.fail_stride);
+        auto fail_at = [](uint32_t i) { return FL ? i * 4 + 3 : i; };
         const uint32_t orow = (FL ? unit : g) * A.off_stride, erow = ge * A.off_stride;
         // run boundaries of 8 rounds at once: lane L holds those of tile
         // tg0 + (L / 8) * kStep + L % 8 (0, 0 past tb); a round's lanes take
@@ -916,7 +923,7 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                     fm &= fm - 1;
                     const uint32_t at = (pick(j) >> 20) & tmask;  // k_part_a3's swipe field
                     if (pos < kPbLanes) q[k * kPbLanes + pos] = at;
-                    else __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail, tbase + at, 0, 0);  // overflow
+                    else __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail, fail_at(tbase + at), 0, 0);  // overflow
                     pos++;
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -961,7 +968,7 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                                                     : ((rr & kPSliceMask) | ((rr >> kPTileLog) & kPSliceBits));
                     if (!((img[o >> 3] >> (o & 7)) & 1))
                         __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail,
-                                                             tbase + ((rr >> (FL ? 20 : kPSliceLog)) & tmask), 0, 0);
+                                                             fail_at(tbase + ((rr >> (FL ? 20 : kPSliceLog)) & tmask)), 0, 0);
                 }
             }
             bc = b1;
@@ -1079,9 +1086,9 @@ __global__ void __launch_bounds__(kPcFlBlock) k_part_c_fl(const PartArgs A) {
         for (int u = 0; u < U; u++) {
             const uint32_t i = t * 1024 + uint32_t(u) * kPcFlBlock + tid;
             const bool act = t < tend && i < A.n;
-            in.fb[u] = act ? nt_ld<16>(A.fail + i) : 1u;
             in.sl[u] = act ? nt_ld<16>(A.slot + i) : 0u;
-            in.hv[u] = act ? nt_ld<16>(A.hllw + i) : 0u;
+            in.hv[u] = act ? nt_ld<16>(A.hllw + i) : 0xff000000u;  // (top byte: pass B's overflow flag)
+            in.fb[u] = in.hv[u] >> 24;
         }
     };
     lds_barrier();
@@ -1128,7 +1135,7 @@ __global__ void __launch_bounds__(kPcFlBlock) k_part_c_fl(const PartArgs A) {
                 w[u] = nullptr;
                 rank[u] = sh[u] = 0;
                 if (valid[u]) {
-                    const uint32_t rk = cur.hv[u] >> 16;
+                    const uint32_t rk = (cur.hv[u] >> 16) & 0xffu;
                     if (cur.sl[u] >= A.nslots) {
                         atomicOr(A.err, 1u);
                     } else {
@@ -1282,15 +1289,15 @@ __global__ void __launch_bounds__(1024, 8) k_seg_c1(const PartArgs A, const SegA
         const uint32_t t0 = r * kSegRunTiles;
         const uint32_t t1 = t0 + kSegRunTiles < A.ntiles ? t0 + kSegRunTiles : A.ntiles;
         const uint16_t ep = uint16_t(r + 1);  // <= 2048: marks are never cleared
-        // the run's streams, every tile's in flight together
-        uint32_t fb[kSegRunTiles], sl[kSegRunTiles], hv[kSegRunTiles];
+        // the run's streams, every tile's in flight together (the HLL
+        // word's top byte is pass B's overflow flag)
+        uint32_t sl[kSegRunTiles], hv[kSegRunTiles];
 #pragma unroll
         for (uint32_t u = 0; u < kSegRunTiles; u++) {
             const uint32_t i = (t0 + u) * 1024 + tid;
             const bool act = t0 + u < t1 && i < A.n;
-            fb[u] = act ? nt_ld<16>(A.fail + i) : 1u;
             sl[u] = act ? nt_ld<16>(A.slot + i) : 0u;
-            hv[u] = act ? nt_ld<16>(A.hllw + i) : 0u;
+            hv[u] = act ? nt_ld<16>(A.hllw + i) : 0xff000000u;
         }
         if (tid <= S.nb1) cnt[tid] = 0;
         // the run's fail lists -> marks (piece p = unit p / 8, tile t0 + p % 8)
@@ -1322,7 +1329,7 @@ __global__ void __launch_bounds__(1024, 8) k_seg_c1(const PartArgs A, const SegA
         for (uint32_t u = 0; u < kSegRunTiles; u++) {
             const uint32_t i = (t0 + u) * 1024 + tid;
             const bool act = t0 + u < t1 && i < A.n;
-            const bool valid = act && fb[u] == 0 && mark[u * 1024 + tid] != ep;
+            const bool valid = act && (hv[u] >> 24) == 0 && mark[u * 1024 + tid] != ep;
             if (A.out && act) nt_st<16>(A.out + i, uint8_t(valid));
             pos[u] = 0xffffffffu;
             rec[u] = 0;
@@ -1906,7 +1913,10 @@ static hipError_t part_scratch(PartArgs *A, uint64_t n, uint32_t sub, const SegO
     part_glayout(A, so, ntiles_max);
     A->rec = (uint32_t *)scratch_get(scr, 28, (size_t(A->govf) + size_t(ntiles_max) * A->stride) * 4, &e);
     if (e == hipSuccess) A->off = (uint32_t *)scratch_get(scr, 29, size_t(A->off_stride) * (A->nslices + 1) * 4, &e);
-    if (e == hipSuccess) A->fail = (uint8_t *)scratch_get(scr, 30, size_t(fstride) * A->nlinks, &e);
+    // (fail bytes: the fail-list chains keep their overflow flags in the HLL words)
+    A->fail = nullptr;
+    if (e == hipSuccess && !part_flist(*A))
+        A->fail = (uint8_t *)scratch_get(scr, 30, size_t(fstride) * A->nlinks, &e);
     if (e == hipSuccess) A->hllw = (uint32_t *)scratch_get(scr, 31, size_t(m) * 4, &e);
     A->fail_stride = fstride;
     A->fl_stride = A->off_stride;

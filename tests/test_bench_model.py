@@ -22,9 +22,13 @@ def test_partitioned_pass_bytes_c3():
     alg = b.pass_bytes(n, nvalid, probes, 8, False, [(bits, k)])
     nslices, ntiles = 302, 15_625                  # ceil(bits / 2^19), ceil(n / 1024)
     rec = 4 * k * n
-    assert alg["k_part_a"] == n * (8 + 4) + rec + 4 * (nslices + 1) * ntiles + 4 * n + n
+    # (the fail-list chain: no fail bytes -- overflow flags in the HLL word)
+    assert alg["k_part_a"] == n * (8 + 4) + rec + 4 * (nslices + 1) * ntiles + 4 * n
     assert alg["k_part_b"] == rec + 8 * nslices * ntiles + bits // 8
-    assert alg["k_part_c"] == n * (1 + 4 + 4 + 1) + 128 * nvalid   # 128 B per valid swipe
+    assert alg["k_part_c"] == n * (4 + 4 + 1) + 128 * nvalid   # 128 B per valid swipe
+    # a two-link chain keeps one fail byte per swipe and link
+    alg2 = b.pass_bytes(n, nvalid, probes, 8, False, [(bits, 8), (2 * bits, 9)])
+    assert alg2["k_part_c"] == n * (2 + 4 + 4 + 1) + 128 * nvalid
     assert alg["k1_stage"] == 0
 
 
