@@ -189,6 +189,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t part_rsrc(const void *p, uint3
 #ifndef SKE_NT
 #define SKE_NT 71
 #endif
+// pass A3's id prefetch distance: 1 -- a tile's ids load after the previous
+// tile's atomics (from offsets loaded at that tile's start); 2 -- at the
+// previous tile's start, from offsets loaded a tile earlier
+#ifndef SKE_PA_AHEAD
+#define SKE_PA_AHEAD 2
+#endif
 typedef uint32_t part_u32x4 __attribute__((ext_vector_type(4)));
 template <int BIT, class T> __device__ __forceinline__ T nt_ld(const T *p) {
     if constexpr ((SKE_NT & BIT) != 0) return __builtin_nontemporal_load(p);
@@ -472,11 +478,19 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
     PartId it[kU];
     uint32_t gofs[kPer / 2] = {};  // GL: this thread's units' places in the current group
     {
+        // the first tile's ids, then the second tile's offsets (SKE_PA_AHEAD
+        // 2: a tile's ids load at the start of the tile before it, from
+        // offsets loaded one tile earlier still)
         const uint32_t t = tfirst;
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++) {
             offsets(t < gt1 ? t : gt0, u, nb_[u], ne_[u]);
             part_id_load(rbytes, nb_[u], ne_[u], it[u]);
+        }
+        if (SKE_PA_AHEAD == 2) {
+            const uint32_t t1 = t < gt1 && tnext(t) < gt1 ? tnext(t) : (t < gt1 ? t : gt0);
+#pragma unroll
+            for (uint32_t u = 0; u < kU; u++) offsets(t1, u, nb_[u], ne_[u]);
         }
     }
     const uint8_t *cntb = reinterpret_cast<const uint8_t *>(cnt);
@@ -495,8 +509,19 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
         const uint32_t pb = cb * 4;  // the parity's byte base, above (kCnt - 1) * 4
         uint32_t rv[kU][KM], rp[kU][KM];
         const uint32_t tn = tnext(t) < gt1 ? tnext(t) : t;
+        PartId itn[kU];
+        if (SKE_PA_AHEAD == 2) {
+            // the next tile's ids (nb_ / ne_ hold its offsets), then the
+            // offsets of the tile after it
+            const uint32_t tn2 = tnext(tn) < gt1 ? tnext(tn) : tn;
 #pragma unroll
-        for (uint32_t u = 0; u < kU; u++) offsets(tn, u, nb_[u], ne_[u]);
+            for (uint32_t u = 0; u < kU; u++) part_id_load(rbytes, nb_[u], ne_[u], itn[u]);
+#pragma unroll
+            for (uint32_t u = 0; u < kU; u++) offsets(tn2, u, nb_[u], ne_[u]);
+        } else {
+#pragma unroll
+            for (uint32_t u = 0; u < kU; u++) offsets(tn, u, nb_[u], ne_[u]);
+        }
         const bool full = (t + 1) * kTile <= A.n;  // block-uniform
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++) {
@@ -538,7 +563,10 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
         }
         lds_barrier();
 #pragma unroll
-        for (uint32_t u = 0; u < kU; u++) part_id_load(rbytes, nb_[u], ne_[u], it[u]);  // the next tile's ids
+        for (uint32_t u = 0; u < kU; u++) {  // the next tile's ids
+            if (SKE_PA_AHEAD == 2) it[u] = itn[u];
+            else part_id_load(rbytes, nb_[u], ne_[u], it[u]);
+        }
         // exclusive scan over pairs of their two slices' counts
         uint32_t v[kPer], s = 0;
 #pragma unroll
