@@ -1569,7 +1569,14 @@ template <int KLOG> struct SegE {
     static constexpr uint32_t RPT = KLOG >= 3 ? 16 : (KLOG == 2 ? 8 : 4);  // records per thread per round
     static constexpr uint32_t EP = KLOG == 2 ? 512 : T;  // runs staged at once
 };
-__host__ __device__ constexpr uint32_t seg_slice(uint32_t klog) { return 16384u << (klog < 2 ? klog : 2); }
+// records per slice of a cut window: SKE_SEG_SLICE << min(klog, 2) (64 k at
+// klog 1: the window pass 0.930 -> 0.891 ms at N = 1 and 0.477 -> 0.427 ms at
+// the 8-way shard against 32 k; 16 k / 8 k / 128 k slower --
+// profiles/r05_ab_seg_slice.txt)
+#ifndef SKE_SEG_SLICE
+#define SKE_SEG_SLICE 32768
+#endif
+__host__ __device__ constexpr uint32_t seg_slice(uint32_t klog) { return uint32_t(SKE_SEG_SLICE) << (klog < 2 ? klog : 2); }
 
 template <int KLOG, bool QUEUE>
 __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const PartArgs A, const SegArgs S) {
