@@ -1562,11 +1562,14 @@ hipError_t set_seg_stamp_buffer(void *) { return hipErrorNotSupported; }
 // Block shape per window size: windows of 2^KLOG keys (16 KiB each) in
 // blocks of T threads, BPC blocks resident per CU (LDS: the window + its
 // staging), so that small windows keep more windows in flight per CU.
+#ifndef SKE_SEG_RPT1
+#define SKE_SEG_RPT1 4
+#endif
 template <int KLOG> struct SegE {
     static constexpr uint32_t T = KLOG >= 2 ? 1024 : (KLOG == 1 ? 512 : 256);
     static constexpr uint32_t BPC = KLOG >= 3 ? 1 : (KLOG == 2 ? 2 : (KLOG == 1 ? 4 : 8));
     static constexpr uint32_t WPS = T / 64 * BPC / 4;  // waves per SIMD (launch bounds)
-    static constexpr uint32_t RPT = KLOG >= 3 ? 16 : (KLOG == 2 ? 8 : 4);  // records per thread per round
+    static constexpr uint32_t RPT = KLOG >= 3 ? 16 : (KLOG == 2 ? 8 : SKE_SEG_RPT1);  // records per thread per round
     static constexpr uint32_t EP = KLOG == 2 ? 512 : T;  // runs staged at once
 };
 // records per slice of a cut window: SKE_SEG_SLICE << min(klog, 2) (64 k at
