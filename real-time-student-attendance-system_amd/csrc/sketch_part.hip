@@ -721,13 +721,17 @@ hipError_t set_pb_stamp_buffer(void *p) {
 // SKE_PB_SPLIT: how pass B's blocks share the (slice unit, tile) space.
 // 0: per XCD tile group, unit major (round 3); 1: all tiles, unit major (a
 // block restages its image once or twice: pass B 0.189 -> 0.183 ms);
-// 2 (default): XCD x takes tile group x and its 32 blocks take units round
+// 2: XCD x takes tile group x and its 32 blocks take units round
 // robin, so adjacent units' runs, which share their boundary lines, are read
 // by neighbouring CUs of one XCD at about the same time (round 4, A/B of
 // three alternations on one box: 0.211 -> 0.200 ms; 128-B read requests
-// 8.34 -> 8.06 M, L2 hits 0.65 -> 1.84 M per dispatch)
+// 8.34 -> 8.06 M, L2 hits 0.65 -> 1.84 M per dispatch); 3 (default, round 5):
+// as 2 while every block gets a whole unit (4 rounds of 32 of C3's 152), then
+// the remaining units' (unit, 8-tile group) space in equal contiguous shares,
+// so no block runs a fifth unit while the others wait (pass B 0.368 -> 0.362
+// ms per 2^25 sub-batch, three alternations; profiles/r05_ab_pass_b_split.txt)
 #ifndef SKE_PB_SPLIT
-#define SKE_PB_SPLIT 2
+#define SKE_PB_SPLIT 3
 #endif
 // GL (FL only): the group layout -- a run's start is its place in the (tile
 // group, unit) region, or (bit 31 of its run word) in the tile's overflow row
@@ -757,10 +761,27 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
     const uint32_t total = nunits * gn;
     uint32_t w = uint32_t(uint64_t(total) * bi / nblk);
     uint32_t wend = uint32_t(uint64_t(total) * (bi + 1) / nblk);
-    uint32_t su = bi;  // SKE_PB_SPLIT 2: this block's current unit
-    if (SKE_PB_SPLIT == 2) {
-        w = su < nunits ? su * gn : total;
-        wend = su < nunits ? w + gn : total;
+    uint32_t su = bi;  // SKE_PB_SPLIT 2 / 3: this block's current unit
+    // SKE_PB_SPLIT 3: units round robin while every block gets a whole one,
+    // then the remaining units' (unit, 8-tile group) space in equal
+    // contiguous shares, so no block waits with a fifth unit while others idle
+    const uint32_t full = SKE_PB_SPLIT == 3 ? nunits / nblk * nblk : nunits;
+    const uint32_t gn8 = (gn + 7) / 8;
+    auto lin = [&](uint32_t c) {  // the remaining space's 8-tile group c as a (unit, tile) index
+        const uint32_t t8 = (c % gn8) * 8;
+        return (full + c / gn8) * gn + (t8 < gn ? t8 : gn);
+    };
+    bool rest = false;
+    auto take_rest = [&]() {
+        const uint32_t space = (nunits - full) * gn8;
+        w = lin(uint32_t(uint64_t(space) * bi / nblk));
+        wend = lin(uint32_t(uint64_t(space) * (bi + 1) / nblk));
+        rest = true;
+    };
+    if (SKE_PB_SPLIT == 2 || SKE_PB_SPLIT == 3) {
+        w = su < full ? su * gn : total;
+        wend = su < full ? w + gn : total;
+        if (SKE_PB_SPLIT == 3 && su >= full) take_rest();
     }
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t k = lane / kPbLanes, qq = lane % kPbLanes;
@@ -776,11 +797,17 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
     uint32_t *q = fq[wave];
     while (true) {
         if (w >= wend) {
-            if (SKE_PB_SPLIT != 2) break;
+            if (SKE_PB_SPLIT != 2 && SKE_PB_SPLIT != 3) break;
+            if (rest) break;
             su += nblk;  // block-uniform
-            if (su >= nunits) break;
-            w = su * gn;
-            wend = w + gn;
+            if (su < full) {
+                w = su * gn;
+                wend = w + gn;
+            } else {
+                if (SKE_PB_SPLIT == 2) break;
+                take_rest();
+                if (w >= wend) break;
+            }
         }
         // slices g .. g + SP - 1 (SP = 2: one link only, host-checked), so
         // one run per tile covers them all
