@@ -1592,9 +1592,12 @@ hipError_t set_seg_stamp_buffer(void *) { return hipErrorNotSupported; }
 #ifndef SKE_SEG_RPT1
 #define SKE_SEG_RPT1 4
 #endif
+#ifndef SKE_SEG_BPC1
+#define SKE_SEG_BPC1 4  // blocks per CU at klog 1
+#endif
 template <int KLOG> struct SegE {
     static constexpr uint32_t T = KLOG >= 2 ? 1024 : (KLOG == 1 ? 512 : 256);
-    static constexpr uint32_t BPC = KLOG >= 3 ? 1 : (KLOG == 2 ? 2 : (KLOG == 1 ? 4 : 8));
+    static constexpr uint32_t BPC = KLOG >= 3 ? 1 : (KLOG == 2 ? 2 : (KLOG == 1 ? SKE_SEG_BPC1 : 8));
     static constexpr uint32_t WPS = T / 64 * BPC / 4;  // waves per SIMD (launch bounds)
     static constexpr uint32_t RPT = KLOG >= 3 ? 16 : (KLOG == 2 ? 8 : SKE_SEG_RPT1);  // records per thread per round
     static constexpr uint32_t EP = KLOG == 2 ? 512 : T;  // runs staged at once
