@@ -1292,7 +1292,8 @@ struct SegArgs {
     uint32_t maxch;   // level-2 chunk slots per sub-batch
     uint32_t nwin;    // windows of the slab (E)
     uint32_t dense_min;  // E: records at which a window is staged in LDS
-    uint32_t *q;      // window pass queue header: [0] queued slices, [1] copies, [2] cut windows (zeroed per call)
+    uint32_t *q;      // window pass queue header: [0] queued slices, [1] copies, [2] cut windows, [4] / [5] E1 / E2
+                      // items claimed past the first gridDim.x (zeroed per window pass)
     uint4 *qitems;    // queued slices (window, slice, copy)
     uint4 *mlist;     // cut windows (window, first copy, slices)
     uint8_t *copies;  // [ccap][window bytes] LDS copies of cut windows' slices
@@ -1595,6 +1596,9 @@ hipError_t set_seg_stamp_buffer(void *) { return hipErrorNotSupported; }
 #ifndef SKE_SEG_BPC1
 #define SKE_SEG_BPC1 4  // blocks per CU at klog 1
 #endif
+#ifndef SKE_SEG_CLAIM
+#define SKE_SEG_CLAIM 1  // the window pass claims items from a counter
+#endif
 template <int KLOG> struct SegE {
     static constexpr uint32_t T = KLOG >= 2 ? 1024 : (KLOG == 1 ? 512 : 256);
     static constexpr uint32_t BPC = KLOG >= 3 ? 1 : (KLOG == 2 ? 2 : (KLOG == 1 ? SKE_SEG_BPC1 : 8));
@@ -1705,7 +1709,11 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
         p2(0, wi_n);
         image(wi_n);
     }
-    for (; it < nitems; it += gridDim.x, par ^= 1) {
+    // items past the first gridDim.x are claimed one ahead from a counter
+    // (SKE_SEG_CLAIM; else every gridDim.x-th), so a block that drew a hot
+    // window's long first slice takes fewer of the rest
+    uint32_t nit = 0;
+    for (; it < nitems; it = nit, par ^= 1) {
         const uint32_t wi = wi_n, sl = sl_n;
         uint32_t copy = copy_n;
         const uint32_t np = pnp;
@@ -1758,9 +1766,10 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
         const bool dense = nrec > 0 && (cut || nrec >= S.dense_min);
         if (dense)
             for (uint32_t j = tid; j < NL; j += T) dirty[j] = 0;
+        if (SKE_SEG_CLAIM && tid == 0) hdr[1] = gridDim.x + atomicAdd(&S.q[QUEUE ? 5 : 4], 1u);
         __syncthreads();  // the window's registers landed in LDS (vmcnt), its first runs staged
         // P1 of the next item: its loads fly while this item's records are raised
-        const uint32_t nit = it + gridDim.x;
+        nit = SKE_SEG_CLAIM ? hdr[1] : it + gridDim.x;
         if (nit < nitems) {
             item(nit, wi_n, sl_n, copy_n);
             p1(wi_n);
@@ -2094,7 +2103,7 @@ static hipError_t seg_scratch(const SegPlan &P, uint32_t sub, uint64_t n, Scratc
     // copies, queue entries and cut windows always suffice
     const uint32_t ccap = uint32_t(2 * ((mg + seg_slice(P.klog) - 1) / seg_slice(P.klog)) + 2);
     const size_t wb = size_t(1) << (P.klog + kHllP);
-    if (e == hipSuccess) S->q = (uint32_t *)scratch_get(scr, 39, 16, &e);
+    if (e == hipSuccess) S->q = (uint32_t *)scratch_get(scr, 39, 32, &e);
     if (e == hipSuccess) S->qitems = (uint4 *)scratch_get(scr, 42, size_t(ccap) * 16, &e);
     if (e == hipSuccess) S->mlist = (uint4 *)scratch_get(scr, 43, size_t(ccap) * 16, &e);
     if (e == hipSuccess) S->copies = (uint8_t *)scratch_get(scr, 45, size_t(ccap) * wb, &e);
@@ -2186,7 +2195,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             S.nsub = ns;
             A.n = 0;
             if (hook) hook(hook_user, 4, 0, st);
-            hipError_t we = hipMemsetAsync(S.q, 0, 16, st);
+            hipError_t we = hipMemsetAsync(S.q, 0, 32, st);
             if (we != hipSuccess) return we;
             switch (P.klog) {
 #define SEG_E_LAUNCH(K)                                                                                  \
