@@ -1292,8 +1292,8 @@ struct SegArgs {
     uint32_t maxch;   // level-2 chunk slots per sub-batch
     uint32_t nwin;    // windows of the slab (E)
     uint32_t dense_min;  // E: records at which a window is staged in LDS
-    uint32_t *q;      // window pass queue header: [0] queued slices, [1] copies, [2] cut windows, [4] / [5] E1 / E2
-                      // items claimed past the first gridDim.x (zeroed per window pass)
+    uint32_t *q;      // window pass queue header: [0] queued slices, [1] copies, [2] cut windows, [5] E2 items
+                      // and [8 + x] XCD x's E1 items claimed past the first gridDim.x (zeroed per window pass)
     uint4 *qitems;    // queued slices (window, slice, copy)
     uint4 *mlist;     // cut windows (window, first copy, slices)
     uint8_t *copies;  // [ccap][window bytes] LDS copies of cut windows' slices
@@ -1766,7 +1766,15 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
         const bool dense = nrec > 0 && (cut || nrec >= S.dense_min);
         if (dense)
             for (uint32_t j = tid; j < NL; j += T) dirty[j] = 0;
-        if (SKE_SEG_CLAIM && tid == 0) hdr[1] = gridDim.x + atomicAdd(&S.q[QUEUE ? 5 : 4], 1u);
+        // (E1: per XCD -- block b takes items i = b mod 8 from counter b mod 8,
+        // so the windows of a bucket (W mod nb1) stay on one XCD, whose L2
+        // then serves the chunk lines two neighbouring windows' runs share)
+        // (every residue mod 8 needs a block: a grid under 8 takes one counter)
+        if (SKE_SEG_CLAIM && tid == 0)
+            hdr[1] = QUEUE || gridDim.x < kPGroups
+                         ? gridDim.x + atomicAdd(&S.q[QUEUE ? 5 : 4], 1u)
+                         : gridDim.x + kPGroups * atomicAdd(&S.q[8 + blockIdx.x % kPGroups], 1u) +
+                               blockIdx.x % kPGroups;
         __syncthreads();  // the window's registers landed in LDS (vmcnt), its first runs staged
         // P1 of the next item: its loads fly while this item's records are raised
         nit = SKE_SEG_CLAIM ? hdr[1] : it + gridDim.x;
@@ -2103,7 +2111,7 @@ static hipError_t seg_scratch(const SegPlan &P, uint32_t sub, uint64_t n, Scratc
     // copies, queue entries and cut windows always suffice
     const uint32_t ccap = uint32_t(2 * ((mg + seg_slice(P.klog) - 1) / seg_slice(P.klog)) + 2);
     const size_t wb = size_t(1) << (P.klog + kHllP);
-    if (e == hipSuccess) S->q = (uint32_t *)scratch_get(scr, 39, 32, &e);
+    if (e == hipSuccess) S->q = (uint32_t *)scratch_get(scr, 39, 64, &e);
     if (e == hipSuccess) S->qitems = (uint4 *)scratch_get(scr, 42, size_t(ccap) * 16, &e);
     if (e == hipSuccess) S->mlist = (uint4 *)scratch_get(scr, 43, size_t(ccap) * 16, &e);
     if (e == hipSuccess) S->copies = (uint8_t *)scratch_get(scr, 45, size_t(ccap) * wb, &e);
@@ -2195,7 +2203,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             S.nsub = ns;
             A.n = 0;
             if (hook) hook(hook_user, 4, 0, st);
-            hipError_t we = hipMemsetAsync(S.q, 0, 32, st);
+            hipError_t we = hipMemsetAsync(S.q, 0, 64, st);
             if (we != hipSuccess) return we;
             switch (P.klog) {
 #define SEG_E_LAUNCH(K)                                                                                  \
