@@ -158,7 +158,7 @@ struct SegOpts {
     int b1 = -1;  // option "seg_b1": 2^b1 level-1 buckets (-1: auto, seg_plan)
 };
 // sizes the context scratch for batches of up to n swipes (no launch)
-// sub: swipes per sub-batch of the three passes (0: the default, 16M)
+// sub: swipes per sub-batch of the three passes (0: the default, 2^25 = kPSubDefault)
 hipError_t part_reserve(const ChainDev &ch, uint64_t n, uint32_t sub, uint32_t nslots, const SegOpts &so,
                         Scratch *scr);
 // hook (may be null): called as hook(user, pass, 0) right before and

@@ -757,6 +757,9 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
         bi = blockIdx.x / kPGroups;
     }
     const uint32_t gn = gt1 - gt0;
+    // (an empty XCD tile group -- a sub-batch of fewer than 64 tiles: the
+    // whole block leaves before the split arithmetic divides by gn8 = 0)
+    if (gn == 0) return;
     const uint32_t nunits = (A.nslices + SP - 1) / SP;
     const uint32_t total = nunits * gn;
     uint32_t w = uint32_t(uint64_t(total) * bi / nblk);
@@ -1272,6 +1275,7 @@ constexpr uint32_t kSegChunk = 8192;                        // records per level
 constexpr uint32_t kSegMaxRuns = kPSub / kSegRunSw;         // 8192 runs per sub-batch
 constexpr uint32_t kSegDStage = 2048;                       // D: runs of a chunk staged in LDS
 constexpr uint32_t kSegRecShift = 20;                       // record: slot-in-bucket above bit 20
+static_assert(kSegMaxRuns < 65536, "k_seg_c1's uint16 mark epochs (run + 1) would wrap");
 
 struct SegArgs {
     uint32_t *r1;     // [nruns][kSegRunSw] level-1 records of a sub-batch, bucket-sorted per run
@@ -1344,7 +1348,7 @@ __global__ void __launch_bounds__(1024, 8) k_seg_c1(const PartArgs A, const SegA
     for (uint32_t r = blockIdx.x; r < S.nruns; r += gridDim.x) {
         const uint32_t t0 = r * kSegRunTiles;
         const uint32_t t1 = t0 + kSegRunTiles < A.ntiles ? t0 + kSegRunTiles : A.ntiles;
-        const uint16_t ep = uint16_t(r + 1);  // <= 2048: marks are never cleared
+        const uint16_t ep = uint16_t(r + 1);  // <= kSegMaxRuns (8192) < 2^16: marks are never cleared
         // the run's streams, every tile's in flight together (the HLL
         // word's top byte is pass B's overflow flag)
         uint32_t sl[kSegRunTiles], hv[kSegRunTiles];
@@ -1447,6 +1451,14 @@ __global__ void __launch_bounds__(1024) k_seg_scan(const SegArgs S) {
     }
 }
 
+// D's record gather: 2 -- staged chunks read their run tables through LDS
+// pointers only and their records lane-interleaved (one buffer load covers
+// 64 consecutive records); 1 -- round 5's form (8 consecutive records per
+// thread, the run tables through a pointer that may be LDS or global, which
+// makes every table read a flat load)
+#ifndef SKE_SEG_D
+#define SKE_SEG_D 2
+#endif
 __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
     __shared__ uint32_t tot[kSegMaxB1], cbl[kSegMaxB1 + 1];
     // the chunk's runs' prefix and starts, staged when at most kSegDStage
@@ -1471,8 +1483,12 @@ __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
     lds_barrier();
     uint32_t *r2 = S.r2 + size_t(S.s) * S.maxch * kSegChunk;
     uint32_t *o2 = S.o2 + size_t(S.s) * S.maxch * (wpb + 1);
+    const __amdgpu_buffer_rsrc_t rr1 = part_rsrc(S.r1, S.nruns * kSegRunSw * 4);
+    (void)rr1;
     for (uint32_t q = blockIdx.x; q < nq; q += gridDim.x) {
-        const uint32_t h = seg_last_le(cbl, S.nb1, q);  // buckets without chunks share the next one's base
+        // (block-uniform: in a scalar register, so the bucket's run-table
+        // words below are scalar loads)
+        const uint32_t h = __builtin_amdgcn_readfirstlane(seg_last_le(cbl, S.nb1, q));  // buckets without chunks share the next one's base
         const uint32_t c = q - cbl[h], w0 = c * kSegChunk;
         const uint32_t w1 = tot[h] - w0 < kSegChunk ? tot[h] : w0 + kSegChunk;
         const uint32_t *pp = S.p1 + size_t(h) * (kSegMaxRuns + 1);
@@ -1482,6 +1498,65 @@ __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
         const uint32_t ng = gb - ga;
         const bool staged = ng < kSegDStage;  // block-uniform
         const uint32_t *gpp = pp + ga, *gob = S.o1 + size_t(h) * kSegMaxRuns + ga;
+        uint32_t rec[8], pos[8];
+#if SKE_SEG_D == 2
+        // Staged (every chunk but a sparse bucket's): the runs' record
+        // prefix and, per run, the offset that turns a record index into
+        // its word in r1 (run * 8192 + start in run - prefix), in LDS and
+        // read through LDS pointers only; records lane-interleaved (a wave
+        // reads 64 consecutive records per instruction), each lane's run
+        // found by its own binary search, 8 searches side by side.
+        if (staged)
+            for (uint32_t j = tid; j <= ng; j += 1024) {
+                const uint32_t a = gpp[j];
+                spp[j] = a;
+                if (j < ng) sob[j] = (ga + j) * kSegRunSw + gob[j] - a;
+            }
+        if (tid <= wpb) c2[tid] = 0;
+        lds_barrier();
+        if (staged) {
+            uint32_t k[8];
+#pragma unroll
+            for (uint32_t j = 0; j < 8; j++) k[j] = 0;
+            for (uint32_t len = ng; len > 1;) {
+                const uint32_t half = len >> 1;
+#pragma unroll
+                for (uint32_t j = 0; j < 8; j++) {
+                    const uint32_t p = w0 + j * 1024 + tid;
+                    k[j] = spp[k[j] + half] <= p ? k[j] + half : k[j];
+                }
+                len -= half;
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < 8; j++) {
+                const uint32_t p = w0 + j * 1024 + tid;
+                rec[j] = __builtin_amdgcn_raw_buffer_load_b32(rr1, p < w1 ? (sob[k[j]] + p) * 4 : kOOR, 0, 0);
+            }
+        } else {
+            // (a sparse bucket's chunk over more runs than LDS stages: read
+            // the run tables in place, one search per thread, then a walk)
+            const uint32_t p0 = w0 + tid * 8;
+            uint32_t k = p0 < w1 ? seg_last_le(gpp, ng, p0) : 0u;
+#pragma unroll
+            for (uint32_t j = 0; j < 8; j++) {
+                const uint32_t p = p0 + j;
+                rec[j] = 0;
+                if (p < w1) {
+                    while (gpp[k + 1] <= p) k++;
+                    rec[j] = S.r1[size_t(ga + k) * kSegRunSw + gob[k] + (p - gpp[k])];
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            pos[j] = 0xffffffffu;
+            const uint32_t p = staged ? w0 + j * 1024 + tid : w0 + tid * 8 + j;
+            if (p < w1) {
+                const uint32_t w2 = (rec[j] >> (kSegRecShift + S.klog)) & (wpb - 1);
+                pos[j] = (w2 << 16) | atomicAdd(&c2[w2], 1u);
+            }
+        }
+#else
         if (staged)
             for (uint32_t j = tid; j <= ng; j += 1024) {
                 spp[j] = gpp[j];
@@ -1491,7 +1566,6 @@ __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
         lds_barrier();
         const uint32_t *vpp = staged ? spp : gpp, *vob = staged ? sob : gob;
         // 8 consecutive records per thread: one search, then a walk
-        uint32_t rec[8], pos[8];
         const uint32_t p0 = w0 + tid * 8;
         uint32_t k = p0 < w1 ? seg_last_le(vpp, ng, p0) : 0u;
 #pragma unroll
@@ -1511,6 +1585,7 @@ __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
                 pos[j] = (w2 << 16) | atomicAdd(&c2[w2], 1u);
             }
         }
+#endif
         lds_barrier();
         uint32_t total;
         const uint32_t ex = seg_scan(tid <= wpb ? c2[tid] : 0u, ws, total);
