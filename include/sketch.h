@@ -174,13 +174,19 @@ int ske_hll_pfadd(ske_ctx *ctx, const uint32_t *slot, const uint8_t *bytes,
 int ske_hll_pfcount(ske_ctx *ctx, const uint32_t *slots, uint32_t nkeys, uint64_t *out);
 /* PFCOUNT of each key separately (rankings, attendance_analysis.py:87-97 as
  * README.md:179 describes); slots == NULL: keys 0..nkeys-1 of the slab.
- * Group form: union over slots[goffs[g]..goffs[g+1]). */
+ * Group form: union over slots[goffs[g]..goffs[g+1]).  With SKE_MEM_DEVICE the
+ * slot list of the each form is range-checked on the device (SKE_ERANGE). */
 int ske_hll_pfcount_each(ske_ctx *ctx, const uint32_t *slots, uint32_t nkeys, uint64_t *out,
                          int mem);
 int ske_hll_pfcount_groups(ske_ctx *ctx, const uint32_t *slots, const uint32_t *goffs,
                            uint32_t ngroups, uint64_t *out, int mem);
 /* PFMERGE dst src...  (dst's own registers take part, as in Redis) */
 int ske_hll_pfmerge(ske_ctx *ctx, uint32_t dst, const uint32_t *srcs, uint32_t n);
+/* the same with a device-resident source list (a plan kept on the GPU, e.g.
+ * the campus PFMERGE of C5's 1.8M day keys): its range is checked on the
+ * device (SKE_ERANGE), nothing is staged from the host.
+ *   replaces: PFMERGE (north star; attendance_analysis.py:87-97 as README.md:179) */
+int ske_hll_pfmerge_dev(ske_ctx *ctx, uint32_t dst, const uint32_t *srcs_dev, uint32_t n);
 int ske_hll_histogram(ske_ctx *ctx, uint32_t slot, uint32_t *out64);
 int ske_hll_export_raw(ske_ctx *ctx, uint32_t slot, uint8_t *out16384);
 int ske_hll_export_dense(ske_ctx *ctx, uint32_t slot, uint8_t *out12288);

@@ -79,8 +79,8 @@ struct ske_ctx {
     double *tau = nullptr, *sig = nullptr;  // device estimator tables (lazy)
     Scratch *scratch = nullptr;
     // staging buffers (grow on demand)
-    void *stg[8] = {};
-    size_t stg_cap[8] = {};
+    void *stg[9] = {};  // staging buffers by use (8: the device slot-range check word)
+    size_t stg_cap[9] = {};
     HostStager *hs = nullptr;  // pinned double buffer + copy threads for pageable inputs (lazy)
     unsigned int *err = nullptr;  // [0] sticky slot-error word; see check_call_err
     bool err_pending = false;     // taken from the device, not yet reported by ske_sync
@@ -693,7 +693,7 @@ int ske_close(ske_ctx *c) {
     if (c->regs) (void)hipFree(c->regs);
     if (c->tau) (void)hipFree(c->tau);
     if (c->sig) (void)hipFree(c->sig);
-    for (int i = 0; i < 8; i++)
+    for (int i = 0; i < 9; i++)
         if (c->stg[i]) (void)hipFree(c->stg[i]);
     stager_delete(c->hs);
     if (c->err) (void)hipFree(c->err);
@@ -1627,6 +1627,20 @@ static int check_slots_host(ske_ctx *c, const uint32_t *slots, uint64_t n) {
     return SKE_OK;
 }
 
+// a device-resident slot list in range of the slab (one reduction kernel and
+// a 4-byte read back): SKE_ERANGE before any kernel addresses the slab with it
+static int check_slots_dev(ske_ctx *c, const uint32_t *slots, uint64_t n) {
+    if (n == 0) return SKE_OK;
+    int rc = SKE_OK;
+    unsigned int *d = (unsigned int *)stage_buf(c, 8, 4, &rc);
+    if (rc) return rc;
+    unsigned int mx = 0;
+    HIPCHK(c, launch_slots_max(slots, n, d, c->cus, c->st));
+    HIPCHK(c, hipMemcpyAsync(&mx, d, 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return mx >= c->nslots ? SKE_ERANGE : SKE_OK;
+}
+
 int ske_hll_pfcount(ske_ctx *c, const uint32_t *slots, uint32_t nkeys, uint64_t *out) {
     if (!c || !slots || !out || nkeys == 0) return SKE_EINVAL;
     int rc = check_slots_host(c, slots, nkeys);
@@ -1645,8 +1659,8 @@ int ske_hll_pfcount_each(ske_ctx *c, const uint32_t *slots, uint32_t nkeys, uint
                          int mem) {
     if (!c || !out) return SKE_EINVAL;
     if (nkeys == 0) return SKE_OK;
-    if (mem != SKE_MEM_DEVICE && slots) {
-        int rc = check_slots_host(c, slots, nkeys);
+    if (slots) {
+        int rc = mem == SKE_MEM_DEVICE ? check_slots_dev(c, slots, nkeys) : check_slots_host(c, slots, nkeys);
         if (rc) return rc;
     }
     const uint32_t *ds = nullptr;
@@ -1710,14 +1724,14 @@ int ske_hll_count_raw_dev(ske_ctx *c, const uint8_t *regs_dev, uint32_t nkeys, u
     return pfcount_impl(c, regs_dev, nullptr, nullptr, nkeys, out, SKE_MEM_HOST);
 }
 
-int ske_hll_pfmerge(ske_ctx *c, uint32_t dst, const uint32_t *srcs, uint32_t n) {
+static int pfmerge_impl(ske_ctx *c, uint32_t dst, const uint32_t *srcs, uint32_t n, int mem) {
     if (!c || (n && !srcs)) return SKE_EINVAL;
     if (dst >= c->nslots) return SKE_ERANGE;
-    int rc = check_slots_host(c, srcs, n);
+    int rc = mem == SKE_MEM_DEVICE ? check_slots_dev(c, srcs, n) : check_slots_host(c, srcs, n);
     if (rc) return rc;
     if (n == 0) return SKE_OK;
     const uint32_t *ds;
-    rc = stage_u32(c, srcs, n, SKE_MEM_HOST, 6, &ds);
+    rc = stage_u32(c, srcs, n, mem, 6, &ds);
     if (rc) return rc;
     if (n <= 256) {
         HIPCHK(c, launch_pfmerge(c->regs, dst, ds, n, c->st));
@@ -1735,6 +1749,14 @@ int ske_hll_pfmerge(ske_ctx *c, uint32_t dst, const uint32_t *srcs, uint32_t n) 
     }
     HIPCHK(c, hipStreamSynchronize(c->st));
     return SKE_OK;
+}
+
+int ske_hll_pfmerge(ske_ctx *c, uint32_t dst, const uint32_t *srcs, uint32_t n) {
+    return pfmerge_impl(c, dst, srcs, n, SKE_MEM_HOST);
+}
+
+int ske_hll_pfmerge_dev(ske_ctx *c, uint32_t dst, const uint32_t *srcs_dev, uint32_t n) {
+    return pfmerge_impl(c, dst, srcs_dev, n, SKE_MEM_DEVICE);
 }
 
 int ske_hll_histogram(ske_ctx *c, uint32_t slot, uint32_t *out64) {

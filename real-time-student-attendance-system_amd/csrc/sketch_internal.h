@@ -25,6 +25,7 @@ hipError_t launch_pfmerge(uint8_t *regs, uint32_t dst, const uint32_t *srcs, uin
 uint32_t pfmerge_partitions(uint32_t n, int cus, uint32_t *per);
 hipError_t launch_pfmerge_wide(uint8_t *regs, uint32_t dst, const uint32_t *srcs, uint32_t n,
                                uint8_t *partial, uint32_t per, uint32_t P, hipStream_t st);
+hipError_t launch_slots_max(const uint32_t *slots, uint64_t n, unsigned int *out, int cus, hipStream_t st);
 hipError_t launch_merge_groups(const uint8_t *regs, const uint32_t *slots, const uint32_t *goffs,
                                uint32_t ngroups, uint8_t *dst, int cus, hipStream_t st);
 hipError_t launch_dense(const uint8_t *regs, uint8_t *dense, hipStream_t st);

@@ -785,6 +785,27 @@ hipError_t launch_pfmerge_wide(uint8_t *regs, uint32_t dst, const uint32_t *srcs
     return hipGetLastError();
 }
 
+// the largest of n device slots, into *out (zeroed by the caller): the range
+// check of a device-resident slot list (ske_hll_pfmerge_dev, ske_hll_pfcount_each
+// with SKE_MEM_DEVICE) before any kernel addresses the slab with it
+__global__ void __launch_bounds__(256) k_slots_max(const uint32_t *__restrict__ s, uint64_t n, unsigned int *out) {
+    uint32_t m = 0;
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256)
+        m = s[i] > m ? s[i] : m;
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t y = __shfl_xor(m, o, 64);
+        m = y > m ? y : m;
+    }
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
+}
+
+hipError_t launch_slots_max(const uint32_t *slots, uint64_t n, unsigned int *out, int cus, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(out, 0, 4, st);
+    if (e != hipSuccess || n == 0) return e;
+    hipLaunchKernelGGL(k_slots_max, dim3(grid_for(n, 256, cus * 4)), dim3(256), 0, st, slots, n, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_dense(const uint8_t *regs, uint8_t *dense, hipStream_t st) {
     hipLaunchKernelGGL(k_dense, dim3(kHllRegs / 4 / 256), dim3(256), 0, st, regs, dense);
     return hipGetLastError();

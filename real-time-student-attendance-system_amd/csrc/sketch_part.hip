@@ -1424,7 +1424,15 @@ __global__ void __launch_bounds__(1024, 8) k_seg_c1(const PartArgs A, const SegA
     }
 }
 
+// C1 with the next run's streams in flight (chains whose fail lists of a run
+// fit NP 16-B pieces per thread: C3/C5's 152 slice pairs take 1216 of 2048).
+// The run's slots, HLL words and fail lists are loaded into registers while
+// the previous run is sorted and copied out; every memory operation after
+// those loads is a buffer operation issued a fixed number of times (offsets
+// past a range for lanes with nothing to do), so the wait for them is exact
+// and does not wait for the copy-out's stores.  Same output as k_seg_c1.
 __global__ void __launch_bounds__(1024) k_seg_scan(const SegArgs S) {
+
     __shared__ uint32_t ws[16];
     const uint32_t h = blockIdx.x, tid = threadIdx.x;
     const uint32_t *oa = S.o1 + size_t(h) * kSegMaxRuns, *ob = oa + kSegMaxRuns;
@@ -1451,22 +1459,34 @@ __global__ void __launch_bounds__(1024) k_seg_scan(const SegArgs S) {
     }
 }
 
-// D's record gather: 2 -- staged chunks read their run tables through LDS
-// pointers only and their records lane-interleaved (one buffer load covers
-// 64 consecutive records); 1 -- round 5's form (8 consecutive records per
-// thread, the run tables through a pointer that may be LDS or global, which
-// makes every table read a flat load)
-#ifndef SKE_SEG_D
-#define SKE_SEG_D 2
+// D: per chunk of 8 192 records of one bucket, the records gathered from
+// the level-1 runs that hold them and counting-sorted by window within the
+// bucket.  A staged chunk (every chunk but a sparse bucket's: fewer than
+// kSegDStage runs) keeps its runs' record prefix and, per run, the offset
+// that turns a record index into its word in r1 (run * 8192 + start in run
+// - prefix) in LDS, read through LDS pointers only (round 5 read them
+// through a pointer that could be LDS or global: every table read a flat
+// load); records are lane-interleaved (one buffer load covers 64
+// consecutive records), each lane's run found by its own binary search, 8
+// searches side by side (S + D 0.122 -> 0.100 ms per 2^25 sub-batch,
+// profiles/r06_ab_seg_d.txt).  Not kept (profiles/r06_ab_seg_c1d.txt): the
+// next chunk's run-table words loaded during this chunk's sort
+// (SKE_SEG_D_PIPE 1: 0.101 -> 0.106 ms, 64 VGPRs with spills), and C1 with
+// the next run's streams loaded during this run's sort (0.120 -> 0.163 ms,
+// spills) or copy-out (0.122).
+#ifndef SKE_SEG_D_PIPE
+#define SKE_SEG_D_PIPE 0
 #endif
 __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
     __shared__ uint32_t tot[kSegMaxB1], cbl[kSegMaxB1 + 1];
-    // the chunk's runs' prefix and starts, staged when at most kSegDStage
-    // runs hold it (a chunk of a sparse bucket spanning more reads them in place)
+    // the chunk's runs' prefix and r1 offsets, staged when fewer than
+    // kSegDStage runs hold it (a chunk of a sparse bucket spanning more
+    // reads them in place)
     __shared__ uint32_t spp[kSegDStage + 1], sob[kSegDStage];
     __shared__ uint32_t c2[kSegMaxWpb + 1];
     __shared__ __attribute__((aligned(16))) uint32_t sb[kSegChunk];
     __shared__ uint32_t ws[16];
+    static_assert(kSegDStage == 2 * 1024, "two run-table words per thread");
     const uint32_t tid = threadIdx.x, wpb = 1u << S.wlog;
     // the buckets' chunk bases (every block; block 0 keeps them for E)
     uint32_t t = 0;
@@ -1484,36 +1504,64 @@ __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
     uint32_t *r2 = S.r2 + size_t(S.s) * S.maxch * kSegChunk;
     uint32_t *o2 = S.o2 + size_t(S.s) * S.maxch * (wpb + 1);
     const __amdgpu_buffer_rsrc_t rr1 = part_rsrc(S.r1, S.nruns * kSegRunSw * 4);
-    (void)rr1;
-    for (uint32_t q = blockIdx.x; q < nq; q += gridDim.x) {
-        // (block-uniform: in a scalar register, so the bucket's run-table
-        // words below are scalar loads)
-        const uint32_t h = __builtin_amdgcn_readfirstlane(seg_last_le(cbl, S.nb1, q));  // buckets without chunks share the next one's base
-        const uint32_t c = q - cbl[h], w0 = c * kSegChunk;
-        const uint32_t w1 = tot[h] - w0 < kSegChunk ? tot[h] : w0 + kSegChunk;
-        const uint32_t *pp = S.p1 + size_t(h) * (kSegMaxRuns + 1);
-        const uint32_t *cs = S.cst + size_t(h) * (kSegMaxRuns + 1);
-        const uint32_t ga = cs[c];
-        const uint32_t gb = w1 < tot[h] ? cs[c + 1] + 1 : S.nruns;  // runs [ga, gb) hold [w0, w1)
-        const uint32_t ng = gb - ga;
-        const bool staged = ng < kSegDStage;  // block-uniform
-        const uint32_t *gpp = pp + ga, *gob = S.o1 + size_t(h) * kSegMaxRuns + ga;
-        uint32_t rec[8], pos[8];
-#if SKE_SEG_D == 2
-        // Staged (every chunk but a sparse bucket's): the runs' record
-        // prefix and, per run, the offset that turns a record index into
-        // its word in r1 (run * 8192 + start in run - prefix), in LDS and
-        // read through LDS pointers only; records lane-interleaved (a wave
-        // reads 64 consecutive records per instruction), each lane's run
-        // found by its own binary search, 8 searches side by side.
-        if (staged)
-            for (uint32_t j = tid; j <= ng; j += 1024) {
-                const uint32_t a = gpp[j];
-                spp[j] = a;
-                if (j < ng) sob[j] = (ga + j) * kSegRunSw + gob[j] - a;
+    const __amdgpu_buffer_rsrc_t rp1 = part_rsrc(S.p1, S.nb1 * (kSegMaxRuns + 1) * 4);
+    const __amdgpu_buffer_rsrc_t ro1 = part_rsrc(S.o1, S.nb1 * kSegMaxRuns * 4);
+    // chunk q: bucket h (block-uniform, in a scalar register, so its run
+    // table's chunk starts are scalar loads), records [w0, w1) of the bucket,
+    // held by runs [ga, ga + ng)
+    struct Chunk {
+        uint32_t h, w0, w1, ga, ng;
+    };
+    auto desc = [&](uint32_t q) {
+        Chunk d;
+        d.h = __builtin_amdgcn_readfirstlane(seg_last_le(cbl, S.nb1, q));  // buckets without chunks share the next one's base
+        const uint32_t c = __builtin_amdgcn_readfirstlane(q - cbl[d.h]), th = __builtin_amdgcn_readfirstlane(tot[d.h]);
+        d.w0 = c * kSegChunk;
+        d.w1 = th - d.w0 < kSegChunk ? th : d.w0 + kSegChunk;
+        const uint32_t *cs = S.cst + size_t(d.h) * (kSegMaxRuns + 1);
+        d.ga = cs[c];
+        const uint32_t gb = d.w1 < th ? cs[c + 1] + 1 : S.nruns;
+        d.ng = gb - d.ga;
+        return d;
+    };
+    // a staged chunk's table words j = tid, tid + 1024: prefix (j <= ng) and
+    // start in run (j < ng); always the same four loads (offsets past the
+    // range read nothing), so the wait for the records before them is exact
+    uint32_t ta[2], tb[2];
+    auto tload = [&](const Chunk &d, bool on) {
+#pragma unroll
+        for (uint32_t i = 0; i < 2; i++) {
+            const uint32_t j = tid + i * 1024;
+            const bool st = on && d.ng < kSegDStage;
+            ta[i] = __builtin_amdgcn_raw_buffer_load_b32(
+                rp1, st && j <= d.ng ? (d.h * (kSegMaxRuns + 1) + d.ga + j) * 4 : kOOR, 0, 0);
+            tb[i] = __builtin_amdgcn_raw_buffer_load_b32(
+                ro1, st && j < d.ng ? (d.h * kSegMaxRuns + d.ga + j) * 4 : kOOR, 0, 0);
+        }
+    };
+    uint32_t q = blockIdx.x;
+    Chunk cur{};
+    if (q < nq) {
+        cur = desc(q);
+        tload(cur, true);
+    }
+    while (q < nq) {
+        const bool staged = cur.ng < kSegDStage;  // block-uniform
+        const uint32_t w0 = cur.w0, w1 = cur.w1, ga = cur.ga, ng = cur.ng;
+        if (staged) {
+#pragma unroll
+            for (uint32_t i = 0; i < 2; i++) {
+                const uint32_t j = tid + i * 1024;
+                if (j <= ng) spp[j] = ta[i];
+                if (j < ng) sob[j] = (ga + j) * kSegRunSw + tb[i] - ta[i];
             }
+        }
         if (tid <= wpb) c2[tid] = 0;
         lds_barrier();
+        const uint32_t qn = q + gridDim.x;
+        Chunk nx{};
+        if (SKE_SEG_D_PIPE && qn < nq) nx = desc(qn);
+        uint32_t rec[8], pos[8];
         if (staged) {
             uint32_t k[8];
 #pragma unroll
@@ -1533,8 +1581,10 @@ __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
                 rec[j] = __builtin_amdgcn_raw_buffer_load_b32(rr1, p < w1 ? (sob[k[j]] + p) * 4 : kOOR, 0, 0);
             }
         } else {
-            // (a sparse bucket's chunk over more runs than LDS stages: read
-            // the run tables in place, one search per thread, then a walk)
+            // (a sparse bucket's chunk over more runs than LDS stages: the
+            // run tables read in place, one search per thread, then a walk)
+            const uint32_t *gpp = S.p1 + size_t(cur.h) * (kSegMaxRuns + 1) + ga;
+            const uint32_t *gob = S.o1 + size_t(cur.h) * kSegMaxRuns + ga;
             const uint32_t p0 = w0 + tid * 8;
             uint32_t k = p0 < w1 ? seg_last_le(gpp, ng, p0) : 0u;
 #pragma unroll
@@ -1547,6 +1597,8 @@ __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
                 }
             }
         }
+        // the next chunk's run table, in flight during this chunk's sort
+        if (SKE_SEG_D_PIPE) tload(nx, qn < nq);
 #pragma unroll
         for (uint32_t j = 0; j < 8; j++) {
             pos[j] = 0xffffffffu;
@@ -1556,36 +1608,6 @@ __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
                 pos[j] = (w2 << 16) | atomicAdd(&c2[w2], 1u);
             }
         }
-#else
-        if (staged)
-            for (uint32_t j = tid; j <= ng; j += 1024) {
-                spp[j] = gpp[j];
-                if (j < ng) sob[j] = gob[j];
-            }
-        if (tid <= wpb) c2[tid] = 0;
-        lds_barrier();
-        const uint32_t *vpp = staged ? spp : gpp, *vob = staged ? sob : gob;
-        // 8 consecutive records per thread: one search, then a walk
-        const uint32_t p0 = w0 + tid * 8;
-        uint32_t k = p0 < w1 ? seg_last_le(vpp, ng, p0) : 0u;
-#pragma unroll
-        for (uint32_t j = 0; j < 8; j++) {
-            const uint32_t p = p0 + j;
-            rec[j] = 0;
-            if (p < w1) {
-                while (vpp[k + 1] <= p) k++;
-                rec[j] = S.r1[size_t(ga + k) * kSegRunSw + vob[k] + (p - vpp[k])];
-            }
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < 8; j++) {
-            pos[j] = 0xffffffffu;
-            if (p0 + j < w1) {
-                const uint32_t w2 = (rec[j] >> (kSegRecShift + S.klog)) & (wpb - 1);
-                pos[j] = (w2 << 16) | atomicAdd(&c2[w2], 1u);
-            }
-        }
-#endif
         lds_barrier();
         uint32_t total;
         const uint32_t ex = seg_scan(tid <= wpb ? c2[tid] : 0u, ws, total);
@@ -1601,6 +1623,14 @@ __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
         uint4 *dst = reinterpret_cast<uint4 *>(r2 + size_t(q) * kSegChunk);
         const uint4 *src = reinterpret_cast<const uint4 *>(sb);
         for (uint32_t j = tid; j * 4 < total; j += 1024) dst[j] = src[j];
+        // (the next chunk rewrites spp / sob / c2 only after the barriers
+        // that every reader of this chunk's values has passed)
+        if (!SKE_SEG_D_PIPE && qn < nq) {
+            nx = desc(qn);
+            tload(nx, true);
+        }
+        q = qn;
+        cur = nx;
     }
 }
 
