@@ -67,7 +67,8 @@ RANDOM_SECTOR_GPS = 55.3
 RANDOM_CAS_GPS = 21.1
 MALL_BYTES = 256 << 20  # Infinity Cache: a slab this small stays on chip
 METRIC = "swipes/sec (fused BF.EXISTS+PFADD) at 1/2/4/8 GPUs; % of HBM peak"
-PASS_NAMES = ["k1", "k_part_a", "k_part_b", "k_part_c", "k_seg_d", "k_seg_e"]
+PASS_NAMES = ["k1", "k_part_a", "k_part_b", "k_part_c", "k_seg_d", "k_seg_e", "feed_h2d", "feed_d2h", "feed_call"]
+K1_PASSES = 6  # PASS_NAMES[:6] are K1 kernels; the rest the stages of a host-fed call
 PMC_ROUNDS = ["r05", "r04", "r03", "r02"]  # newest committed PMC summaries first
 VERIFY_KEYS = 64
 # swipes per GPU and step where it differs from the workload's own
@@ -133,9 +134,17 @@ def parse(argv=None):
                          "config's step swipes, each rank's batch the probability mass of the keys "
                          "it owns (the fixed 1B-event stream of north_star, cut per step); "
                          "equal = every rank the config's step swipes over its own keys")
+    ap.add_argument("--ownership", default="hash", choices=["hash", "mass"],
+                    help="N > 1: key owners by MurmurHash64A(key) mod N (north_star's rule, the default) or "
+                         "mass-balanced (distributed.balanced_owners: the key hash's 256 x N virtual buckets "
+                         "assigned to ranks by greedy key mass)")
     ap.add_argument("--rollup", type=int, default=-1,
                     help="1: after the K1 steps, time the rankings / campus PFMERGE over the registers "
                          "(ShardedSketch; default on for --config c5)")
+    ap.add_argument("--stream-1b", type=int, default=1,
+                    help="1: after timing, north_star's 1B-event stream from a zeroed slab: ceil(2^30 / "
+                         "swipes per step of all ranks) steps (8 at N = 1), timed, then replayed with "
+                         "per-pass events (stream_1b; host-launched partitioned K1 only)")
     ap.add_argument("--host-fed", type=int, default=1,
                     help="N = 1: also time one 16M-swipe sample handed over in host memory (PCIe-inclusive, "
                          "pageable / pinned / fixed-width 1-bit answers), reported as host_fed, never value")
@@ -320,24 +329,41 @@ def host_fed(engine, batch, reps=3, cap=1 << 24):
     want = ref.to_host(np.uint8, n)
     ref.free()
 
+    stages = {}
+
     def timed(call):
+        """median wall time of `reps` calls after one untimed call; the
+        calls' stages (HIP events the library records on the streams each
+        stage runs on: H2D copies, the K1 kernels, D2H copies, the whole
+        call) averaged over the timed calls into `stages`"""
         call()
+        engine.set_option("pass_timing", 1)
+        engine.pass_times(reset=True)
         ts = []
         for _ in range(reps):
             t0 = time.perf_counter()
             call()
             ts.append(time.perf_counter() - t0)
+        pt = engine.pass_times(reset=True)
+        engine.set_option("pass_timing", 0)
+        stages.clear()
+        stages.update({"h2d_ms": pt[6][0] / reps, "k1_ms": sum(ms for ms, _ in pt[:6]) / reps,
+                       "d2h_ms": pt[7][0] / reps, "call_ms": pt[8][0] / reps,
+                       "chunks": pt[6][1] // reps, "first_call_excluded": True})
         return float(np.median(ts))
 
     out = {"swipes": n, "what": "ske_swipes(..., SKE_MEM_HOST): H2D of ids + offsets + slots, K1, D2H of the "
-                                "answers, synchronous; median of %d calls" % reps}
+                                "answers, synchronous; median of %d calls; stages: device-side HIP events per "
+                                "stage (h2d: the copies' span on the stream they run on, summed over chunks; "
+                                "k1: the kernels; d2h; call: first enqueued operation to the last), mean of "
+                                "the timed calls" % reps}
 
     def offsets_form(b, o, sl, ans, label):
         t = timed(lambda: engine.ctx.call("ske_swipes", 0, ptr(sl), ptr(b), ptr(o), n, ptr(ans), SKE_MEM_HOST))
         got = ans if isinstance(ans, np.ndarray) else ans.numpy()
         out[label] = {"swipes_per_s": n / t, "ms": t * 1e3,
                       "host_GBps": (b.nbytes + o.nbytes + sl.nbytes + n) / t / 1e9,
-                      "answers_equal": bool(np.array_equal(got, want))}
+                      "answers_equal": bool(np.array_equal(got, want)), "stages": dict(stages)}
 
     offsets_form(buf, offs, slot, np.zeros(n, np.uint8), "pageable")
     pb, po, ps = (torch.from_numpy(x).pin_memory() for x in (buf, offs, slot))
@@ -355,7 +381,7 @@ def host_fed(engine, batch, reps=3, cap=1 << 24):
             out[label] = {"swipes_per_s": n / t, "ms": t * 1e3,
                           "host_GBps": (n * width + 4 * n + (n + 7) // 8) / t / 1e9,
                           "answers_equal": bool(np.array_equal(np.unpackbits(got, count=n, bitorder="little"),
-                                                               want))}
+                                                               want)), "stages": dict(stages)}
     return out
 
 
@@ -373,7 +399,7 @@ def rollup_bench(run, dist, reps=3):
     import torch
     import rtsas_amd
     from rtsas_amd.distributed import ShardedSketch
-    from rtsas_amd.processor import rank_top_bottom
+    from rtsas_amd.processor import rank_top_bottom_dev
     w = run.w_all
     L, D = w.zipf_lectures, w.zipf_days
     world, rank, dev = run.world, run.rank, run.dev
@@ -383,6 +409,7 @@ def rollup_bench(run, dist, reps=3):
     groups = [np.arange(l * D, (l + 1) * D) for l in range(L)]
     plan = sk.plan(km, groups)
     allk = np.arange(len(km))
+    kplan = sk.plan_keys(km, allk)
     scratch = run.sinks[0 if run.args.shard else run.kr] + 1
 
     def barrier():
@@ -404,13 +431,16 @@ def rollup_bench(run, dist, reps=3):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t[0]), out
 
-    t_each, each = timed(lambda: sk.pfcount_each_planned(km, allk))
-    t_groups, lect = timed(lambda: sk.rollup_planned(plan))
-    t_merge, (campus, row) = timed(lambda: sk.pfmerge_planned(km, allk, scratch))
+    # every query device-resident: the plans' slot lists live on the device,
+    # counts stay there, and only the top / bottom-3 (6 keys) reach the host
+    t_each, each_dev = timed(lambda: sk.pfcount_each_planned(kplan))
+    t_rank_each, (ehead, etail) = timed(lambda: rank_top_bottom_dev(each_dev, 3))
+    t_groups, lect_dev = timed(lambda: sk.rollup_planned(plan, device=True))
+    t_merge, (campus, row) = timed(lambda: sk.pfmerge_planned(kplan, scratch))
+    t_rank, (head, tail) = timed(lambda: rank_top_bottom_dev(lect_dev, 3))
     names = [f"LECT{l:05d}" for l in range(L)]
-    t0 = time.perf_counter()
-    head, tail = rank_top_bottom(lect.astype(np.int64), names, 3)
-    t_rank = time.perf_counter() - t0
+    each = each_dev.cpu().numpy().astype(np.uint64)  # (the checks' copies, after timing)
+    lect = lect_dev.cpu().numpy().astype(np.uint64)
     # ---- checks: the oracle's estimator over the device registers
     orc = __import__("__graft_entry__").load_oracle()
     p_, nb = C.c_void_p(), C.c_uint64()
@@ -452,24 +482,94 @@ def rollup_bench(run, dist, reps=3):
         u = torch.maximum(u, slab[a:min(nmine, a + (1 << 16))].amax(0))
     ug = global_max(u.reshape(1, -1))[0]
     ok_m = bool(np.array_equal(ug, row.cpu().numpy()[0])) and orc.hll_count_regs(ug) == campus
-    order = np.lexsort((np.arange(L), -lect.astype(np.int64)))
+    order = np.lexsort((np.arange(L), ~lect))
     ok_r = list(head) == [int(i) for i in order[:3]] and list(tail) == [int(i) for i in order[-3:]]
-    ok = torch.tensor([int(ok_l and ok_e and ok_m and ok_r)], device=cdev)
+    # the lecture-day ranking: key index order is the key names' order (LECT%05d:YYYY-MM-DD)
+    knames = np.asarray(run.names)
+    eorder = np.lexsort((np.arange(len(km)), ~each))
+    ok_re = bool(np.all(knames[:-1] < knames[1:])) and list(ehead) == [int(i) for i in eorder[:3]] and \
+        list(etail) == [int(i) for i in eorder[-3:]]
+    ok = torch.tensor([int(ok_l and ok_e and ok_m and ok_r and ok_re)], device=cdev)
     if world > 1:
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     slab_rank = nmine * 16384
     return {"each_ms": t_each * 1e3, "groups_ms": t_groups * 1e3, "merge_ms": t_merge * 1e3,
-            "rank_ms": t_rank * 1e3, "ok": bool(ok.item()),
+            "rank_ms": t_rank * 1e3, "rank_each_ms": t_rank_each * 1e3, "ok": bool(ok.item()),
             "checks": {"sampled_lecture_unions": bool(ok_l), "sampled_key_counts": ok_e,
-                       "campus_pfmerge": ok_m, "top_bottom_3": ok_r},
+                       "campus_pfmerge": ok_m, "top_bottom_3": ok_r, "top_bottom_3_day_keys": ok_re},
             "keys": len(km), "lectures": L, "days": D, "slab_GB_this_gpu": slab_rank / 1e9,
             "GBps_this_gpu": {"each": slab_rank / t_each / 1e9, "groups": slab_rank / t_groups / 1e9,
                               "merge": slab_rank / t_merge / 1e9},
             "campus_pfcount": campus, "top3": {names[i]: int(lect[i]) for i in head},
             "bottom3": {names[i]: int(lect[i]) for i in tail},
-            "what": "ShardedSketch planned queries over this run's registers; wall time per query, best "
-                    "of %d (host staging of the plan's slot arrays included); checked with the oracle's "
-                    "estimator over device registers" % reps}
+            "top3_day_keys": {run.names[i]: int(each[i]) for i in ehead},
+            "bottom3_day_keys": {run.names[i]: int(each[i]) for i in etail},
+            "what": "ShardedSketch planned queries over this run's registers, device-resident (plans built "
+                    "once on the device, counts kept there, top / bottom-3 by rank_top_bottom_dev: 6 keys "
+                    "reach the host); wall time per query, best of %d; checked with the oracle's estimator "
+                    "over device registers and a full host sort" % reps}
+
+
+def stream_1b(run, n_all, warm_pt, total=1 << 30):
+    """north_star's workload as a whole: the 1B-event stream
+    from a zeroed slab -- ceil(2^30 / n_all) steps of this run's batches
+    (0, 1, ...; 8 steps of 2^27 at N = 1, the whole stream on every rank's
+    share at N > 1), timed like the headline (barrier + synchronize on both
+    sides, max over ranks), then the same cold stream replayed with a HIP
+    event pair around every kernel for the per-pass split.  `warm_pt`: the
+    headline's instrumented replay (steps W..W+K-1 of the stream on a slab
+    warmed by W steps), for the cold-versus-warm comparison per pass."""
+    import torch
+    a, e, dist, world = run.args, run.engine, run.dist, run.world
+    steps = -(-total // n_all)
+
+    def go(instrument):
+        run.zero_slab()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        if instrument:
+            e.set_option("pass_timing", 1)
+            e.pass_times(reset=True)
+        t0 = time.perf_counter()
+        for j in range(steps):
+            run.step(j)
+        if run.ex is not None:
+            run.ex.flush()
+        e.set_stream(run.stream.cuda_stream)
+        torch.cuda.synchronize()
+        run.finish()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        pt = None
+        if instrument:
+            pt = e.pass_times(reset=True)
+            e.set_option("pass_timing", 0)
+        e.check_errors()
+        return el, pt
+
+    el, _ = go(False)
+    if world > 1:
+        cdev = run.dev if a.dist_backend == "nccl" else "cpu"
+        t = torch.tensor([el], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t[0])
+    _, pt = go(True)
+
+    def per_pass(p, nsteps):
+        return {PASS_NAMES[i]: {"ms": ms / c, "launches": c, "ms_per_step": ms / nsteps}
+                for i, (ms, c) in enumerate((p or [])[:K1_PASSES]) if c}
+    cold, warm = per_pass(pt, steps), per_pass(warm_pt, a.steps)
+    return {"swipes": steps * n_all, "steps": steps, "swipes_per_s": steps * n_all / el,
+            "ms_per_step": el * 1e3 / steps, "wall_s": el,
+            "passes": cold, "passes_warm": warm,
+            "cold_minus_warm_ms_per_step": {k: cold[k]["ms_per_step"] - warm[k]["ms_per_step"]
+                                            for k in cold if k in warm},
+            "what": "the first %d swipes of the stream (batches 0..%d) from a zeroed slab, every step's "
+                    "registers raised from cold; passes: per-kernel HIP events of a replay of the same "
+                    "cold stream; passes_warm: the headline's replay (steps %d..%d after %d warm-up "
+                    "steps)" % (steps * n_all, steps - 1, a.warmup, a.warmup + a.steps - 1, a.warmup)}
 
 
 def checked(fn, *a, **k):
@@ -647,7 +747,7 @@ class Run:
         probs = synthetic.key_probs(w_all)
         # --shard N: this process plays one rank (kr) of an N-rank job (kw)
         kw = args.shard if args.shard else world
-        self.km = KeyMap(self.names, kw)
+        self.km = KeyMap(self.names, kw, balance=args.ownership, weights=probs)
         if args.shard:
             masses = [float(probs[self.km.keys_of(r)].sum()) if probs is not None
                       else self.km.keys_of(r).size / len(self.names) for r in range(kw)]
@@ -878,7 +978,7 @@ class Run:
                          slab_bytes=(self.nslots if seg else self.nslots + VERIFY_KEYS) * 16384, cus=cus,
                          seg=seg, nsub=nsub)
         passes = {}
-        for i, (ms, cnt) in enumerate(pt or []):
+        for i, (ms, cnt) in enumerate((pt or [])[:K1_PASSES]):
             if cnt:
                 mean = ms / cnt
                 name = PASS_NAMES[i]
@@ -991,7 +1091,9 @@ class Run:
                  if a.shard else {})
         return {"workload": w.name, **shard, "swipes_per_step": self.n, "students": w.n_members,
                 "hll_keys_total": self.w_all.n_keys, "hll_keys_this_gpu": w.n_keys,
-                "key_ownership": "MurmurHash64A(key name, 0) mod world (distributed.KeyMap)",
+                "key_ownership": ("MurmurHash64A(key name, 0) mod world (distributed.KeyMap)" if a.ownership == "hash"
+                                  else "mass-balanced: MurmurHash64A(key name, 0) mod 256 x world virtual buckets, "
+                                       "assigned by greedy key mass (distributed.balanced_owners)"),
                 "invalid_frac": w.invalid_frac,
                 "bloom": {"error": w.bf_error, "capacity": w.bf_capacity},
                 "id_bytes": self.width, "parallelism": f"dp{self.world} (key-sharded, Bloom replicated)",
@@ -1094,6 +1196,18 @@ def main():
                   "device_mem_used_GB": [r[3] / 1e9 for r in g],
                   "device_mem_note": "hipMemGetInfo used bytes of each rank's device after timing (ranks "
                                      "sharing a GPU in a rehearsal see their sum)"}
+    # each rank's bytes over the inter-GPU links per step: none when input is
+    # routed to the key owners at ingest; with --exchange, the capacity
+    # layout's rows to every peer (id + local slot out, the answer back)
+    if run.ex is not None and world > 1:
+        cap = int(run.ex.stats.get("cap_rows_per_peer", 0))
+        per_rank = cap * (world - 1) * (run.width + 4 + 1)
+        shares["exchange_bytes_per_step"] = [per_rank] * world
+        shares["exchange_what"] = ("rows to every peer (cap_rows_per_peer x (world - 1)) x (id %d B + slot 4 B "
+                                   "out, answer 1 B back), per rank and step" % run.width)
+    else:
+        shares["exchange_bytes_per_step"] = [0] * world
+        shares["exchange_what"] = "input routed to the key owners at ingest: no data-path exchange"
     mean_n = total_swipes / world
     shares.update({"rank_share_max": max(shares["swipes_per_step"]) / mean_n,
                    "rank_share_min": min(shares["swipes_per_step"]) / mean_n,
@@ -1134,6 +1248,8 @@ def main():
         "rank_shares": shares,
     }
     line["config"]["swipes_per_step_all_ranks"] = total_swipes
+    if args.stream_1b and not run.lds_k1 and not run.persistent and run.graph is None and not args.shard:
+        line["stream_1b"] = checked(stream_1b, run, total_swipes, pt)
     if run.ex is not None:
         # cap_rows_per_peer / slack_used: what the timed steps were enqueued
         # with; slack_next: what settle() adapted it to for later batches

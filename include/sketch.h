@@ -331,9 +331,13 @@ int ske_set_option(ske_ctx *ctx, const char *name, int64_t value);
  * [0] single-kernel K1 (LDS / global / XCD-partitioned variants), [1] [2] [3]
  * the partitioned K1's passes A (hash + probe records), B (slice probes),
  * C (answers + register max, or the segmented PFADD's answers + level-1
- * records), [4] the segmented PFADD's level-2 sort, [5] its window apply.
+ * records), [4] the segmented PFADD's level-2 sort, [5] its window apply;
+ * and the stages of a host-fed call (ske_swipes / ske_swipes_fixed_bits with
+ * SKE_MEM_HOST): [6] its host -> device copies (per chunk, on the copy
+ * stream), [7] its device -> host copies of the answers, [8] the whole call
+ * (from its first enqueued operation to the end of its last).
  * reset != 0 zeroes the sums after reading. */
-#define SKE_PASS_KINDS 6
+#define SKE_PASS_KINDS 9
 int ske_pass_times(ske_ctx *ctx, double *ms_out, uint64_t *count_out, int reset);
 
 /* ---- ingest: JSON event decode + key-slot resolution ----

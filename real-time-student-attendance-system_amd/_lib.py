@@ -106,6 +106,7 @@ SIGNATURES = {
     "ske_hll_pfcount_each": (C.c_int, [_CTX, _u32p, C.c_uint32, _u64p, C.c_int]),
     "ske_hll_pfcount_groups": (C.c_int, [_CTX, _u32p, _u32p, C.c_uint32, _u64p, C.c_int]),
     "ske_hll_pfmerge": (C.c_int, [_CTX, C.c_uint32, _u32p, C.c_uint32]),
+    "ske_hll_pfmerge_dev": (C.c_int, [_CTX, C.c_uint32, _vp, C.c_uint32]),
     "ske_hll_histogram": (C.c_int, [_CTX, C.c_uint32, _u32p]),
     "ske_hll_export_raw": (C.c_int, [_CTX, C.c_uint32, _u8p]),
     "ske_hll_export_dense": (C.c_int, [_CTX, C.c_uint32, _u8p]),

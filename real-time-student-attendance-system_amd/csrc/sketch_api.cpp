@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/sketch.h"
@@ -103,6 +104,12 @@ struct ske_ctx {
     void *hook_arg = nullptr;  // launch_swipes_part's pass hook state
     int live_graphs = 0;
     bool capturing = false;
+    // scratch users recorded into the graph being captured (bit 0: xr,
+    // bit 1: rt), and per live graph the users its replays hold: a replay
+    // records only their events, so a graph without routing does not order
+    // the next routing call behind itself
+    unsigned cap_users = 0;
+    std::unordered_map<void *, unsigned> graph_users;
     // pass timing (option "pass_timing"): HIP event pairs around every K1
     // kernel, recorded on the stream the kernel runs on (never inside a
     // capture); ske_pass_times() sums them per pass
@@ -407,6 +414,7 @@ static int scratch_user_begin(ske_ctx *c, unsigned long long *cid_out, ScratchUs
 }
 
 static int scratch_user_end(ske_ctx *c, unsigned long long cid, ScratchUse &u) {
+    if (cid) c->cap_users |= &u == &c->rt ? 2u : 1u;
     u.stream = c->st;
     u.cap = cid;
     u.pending = true;
@@ -1225,22 +1233,30 @@ int ske_swipes(ske_ctx *c, uint32_t fid, const uint32_t *slot, const uint8_t *by
     if (!F) return SKE_EINVAL;
     if (n == 0) return SKE_OK;
     if (const int erc = err_begin(c)) return erc;  // earlier enqueue-only calls' slot errors
+    const bool fed = mem != SKE_MEM_DEVICE;  // pass kinds 6-8: the host-fed call's stages
+    const PassMark mcall = fed ? mark_begin(c, 8) : PassMark();
+    const PassMark mh2d = fed ? mark_begin(c, 6) : PassMark();
     Staged s;
     int rc = stage_items(c, bytes, offs, n, mem, &s);
     if (rc) return rc;
     const uint32_t *dslot;
     rc = stage_u32(c, slot, n, mem, 2, &dslot);
     if (rc) return rc;
+    mark_end(c, mh2d);
     uint8_t *dout = out_valid;
-    if (out_valid && mem != SKE_MEM_DEVICE) {
+    if (out_valid && fed) {
         dout = (uint8_t *)stage_buf(c, 3, n, &rc);
         if (rc) return rc;
     }
     static const ChainDev empty{};
     rc = launch_k1(c, F->exists ? cached_chain(*F) : empty, s.bytes, s.offs, 0, dslot, n, dout);
     if (rc) return rc;
-    if (out_valid && mem != SKE_MEM_DEVICE)
+    if (out_valid && fed) {
+        const PassMark md2h = mark_begin(c, 7);
         HIPCHK(c, hipMemcpyAsync(out_valid, dout, n, hipMemcpyDeviceToHost, c->st));
+        mark_end(c, md2h);
+    }
+    mark_end(c, mcall);
     return check_call_err(c);
 }
 
@@ -1526,6 +1542,7 @@ int ske_swipes_fixed_bits(ske_ctx *c, uint32_t fid, const uint32_t *slot, const 
     }
     // the copy stream starts behind everything already on the context stream
     // (earlier users of the staging buffers)
+    const PassMark mcall = mark_begin(c, 8);  // pass kinds 6-8: this host-fed call's stages
     HIPCHK(c, hipEventRecord(c->chunk_ev[0], c->st));
     HIPCHK(c, hipStreamWaitEvent(c->copy_st, c->chunk_ev[0], 0));
     // once a copy is queued, every exit waits for the copy stream first: the
@@ -1533,20 +1550,25 @@ int ske_swipes_fixed_bits(ske_ctx *c, uint32_t fid, const uint32_t *slot, const 
     auto chunks = [&]() -> int {
         for (uint64_t j = 0; j < nchunks; j++) {
             const uint64_t s0 = j * kFeedChunk, m = n - s0 < kFeedChunk ? n - s0 : kFeedChunk;
+            const PassMark mh2d = mark_begin(c, 6, c->copy_st);
             HIPCHK(c, stage_h2d(c->hs, db + s0 * width, bytes + s0 * width, m * width, c->copy_st, false, nullptr));
             HIPCHK(c, stage_h2d(c->hs, ds + s0, slot + s0, m * 4, c->copy_st, false, nullptr));
+            mark_end(c, mh2d);
             HIPCHK(c, hipEventRecord(c->chunk_ev[j], c->copy_st));
             HIPCHK(c, hipStreamWaitEvent(c->st, c->chunk_ev[j], 0));
             const int r = ske_swipes_fixed_async(c, fid, ds + s0, db + s0 * width, width, m, dans + s0);
             if (r) return r;
             if (out_bits) {
                 HIPCHK(c, launch_pack_bits(dans + s0, m, dbits + s0 / 8, c->cus, c->st));
+                const PassMark md2h = mark_begin(c, 7);
                 HIPCHK(c, hipMemcpyAsync(out_bits + s0 / 8, dbits + s0 / 8, (m + 7) / 8, hipMemcpyDeviceToHost, c->st));
+                mark_end(c, md2h);
             }
         }
         return SKE_OK;
     };
     rc = chunks();
+    mark_end(c, mcall);
     const hipError_t se = hipStreamSynchronize(c->copy_st);
     if (rc) return rc;
     HIPCHK(c, se);
@@ -1986,6 +2008,7 @@ int ske_capture_begin(ske_ctx *c) {
     if (!c) return SKE_EINVAL;
     HIPCHK(c, hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
     c->capturing = true;
+    c->cap_users = 0;
     scratch_set_recording(c->scratch, true);
     return SKE_OK;
 }
@@ -2017,6 +2040,7 @@ int ske_capture_end(ske_ctx *c, void **graph_out) {
         return SKE_EHIP;
     }
     *graph_out = ge;
+    c->graph_users[(void *)ge] = c->cap_users;
     c->live_graphs++;  // the slots it pinned stay pinned until every graph is freed
     return SKE_OK;
 }
@@ -2032,12 +2056,15 @@ int ske_graph_launch(ske_ctx *c, void *graph) {
             if (covered) HIPCHK(c, hipStreamWaitEvent(c->st, u->done, 0));
         }
     HIPCHK(c, hipGraphLaunch(hipGraphExec_t(graph), c->st));
-    // a replay may hold scratch users (the partitioned / XCD-partitioned K1):
-    // a later direct launch on another stream waits for it.  Two replays of
-    // graphs holding scratch users on different streams are not ordered by
-    // this; replay such graphs on one stream.
+    // a replay may hold scratch users (the partitioned / XCD-partitioned K1,
+    // routing): a later direct launch on another stream waits for it.  Only
+    // the users the graph recorded are marked (a graph of unknown origin:
+    // both).  Two replays of graphs holding scratch users on different
+    // streams are not ordered by this; replay such graphs on one stream.
+    const auto gu = c->graph_users.find(graph);
+    const unsigned users = gu == c->graph_users.end() ? 3u : gu->second;
     for (ScratchUse *u : {&c->xr, &c->rt})
-        if (u->done) {
+        if (u->done && (users & (u == &c->rt ? 2u : 1u))) {
             HIPCHK(c, hipEventRecord(u->done, c->st));
             u->stream = c->st;
             u->cap = 0;
@@ -2050,6 +2077,7 @@ int ske_graph_free(ske_ctx *c, void *graph) {
     if (!c) return SKE_EINVAL;
     if (graph) {
         HIPCHK(c, hipGraphExecDestroy(hipGraphExec_t(graph)));
+        c->graph_users.erase(graph);
         if (c->live_graphs > 0) c->live_graphs--;
         if (c->live_graphs == 0 && !c->capturing) scratch_unpin(c->scratch);
     }

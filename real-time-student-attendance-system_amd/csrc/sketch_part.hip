@@ -2191,9 +2191,12 @@ static bool seg_plan(uint32_t nslots, uint64_t n, uint32_t sub, const SegOpts &s
 static bool seg_use(const PartArgs &A, const SegOpts &so, uint32_t nslots, uint64_t n, uint32_t sub, SegPlan *P) {
     if (so.mode == 0 || !part_flist(A) || !seg_plan(nslots, n, sub, so, P)) return false;
     if (so.mode == 1) return true;
-    // break-evens measured at C3 (DESIGN.md §3): ~5 swipes per line over a
-    // 1.6 GB slab, ~12 over a 205 MB one that the 256 MiB Infinity Cache holds
-    const uint64_t thr = uint64_t(so.density_x100) * ((uint64_t(nslots) << kHllP) <= (192ull << 20) ? 2 : 1);
+    // break-evens measured at C3 (DESIGN.md §3a): ~5 swipes per line over a
+    // 1.6 GB slab, ~12 over the 8-way shard's 205 MB one, which the 256 MiB
+    // Infinity Cache holds (pass C's random requests are served there): the
+    // threshold doubles for a slab of at most 256 MiB, so the shard's 16 M
+    // step (~11 per line) takes pass C and its 2^27 step (~92) this form
+    const uint64_t thr = uint64_t(so.density_x100) * ((uint64_t(nslots) << kHllP) <= (256ull << 20) ? 2 : 1);
     return n * 100 >= thr * nslots * (kHllRegs / 128);
 }
 

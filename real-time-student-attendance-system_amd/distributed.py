@@ -64,18 +64,54 @@ def route(keys: Sequence, world: int) -> np.ndarray:
     return (murmur64a_many([encode(k) for k in keys], 0) % np.uint64(world)).astype(np.int32)
 
 
+def balanced_owners(names: Sequence, world: int, weights=None, vbuckets: int | None = None) -> np.ndarray:
+    """Mass-balanced ownership (an option beside north_star's hash rule):
+    every key hashes to one of `vbuckets` virtual buckets (MurmurHash64A(key
+    name, 0) mod V, default V = 256 x world), and the buckets go to ranks by
+    greedy key mass -- heaviest bucket first, each to the rank with the least
+    mass so far (ties: lower bucket, lower rank).  `weights`: each key's share
+    of the stream (default 1 per key).  Deterministic, so every rank derives
+    the same owners from the same names and weights.  Returns owner per key."""
+    names = [encode(n) for n in names]
+    V = int(vbuckets or 256 * world)
+    vb = (murmur64a_many(names, 0) % np.uint64(V)).astype(np.int64) if names else np.zeros(0, np.int64)
+    w = np.ones(len(names)) if weights is None else np.asarray(weights, np.float64)
+    mass = np.bincount(vb, weights=w, minlength=V)
+    order = np.lexsort((np.arange(V), -mass))
+    load = np.zeros(world)
+    assign = np.zeros(V, np.uint32)
+    for b in order:
+        r = int(np.argmin(load))  # the least-loaded rank (argmin: the lowest on ties)
+        assign[b] = r
+        load[r] += mass[b]
+    return assign[vb]
+
+
 class KeyMap:
     """The key namespace of a multi-GPU job.
 
     ``names[g]`` is global key ``g``; ``owner[g]`` = owner(names[g], world);
     ``local[g]`` = base(owner) + the position of g among the keys of that
     owner (increasing g).  ``base`` is an int or one int per rank (slots a
-    rank keeps below the universe, e.g. another universe bound first)."""
+    rank keeps below the universe, e.g. another universe bound first).
+    ``balance="mass"``: owners from balanced_owners(names, world, weights)
+    instead of the hash rule (Zipf-skewed lecture popularity leaves the
+    hash rule's heaviest rank ~10 % above the mean at 8 ranks, which bounds
+    weak scaling; every path below reads ``owner`` from the map, so both
+    rules serve ingest routing, the exchange and the planned queries alike;
+    the name-based ShardedSketch queries take the map as ``keymap``)."""
 
-    def __init__(self, names: Sequence, world: int, base=0):
+    def __init__(self, names: Sequence, world: int, base=0, balance: str = "hash", weights=None,
+                 vbuckets: int | None = None):
         self.names = [encode(n) for n in names]
         self.world = int(world)
-        self.owner = route(self.names, world).astype(np.uint32)
+        self.balance = balance
+        if balance == "hash":
+            self.owner = route(self.names, world).astype(np.uint32)
+        elif balance == "mass":
+            self.owner = balanced_owners(self.names, world, weights, vbuckets).astype(np.uint32)
+        else:
+            raise ValueError(f"unknown ownership rule {balance!r}")
         bases = [int(base)] * self.world if np.isscalar(base) else [int(b) for b in base]
         assert len(bases) == self.world
         self.base = bases
@@ -91,6 +127,16 @@ class KeyMap:
 
     def __len__(self):
         return len(self.names)
+
+    def owner_of(self, keys: Sequence) -> np.ndarray:
+        """owner of each key name (names outside the universe: the hash rule)."""
+        if not hasattr(self, "_index"):
+            self._index = {n: g for g, n in enumerate(self.names)}
+        out = np.empty(len(keys), np.int32)
+        for i, k in enumerate(keys):
+            g = self._index.get(encode(k))
+            out[i] = self.owner[g] if g is not None else owner(k, self.world)
+        return out
 
     def keys_of(self, rank: int) -> np.ndarray:
         """Global indices of the keys `rank` owns (increasing = local slot order)."""
@@ -177,9 +223,10 @@ class LibsketchOps:
 class ShardedSketch:
     """Name-based queries over keys spread by owner() across the ranks."""
 
-    def __init__(self, client, rank: int, world: int, group=None, ops=None):
+    def __init__(self, client, rank: int, world: int, group=None, ops=None, keymap: KeyMap | None = None):
         import torch.distributed as dist
         self.dist = dist
+        self.keymap = keymap  # a balanced ownership's map (None: the hash rule)
         self.client = client
         self.rank, self.world, self.group = rank, world, group
         self.ops = ops if ops is not None else LibsketchOps(client)
@@ -191,10 +238,12 @@ class ShardedSketch:
         keys = list(keys)
         if not keys:
             return np.zeros(0, bool)
+        if self.keymap is not None:
+            return self.keymap.owner_of(keys) == self.rank
         return route(keys, self.world) == self.rank
 
     def owns(self, key) -> bool:
-        return owner(key, self.world) == self.rank
+        return bool(self._owned([key])[0])
 
     def _max(self):
         return self.dist.ReduceOp.MAX
@@ -260,9 +309,13 @@ class ShardedSketch:
 
 
     # ---- planned queries: keys named by their global index in a KeyMap,
-    # the name -> slot resolution done once (plan), the query itself only
-    # device work and one collective (C5's rankings,
-    # attendance_analysis.py:87-97 in PFCOUNT form, and the campus PFMERGE)
+    # the name -> slot resolution done once (plan / plan_keys, kept on the
+    # device), the query itself only device work and one collective
+    # (C5's rankings, attendance_analysis.py:87-97 in PFCOUNT
+    # form, and the campus PFMERGE).  Every library call is preceded by a
+    # torch synchronisation: torch's stream and the context's stream are
+    # different streams, and the plan's tensors, the output tensors and the
+    # registers K1 wrote may still be in flight on either.
     def plan(self, keymap: KeyMap, groups: Sequence) -> dict:
         """This rank's part of every group of global key indices: the local
         slots of the keys it owns, groups padded to a multiple of world (the
@@ -280,24 +333,48 @@ class ShardedSketch:
         goffs += [goffs[-1]] * (per * self.world - G)
         slots = np.concatenate(parts) if parts else np.zeros(0, np.uint32)
         dev = self.ops.device
-        return {"G": G, "per": per, "slots": slots, "goffs": np.asarray(goffs, np.uint32),
-                "slots_dev": torch.from_numpy(slots.view(np.int32) if slots.size else np.zeros(1, np.int32)).to(dev),
-                "goffs_dev": torch.from_numpy(np.asarray(goffs, np.uint32).view(np.int32)).to(dev)}
+        p = {"G": G, "per": per, "slots": slots, "goffs": np.asarray(goffs, np.uint32),
+             "slots_dev": torch.from_numpy(slots.view(np.int32) if slots.size else np.zeros(1, np.int32)).to(dev),
+             "goffs_dev": torch.from_numpy(np.asarray(goffs, np.uint32).view(np.int32)).to(dev)}
+        self.torch_sync()
+        return p
 
-    def rollup_planned(self, plan: dict) -> np.ndarray:
+    def plan_keys(self, keymap: KeyMap, gidx) -> dict:
+        """The plan of a key list (global indices) for pfcount_each_planned /
+        pfmerge_planned: the positions of the keys this rank owns and their
+        local slots, built once and kept on the device (the owner test and
+        the slot lookup are not redone per query, and no slot list crosses
+        the host link per query)."""
+        import torch
+        gidx = np.asarray(gidx, np.int64)
+        pos = np.nonzero(keymap.owner[gidx] == self.rank)[0] if gidx.size else np.zeros(0, np.int64)
+        slots = np.ascontiguousarray(keymap.local[gidx[pos]].astype(np.uint32))
+        dev = self.ops.device
+        ident = pos.size == gidx.size  # every key is this rank's (world 1): counts land in place
+        kp = {"n": int(gidx.size), "mine": int(pos.size), "ident": ident,
+              "slots_dev": torch.from_numpy(slots.view(np.int32) if slots.size else np.zeros(1, np.int32)).to(dev),
+              "pos_dev": None if ident else torch.from_numpy(pos.astype(np.int64)).to(dev)}
+        self.torch_sync()
+        return kp
+
+    def rollup_planned(self, plan: dict, device: bool = False):
         """rollup() of a plan: one union count per group.  One rank: the
         fused per-group K2 (merge + estimator, device arrays); N ranks: K3
         per group into a [groups, 16384] tensor, reduce_scatter MAX (RCCL),
-        K2 estimator on this rank's share, all_gather of the counts."""
+        K2 estimator on this rank's share, all_gather of the counts.
+        device=True: the counts stay on the device (an int64 tensor holding
+        the u64 values), e.g. for rank_top_bottom_dev."""
         import torch
         G, per = plan["G"], plan["per"]
+        dev = self.ops.device
         if self.solo:
-            out = torch.zeros(max(1, G), dtype=torch.int64, device=self.ops.device)
+            out = torch.empty(max(1, G), dtype=torch.int64, device=dev)
             if G:
+                self.torch_sync()
                 self.client.ctx.call("ske_hll_pfcount_groups", C.c_void_p(plan["slots_dev"].data_ptr()),
                                      C.c_void_p(plan["goffs_dev"].data_ptr()), G, C.c_void_p(out.data_ptr()), 1)
-            return out[:G].cpu().numpy().astype(np.uint64)
-        t = torch.zeros((per * self.world, HLL_REGISTERS), dtype=torch.uint8, device=self.ops.device)
+            return out[:G] if device else out[:G].cpu().numpy().astype(np.uint64)
+        t = torch.zeros((per * self.world, HLL_REGISTERS), dtype=torch.uint8, device=dev)
         if per:
             self.torch_sync()
             self.client.ctx.call("ske_hll_merge_groups_dev", plan["slots"].ctypes.data_as(C.c_void_p),
@@ -314,39 +391,50 @@ class ShardedSketch:
             local = local.to(t.device)
         gathered = [torch.zeros_like(local) for _ in range(self.world)]
         self.dist.all_gather(gathered, local, group=self.group)
+        if device:
+            return torch.cat([g.to(dev) for g in gathered])[:G]
         return torch.cat([g.cpu() for g in gathered]).numpy()[:G].astype(np.uint64)
 
-    def pfcount_each_planned(self, keymap: KeyMap, gidx: np.ndarray) -> np.ndarray:
-        """PFCOUNT of every key of gidx (global indices): each rank counts its
-        own keys (K2 per key, device arrays), all_reduce SUM of the counts."""
+    def pfcount_each_planned(self, kp, gidx=None):
+        """PFCOUNT of every key of a plan_keys() plan (or of a KeyMap and
+        global indices, planned on the spot), as a device int64 tensor
+        holding the u64 counts: each rank counts its own keys (K2 per key,
+        device slot list, the counts written in place at world 1 or
+        scattered to their positions), then all_reduce SUM of the counts."""
         import torch
-        gidx = np.asarray(gidx, np.int64)
-        mine = np.nonzero(keymap.owner[gidx] == self.rank)[0]
+        if isinstance(kp, KeyMap):
+            kp = self.plan_keys(kp, gidx)
+        n, mine = kp["n"], kp["mine"]
         dev = self.ops.device
-        counts = torch.zeros(max(1, gidx.size), dtype=torch.int64, device=dev)
-        if mine.size:
-            sl = torch.from_numpy(keymap.local[gidx[mine]].astype(np.uint32).view(np.int32)).to(dev)
-            out = torch.zeros(mine.size, dtype=torch.int64, device=dev)
-            self.client.ctx.call("ske_hll_pfcount_each", C.c_void_p(sl.data_ptr()), int(mine.size),
+        if kp["ident"]:
+            counts = out = torch.empty(max(1, n), dtype=torch.int64, device=dev)
+        else:
+            counts = torch.zeros(max(1, n), dtype=torch.int64, device=dev)
+            out = torch.empty(max(1, mine), dtype=torch.int64, device=dev)
+        if mine:
+            self.torch_sync()
+            self.client.ctx.call("ske_hll_pfcount_each", C.c_void_p(kp["slots_dev"].data_ptr()), mine,
                                  C.c_void_p(out.data_ptr()), 1)
-            counts[torch.from_numpy(mine).to(dev)] = out
+            if not kp["ident"]:
+                counts[kp["pos_dev"]] = out[:mine]
         if not self.solo:
             self._all_reduce_sum(counts)
-        return counts[:gidx.size].cpu().numpy().astype(np.uint64)
+        return counts[:n]
 
-    def pfmerge_planned(self, keymap: KeyMap, gidx: np.ndarray, scratch_slot: int) -> tuple:
-        """The campus PFMERGE of every key of gidx: each rank merges its own
-        keys into `scratch_slot` (cleared first; the two-level K3), the
-        16 KiB rows are max-reduced (all_reduce MAX) and counted.  Returns
-        (PFCOUNT of the union, the union's registers as a uint8 tensor)."""
+    def pfmerge_planned(self, kp, scratch_slot: int, gidx=None) -> tuple:
+        """The campus PFMERGE of every key of a plan_keys() plan: each rank
+        merges its own keys into `scratch_slot` (cleared first; the two-level
+        K3 over the plan's device slot list, ske_hll_pfmerge_dev), the 16 KiB
+        rows are max-reduced (all_reduce MAX) and counted.  Returns (PFCOUNT
+        of the union, the union's registers as a uint8 tensor)."""
         import torch
-        gidx = np.asarray(gidx, np.int64)
-        mine = gidx[keymap.owner[gidx] == self.rank]
-        src = np.ascontiguousarray(keymap.local[mine].astype(np.uint32))
+        if isinstance(kp, KeyMap):
+            kp = self.plan_keys(kp, gidx)
         ctx = self.client.ctx
         ctx.call("ske_hll_clear", int(scratch_slot))
-        if src.size:
-            ctx.call("ske_hll_pfmerge", int(scratch_slot), src.ctypes.data_as(C.c_void_p), int(src.size))
+        if kp["mine"]:
+            self.torch_sync()
+            ctx.call("ske_hll_pfmerge_dev", int(scratch_slot), C.c_void_p(kp["slots_dev"].data_ptr()), kp["mine"])
         p, nb = C.c_void_p(), C.c_uint64()
         ctx.call("ske_hll_slab", C.byref(p), C.byref(nb))
         row = torch.empty((1, HLL_REGISTERS), dtype=torch.uint8, device=self.ops.device)

@@ -15,7 +15,7 @@ import numpy as np
 from ._lib import Context, GenParams, SKE_MEM_DEVICE
 from . import synthetic
 
-PASS_KINDS = 6  # SKE_PASS_KINDS (include/sketch.h)
+PASS_KINDS = 9  # SKE_PASS_KINDS (include/sketch.h)
 
 
 class DeviceBuffer:
@@ -222,7 +222,8 @@ class SketchEngine:
         """(summed ms, kernel count) per K1 pass kind, from the HIP event
         pairs the library records around each kernel while the option
         "pass_timing" is on: [single-kernel K1, partitioned A, B, C (or the
-        segmented C1), segmented level-2 sort, segmented window apply]."""
+        segmented C1), segmented level-2 sort, segmented window apply, and a
+        host-fed call's H2D copies, D2H copies, whole call]."""
         ms = (C.c_double * PASS_KINDS)()
         cnt = (C.c_uint64 * PASS_KINDS)()
         self.ctx.call("ske_pass_times", ms, cnt, 1 if reset else 0)

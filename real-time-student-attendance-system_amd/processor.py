@@ -171,16 +171,50 @@ def rank_top_bottom(counts: np.ndarray, keys: Sequence[str], k: int) -> tuple[li
     k = min(max(int(k), 0), n)
     if k == 0:
         return [], []
-    c = np.asarray(counts, dtype=np.int64)
+    # counts compare as unsigned: PFCOUNT replies are u64, and a saturated
+    # key's (2^63, Redis' llroundl(inf)) is the largest even when the caller
+    # holds it in an int64 array
+    c = np.ascontiguousarray(np.asarray(counts).astype(np.int64)).view(np.uint64)
     karr = np.asarray(keys)
 
     def ordered(idx):
-        return idx[np.lexsort((karr[idx], -c[idx]))]
+        return idx[np.lexsort((karr[idx], ~c[idx]))]
 
     hi = np.partition(c, n - k)[n - k]      # k-th largest count
     head = ordered(np.nonzero(c >= hi)[0])[:k]
     lo = np.partition(c, k - 1)[k - 1]      # k-th smallest count
     tail = ordered(np.nonzero(c <= lo)[0])[-k:]
+    return head.tolist(), tail.tolist()
+
+
+def rank_top_bottom_dev(counts, k: int, key_rank=None) -> tuple[list, list]:
+    """rank_top_bottom over a torch tensor of PFCOUNTs (int64 holding the u64
+    replies; device or CPU) without moving the counts: the k-th largest and
+    k-th smallest counts come from ``torch.topk`` on the tensor, and only the
+    keys tied with or beyond them (normally k each) are copied to the host
+    and ordered there.  Order: count descending, then key ascending, where a
+    key's place in the key order is ``key_rank[i]`` (a tensor, or None when
+    the keys are already in ascending order by index, as C5's
+    ``LECT%05d`` / day-key universes are).  Counts compare as unsigned, so a
+    saturated key's PFCOUNT (2^63, Redis' llroundl(inf)) stays the largest.
+    Returns (head, tail) as rank_top_bottom does."""
+    import torch
+    n = int(counts.numel())
+    k = min(max(int(k), 0), n)
+    if k == 0:
+        return [], []
+    u = counts.view(torch.int64) ^ torch.iinfo(torch.int64).min  # unsigned order as signed order
+    hi = torch.topk(u, k, largest=True, sorted=True).values[-1]
+    lo = torch.topk(u, k, largest=False, sorted=True).values[-1]
+
+    def ordered(mask):
+        idx = torch.nonzero(mask).flatten()
+        c = counts.view(torch.int64)[idx].cpu().numpy().view(np.uint64)
+        key = (key_rank[idx] if key_rank is not None else idx).cpu().numpy()
+        return idx.cpu().numpy()[np.lexsort((key, ~c))]  # ~c: descending unsigned counts
+
+    head = ordered(u >= hi)[:k]
+    tail = ordered(u <= lo)[-k:]
     return head.tolist(), tail.tolist()
 
 

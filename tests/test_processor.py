@@ -258,6 +258,28 @@ def test_rank_top_bottom_matches_full_sort(pkg):
         assert tail == (order[-kk:] if kk else [])
 
 
+def test_rank_top_bottom_dev_matches_host(pkg):
+    """rank_top_bottom_dev (torch.topk on the counts, only the tie sets moved
+    to the host) == rank_top_bottom, keys in index order or ranked by a key
+    order tensor; the saturated PFCOUNT 2^63 (held as int64: negative) sorts
+    as the largest in both."""
+    import torch
+    from rtsas_amd.processor import rank_top_bottom, rank_top_bottom_dev
+    rng = np.random.default_rng(5)
+    for n, distinct, k in [(1, 1, 3), (7, 2, 3), (300, 3, 3), (20000, 50, 3), (64, 64, 70), (9, 4, 0)]:
+        counts = rng.integers(0, distinct, n).astype(np.int64)
+        if n > 5:
+            counts[[1, 4]] = np.uint64(1 << 63).astype(np.int64)  # two saturated keys
+        names = [f"LECT{i:05d}" for i in range(n)]
+        assert rank_top_bottom_dev(torch.from_numpy(counts), k) == rank_top_bottom(counts, names, k)
+        perm = rng.permutation(n)  # key i is the perm[i]-th name in ascending order
+        pnames = [f"K{int(p):06d}" for p in perm]
+        got = rank_top_bottom_dev(torch.from_numpy(counts), k, key_rank=torch.from_numpy(perm))
+        assert got == rank_top_bottom(counts, pnames, k)
+        if n > 5 and k:
+            assert got[0][:2] == sorted([1, 4], key=lambda i: pnames[i])
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("row_types", [True, False])
 def test_process_batch_nacks_per_message_on_device(pkg, orc, row_types):

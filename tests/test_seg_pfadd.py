@@ -12,9 +12,11 @@ Zipf-skewed keys, windows of 4 and 8 keys, every window staged in LDS
 (seg_dense_min 0), none staged (raised in place), the default mix; several
 sub-batches feeding one window pass (part_sub); key counts that are not a
 multiple of the window; an out-of-range slot (error channel); ragged ids of
-0..40 bytes; the auto choice (on at the 8-way shard's density, off at the
-N = 1 default); graph capture; and C3 at the bench's sizes in
-test_full_size.py (the 8-way shard auto-selects this form).
+0..40 bytes; the auto choice (a 1.6 MB slab at its threshold, and the
+8-way shard's 12 500 keys: pass C at a 16 M-swipe batch, this form at the
+2^27 step); graph capture; and C3 at the bench's sizes in test_full_size.py
+(the N = 1 default step and the 8-way shard's 2^27 step auto-select this
+form).
 """
 import numpy as np
 import pytest
@@ -214,6 +216,36 @@ def test_seg_auto_choice(engine):
     engine.set_option("hll_seg", 1)
     assert seg_used(1000)
     engine.set_option("pass_timing", 0)
+
+
+def test_seg_auto_choice_shard(engine):
+    """The auto choice where it matters: the 8-way shard's slab (12 500 keys,
+    204.8 MB, inside the 256 MiB Infinity Cache: 12 swipes per line, i.e.
+    19.2 M swipes) keeps pass C for a 16 M-swipe batch (the shard's round-4
+    step, where pass C measured faster) and takes the segmented form at the
+    bench's 2^27 step; the threshold sits exactly at 12 swipes per line."""
+    w, p = _c3(engine, n_members=100_000, lectures=125, days=100)   # 12 500 keys
+    out = DeviceBuffer_of(engine, 1 << 27)
+    engine.set_option("pass_timing", 1)
+    engine.set_option("hll_seg", -1)
+    engine.set_option("seg_density", 600)
+
+    def seg_used(n):
+        engine.pass_times(reset=True)
+        engine.swipes(0, engine.swipe_batch(p, 0, n), out)
+        pt = engine.pass_times(reset=True)
+        assert pt[3][1] > 0
+        return pt[5][1] > 0
+
+    assert not seg_used(1 << 24)
+    assert not seg_used(19_100_000) and seg_used(19_300_000)
+    assert seg_used(1 << 27)
+    engine.set_option("pass_timing", 0)
+
+
+def DeviceBuffer_of(engine, n):
+    from rtsas_amd.engine import DeviceBuffer
+    return DeviceBuffer(engine.ctx, n)
 
 
 def test_seg_graph_replay(engine, orc):
