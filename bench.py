@@ -301,7 +301,7 @@ def cpu_baseline(orc, chain, w, b0, seconds, key_name):
                                            "(attendance_processor.py:100-137 without transport)"}}
 
 
-def host_fed(engine, batch, reps=3, cap=1 << 24):
+def host_fed(engine, batch, reps=5, cap=1 << 24):
     """SURVEY §7 item 8 / DESIGN §4: the PCIe-inclusive rate -- the same
     swipes handed over in HOST memory (the reference's loop is fed from the
     host, attendance_processor.py:101-113): ske_swipes(..., SKE_MEM_HOST)
@@ -332,31 +332,37 @@ def host_fed(engine, batch, reps=3, cap=1 << 24):
     stages = {}
 
     def timed(call):
-        """median wall time of `reps` calls after one untimed call; the
-        calls' stages (HIP events the library records on the streams each
-        stage runs on: H2D copies, the K1 kernels, D2H copies, the whole
-        call) averaged over the timed calls into `stages`"""
-        call()
+        """median wall time of `reps` calls after one untimed call, and per
+        call its stages: the HIP events the library records on the streams
+        each stage runs on (H2D copies, the K1 kernels, D2H copies, the whole
+        call), so that a slow call shows which stage was slow; `stages`
+        holds the median call's and the slowest call's"""
+        # the untimed call runs with the events on too, so the library's event
+        # pool is filled before timing (creating ~60 events inside the first
+        # timed call had made it look 2.4x slower in its H2D stage)
         engine.set_option("pass_timing", 1)
+        call()
         engine.pass_times(reset=True)
-        ts = []
+        ts, per = [], []
         for _ in range(reps):
             t0 = time.perf_counter()
             call()
             ts.append(time.perf_counter() - t0)
-        pt = engine.pass_times(reset=True)
+            pt = engine.pass_times(reset=True)
+            per.append({"wall_ms": ts[-1] * 1e3, "h2d_ms": pt[6][0], "k1_ms": sum(ms for ms, _ in pt[:6]),
+                        "d2h_ms": pt[7][0], "call_ms": pt[8][0], "chunks": pt[6][1]})
         engine.set_option("pass_timing", 0)
+        order = np.argsort(ts)
         stages.clear()
-        stages.update({"h2d_ms": pt[6][0] / reps, "k1_ms": sum(ms for ms, _ in pt[:6]) / reps,
-                       "d2h_ms": pt[7][0] / reps, "call_ms": pt[8][0] / reps,
-                       "chunks": pt[6][1] // reps, "first_call_excluded": True})
+        stages.update({"median_call": per[int(order[len(ts) // 2])], "slowest_call": per[int(order[-1])],
+                       "wall_ms_all": [round(t * 1e3, 3) for t in ts]})
         return float(np.median(ts))
 
     out = {"swipes": n, "what": "ske_swipes(..., SKE_MEM_HOST): H2D of ids + offsets + slots, K1, D2H of the "
                                 "answers, synchronous; median of %d calls; stages: device-side HIP events per "
                                 "stage (h2d: the copies' span on the stream they run on, summed over chunks; "
-                                "k1: the kernels; d2h; call: first enqueued operation to the last), mean of "
-                                "the timed calls" % reps}
+                                "k1: the kernels; d2h; call: first enqueued operation to the last) of the "
+                                "median and the slowest call" % reps}
 
     def offsets_form(b, o, sl, ans, label):
         t = timed(lambda: engine.ctx.call("ske_swipes", 0, ptr(sl), ptr(b), ptr(o), n, ptr(ans), SKE_MEM_HOST))
