@@ -1334,13 +1334,26 @@ __device__ __forceinline__ uint32_t seg_last_le(const uint32_t *a, uint32_t n, u
     return lo;
 }
 
-__global__ void __launch_bounds__(1024, 8) k_seg_c1(const PartArgs A, const SegArgs S) {
+// C1's block: T threads, U = 8192 / T swipes of a run each (1024 x 8 at two
+// blocks per CU, or 512 x 16 at three: three runs in flight per CU)
+#ifndef SKE_SEG_C1T
+#define SKE_SEG_C1T 512
+#endif
+template <uint32_t T> struct SegC1 {
+    static constexpr uint32_t U = kSegRunSw / T;       // swipes per thread per run
+    static constexpr uint32_t PT = 1024 / T;           // swipes per thread per tile
+    static constexpr uint32_t BPC = T == 1024 ? 2 : 3;  // blocks per CU
+    static constexpr uint32_t WPE = BPC * (T / 64) / 4;
+};
+template <uint32_t T>
+__global__ void __launch_bounds__(T, SegC1<T>::WPE) k_seg_c1(const PartArgs A, const SegArgs S) {
+    constexpr uint32_t U = SegC1<T>::U, PT = SegC1<T>::PT;
     __shared__ uint16_t mark[kSegRunSw];
     __shared__ __attribute__((aligned(16))) uint32_t srec[kSegRunSw];
     __shared__ uint32_t cnt[kSegMaxB1 + 1];
-    __shared__ uint32_t ws[16];
+    __shared__ uint32_t ws[T / 64];
     const uint32_t tid = threadIdx.x;
-    for (uint32_t j = tid; j < kSegRunSw; j += 1024) mark[j] = 0;
+    for (uint32_t j = tid; j < kSegRunSw; j += T) mark[j] = 0;
     const uint32_t npieces = A.nunits * kSegRunTiles;  // 16-B lists of one run
     const __amdgpu_buffer_rsrc_t rfl = part_rsrc(A.flist, A.nunits * A.fl_stride * kPbLanes * 2);
     const uint32_t kmask = (1u << S.klog) - 1, bmask = S.nb1 - 1;
@@ -1351,22 +1364,22 @@ __global__ void __launch_bounds__(1024, 8) k_seg_c1(const PartArgs A, const SegA
         const uint16_t ep = uint16_t(r + 1);  // <= kSegMaxRuns (8192) < 2^16: marks are never cleared
         // the run's streams, every tile's in flight together (the HLL
         // word's top byte is pass B's overflow flag)
-        uint32_t sl[kSegRunTiles], hv[kSegRunTiles];
+        uint32_t sl[U], hv[U];
 #pragma unroll
-        for (uint32_t u = 0; u < kSegRunTiles; u++) {
-            const uint32_t i = (t0 + u) * 1024 + tid;
-            const bool act = t0 + u < t1 && i < A.n;
+        for (uint32_t u = 0; u < U; u++) {  // swipe u: tile u / PT, its (u % PT)-th T-thread slice
+            const uint32_t i = (t0 + u / PT) * 1024 + (u % PT) * T + tid;
+            const bool act = t0 + u / PT < t1 && i < A.n;
             sl[u] = act ? nt_ld<16>(A.slot + i) : 0u;
             hv[u] = act ? nt_ld<16>(A.hllw + i) : 0xff000000u;
         }
-        if (tid <= S.nb1) cnt[tid] = 0;
+        for (uint32_t j = tid; j <= S.nb1; j += T) cnt[j] = 0;
         // the run's fail lists -> marks (piece p = unit p / 8, tile t0 + p % 8)
-        for (uint32_t p0 = 0; p0 < npieces; p0 += 4 * 1024) {
+        for (uint32_t p0 = 0; p0 < npieces; p0 += 4 * T) {
             part_u32x4 e[4];
             bool ok[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const uint32_t p = p0 + uint32_t(j) * 1024 + tid;
+                const uint32_t p = p0 + uint32_t(j) * T + tid;
                 const uint32_t un = p / kSegRunTiles, tt = t0 + p % kSegRunTiles;
                 ok[j] = p < npieces && tt < t1;
                 e[j] = __builtin_bit_cast(part_u32x4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -1374,7 +1387,7 @@ __global__ void __launch_bounds__(1024, 8) k_seg_c1(const PartArgs A, const SegA
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const uint32_t base = ((p0 + uint32_t(j) * 1024 + tid) % kSegRunTiles) * 1024;
+                const uint32_t base = ((p0 + uint32_t(j) * T + tid) % kSegRunTiles) * 1024;
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
                     const uint32_t lo = e[j][c] & 0xffffu, hi = e[j][c] >> 16;
@@ -1384,12 +1397,13 @@ __global__ void __launch_bounds__(1024, 8) k_seg_c1(const PartArgs A, const SegA
             }
         }
         lds_barrier();
-        uint32_t rec[kSegRunTiles], pos[kSegRunTiles];
+        uint32_t rec[U], pos[U];
 #pragma unroll
-        for (uint32_t u = 0; u < kSegRunTiles; u++) {
-            const uint32_t i = (t0 + u) * 1024 + tid;
-            const bool act = t0 + u < t1 && i < A.n;
-            const bool valid = act && (hv[u] >> 24) == 0 && mark[u * 1024 + tid] != ep;
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t lt = (u / PT) * 1024 + (u % PT) * T + tid;  // the swipe's place in the run
+            const uint32_t i = t0 * 1024 + lt;
+            const bool act = t0 + u / PT < t1 && i < A.n;
+            const bool valid = act && (hv[u] >> 24) == 0 && mark[lt] != ep;
             if (A.out && act) nt_st<16>(A.out + i, uint8_t(valid));
             pos[u] = 0xffffffffu;
             rec[u] = 0;
@@ -1406,19 +1420,20 @@ __global__ void __launch_bounds__(1024, 8) k_seg_c1(const PartArgs A, const SegA
         }
         lds_barrier();
         uint32_t total;
-        const uint32_t ex = seg_scan(tid <= S.nb1 ? cnt[tid] : 0u, ws, total);
-        if (tid <= S.nb1) {  // [nb1] = the run's total
+        const uint32_t ex = seg_scan(tid < S.nb1 ? cnt[tid] : 0u, ws, total);
+        if (tid < S.nb1) {
             cnt[tid] = ex;
             S.o1[size_t(tid) * kSegMaxRuns + r] = ex;
         }
+        if (tid == 0) S.o1[size_t(S.nb1) * kSegMaxRuns + r] = total;  // [nb1] = the run's total
         lds_barrier();
 #pragma unroll
-        for (uint32_t u = 0; u < kSegRunTiles; u++)
+        for (uint32_t u = 0; u < U; u++)
             if (pos[u] != 0xffffffffu) srec[cnt[pos[u] >> 16] + (pos[u] & 0xffffu)] = rec[u];
         lds_barrier();
         uint4 *dst = reinterpret_cast<uint4 *>(S.r1 + size_t(r) * kSegRunSw);
         const uint4 *src = reinterpret_cast<const uint4 *>(srec);
-        for (uint32_t j = tid; j * 4 < total; j += 1024) dst[j] = src[j];
+        for (uint32_t j = tid; j * 4 < total; j += T) dst[j] = src[j];
         // (the next run rewrites cnt, marks and srec only behind barriers
         // that every reader of this run's values has passed)
     }
@@ -1477,16 +1492,31 @@ __global__ void __launch_bounds__(1024) k_seg_scan(const SegArgs S) {
 #ifndef SKE_SEG_D_PIPE
 #define SKE_SEG_D_PIPE 0
 #endif
-__global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
+// D's block: T threads, R = 8192 / T records each, BPC blocks per CU (1024 x
+// 8 at 2 per CU, or 512 x 16 at 3 per CU: three chunks in flight per CU)
+#ifndef SKE_SEG_DT
+#define SKE_SEG_DT 512
+#endif
+template <uint32_t T> struct SegD {
+    static constexpr uint32_t R = kSegChunk / T;                 // records per thread
+    static constexpr uint32_t BPC = T == 1024 ? 2 : 3;           // blocks per CU
+    static constexpr uint32_t STAGE = T == 1024 ? 2048 : 1536;   // runs of a chunk staged in LDS
+    static constexpr uint32_t SPT = STAGE / T;                   // table words per thread
+    static constexpr uint32_t WPE = BPC * (T / 64) / 4;          // waves per SIMD (launch bounds)
+};
+template <uint32_t T>
+__global__ void __launch_bounds__(T, SegD<T>::WPE) k_seg_d(const SegArgs S) {
+    using DC = SegD<T>;
+    constexpr uint32_t R = DC::R, STAGE = DC::STAGE, SPT = DC::SPT;
+    static_assert(STAGE % T == 0 && kSegChunk % T == 0 && STAGE <= kSegDStage && kSegMaxWpb <= T && kSegMaxB1 <= T,
+                  "D geometry: whole table words and records per thread; a thread per window and per bucket");
     __shared__ uint32_t tot[kSegMaxB1], cbl[kSegMaxB1 + 1];
-    // the chunk's runs' prefix and r1 offsets, staged when fewer than
-    // kSegDStage runs hold it (a chunk of a sparse bucket spanning more
-    // reads them in place)
-    __shared__ uint32_t spp[kSegDStage + 1], sob[kSegDStage];
+    // the chunk's runs' prefix and r1 offsets, staged when fewer than STAGE
+    // runs hold it (a chunk of a sparse bucket spanning more reads them in place)
+    __shared__ uint32_t spp[STAGE + 1], sob[STAGE];
     __shared__ uint32_t c2[kSegMaxWpb + 1];
     __shared__ __attribute__((aligned(16))) uint32_t sb[kSegChunk];
-    __shared__ uint32_t ws[16];
-    static_assert(kSegDStage == 2 * 1024, "two run-table words per thread");
+    __shared__ uint32_t ws[T / 64];
     const uint32_t tid = threadIdx.x, wpb = 1u << S.wlog;
     // the buckets' chunk bases (every block; block 0 keeps them for E)
     uint32_t t = 0;
@@ -1496,9 +1526,13 @@ __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
     }
     uint32_t nq;
     const uint32_t cbase = seg_scan(tid < S.nb1 ? (t + kSegChunk - 1) / kSegChunk : 0u, ws, nq);
-    if (tid <= S.nb1) {
+    if (tid < S.nb1) {
         cbl[tid] = cbase;
         if (blockIdx.x == 0) S.cb[size_t(S.s) * (S.nb1 + 1) + tid] = cbase;
+    }
+    if (tid == 0) {
+        cbl[S.nb1] = nq;
+        if (blockIdx.x == 0) S.cb[size_t(S.s) * (S.nb1 + 1) + S.nb1] = nq;
     }
     lds_barrier();
     uint32_t *r2 = S.r2 + size_t(S.s) * S.maxch * kSegChunk;
@@ -1524,15 +1558,15 @@ __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
         d.ng = gb - d.ga;
         return d;
     };
-    // a staged chunk's table words j = tid, tid + 1024: prefix (j <= ng) and
-    // start in run (j < ng); always the same four loads (offsets past the
-    // range read nothing), so the wait for the records before them is exact
-    uint32_t ta[2], tb[2];
+    // a staged chunk's table words j = tid + i T: prefix (j <= ng) and start
+    // in run (j < ng); always the same loads (offsets past the range read
+    // nothing), so the wait for the records before them is exact
+    uint32_t ta[SPT], tb[SPT];
     auto tload = [&](const Chunk &d, bool on) {
 #pragma unroll
-        for (uint32_t i = 0; i < 2; i++) {
-            const uint32_t j = tid + i * 1024;
-            const bool st = on && d.ng < kSegDStage;
+        for (uint32_t i = 0; i < SPT; i++) {
+            const uint32_t j = tid + i * T;
+            const bool st = on && d.ng < STAGE;
             ta[i] = __builtin_amdgcn_raw_buffer_load_b32(
                 rp1, st && j <= d.ng ? (d.h * (kSegMaxRuns + 1) + d.ga + j) * 4 : kOOR, 0, 0);
             tb[i] = __builtin_amdgcn_raw_buffer_load_b32(
@@ -1546,38 +1580,38 @@ __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
         tload(cur, true);
     }
     while (q < nq) {
-        const bool staged = cur.ng < kSegDStage;  // block-uniform
+        const bool staged = cur.ng < STAGE;  // block-uniform
         const uint32_t w0 = cur.w0, w1 = cur.w1, ga = cur.ga, ng = cur.ng;
         if (staged) {
 #pragma unroll
-            for (uint32_t i = 0; i < 2; i++) {
-                const uint32_t j = tid + i * 1024;
+            for (uint32_t i = 0; i < SPT; i++) {
+                const uint32_t j = tid + i * T;
                 if (j <= ng) spp[j] = ta[i];
                 if (j < ng) sob[j] = (ga + j) * kSegRunSw + tb[i] - ta[i];
             }
         }
-        if (tid <= wpb) c2[tid] = 0;
+        for (uint32_t j = tid; j <= wpb; j += T) c2[j] = 0;
         lds_barrier();
         const uint32_t qn = q + gridDim.x;
         Chunk nx{};
         if (SKE_SEG_D_PIPE && qn < nq) nx = desc(qn);
-        uint32_t rec[8], pos[8];
+        uint32_t rec[R], pos[R];
         if (staged) {
-            uint32_t k[8];
+            uint32_t k[R];
 #pragma unroll
-            for (uint32_t j = 0; j < 8; j++) k[j] = 0;
+            for (uint32_t j = 0; j < R; j++) k[j] = 0;
             for (uint32_t len = ng; len > 1;) {
                 const uint32_t half = len >> 1;
 #pragma unroll
-                for (uint32_t j = 0; j < 8; j++) {
-                    const uint32_t p = w0 + j * 1024 + tid;
+                for (uint32_t j = 0; j < R; j++) {
+                    const uint32_t p = w0 + j * T + tid;
                     k[j] = spp[k[j] + half] <= p ? k[j] + half : k[j];
                 }
                 len -= half;
             }
 #pragma unroll
-            for (uint32_t j = 0; j < 8; j++) {
-                const uint32_t p = w0 + j * 1024 + tid;
+            for (uint32_t j = 0; j < R; j++) {
+                const uint32_t p = w0 + j * T + tid;
                 rec[j] = __builtin_amdgcn_raw_buffer_load_b32(rr1, p < w1 ? (sob[k[j]] + p) * 4 : kOOR, 0, 0);
             }
         } else {
@@ -1585,10 +1619,10 @@ __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
             // run tables read in place, one search per thread, then a walk)
             const uint32_t *gpp = S.p1 + size_t(cur.h) * (kSegMaxRuns + 1) + ga;
             const uint32_t *gob = S.o1 + size_t(cur.h) * kSegMaxRuns + ga;
-            const uint32_t p0 = w0 + tid * 8;
+            const uint32_t p0 = w0 + tid * R;
             uint32_t k = p0 < w1 ? seg_last_le(gpp, ng, p0) : 0u;
 #pragma unroll
-            for (uint32_t j = 0; j < 8; j++) {
+            for (uint32_t j = 0; j < R; j++) {
                 const uint32_t p = p0 + j;
                 rec[j] = 0;
                 if (p < w1) {
@@ -1600,9 +1634,9 @@ __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
         // the next chunk's run table, in flight during this chunk's sort
         if (SKE_SEG_D_PIPE) tload(nx, qn < nq);
 #pragma unroll
-        for (uint32_t j = 0; j < 8; j++) {
+        for (uint32_t j = 0; j < R; j++) {
             pos[j] = 0xffffffffu;
-            const uint32_t p = staged ? w0 + j * 1024 + tid : w0 + tid * 8 + j;
+            const uint32_t p = staged ? w0 + j * T + tid : w0 + tid * R + j;
             if (p < w1) {
                 const uint32_t w2 = (rec[j] >> (kSegRecShift + S.klog)) & (wpb - 1);
                 pos[j] = (w2 << 16) | atomicAdd(&c2[w2], 1u);
@@ -1610,19 +1644,20 @@ __global__ void __launch_bounds__(1024, 8) k_seg_d(const SegArgs S) {
         }
         lds_barrier();
         uint32_t total;
-        const uint32_t ex = seg_scan(tid <= wpb ? c2[tid] : 0u, ws, total);
-        if (tid <= wpb) {
+        const uint32_t ex = seg_scan(tid < wpb ? c2[tid] : 0u, ws, total);
+        if (tid < wpb) {
             c2[tid] = ex;
             o2[size_t(q) * (wpb + 1) + tid] = ex;
         }
+        if (tid == 0) o2[size_t(q) * (wpb + 1) + wpb] = total;
         lds_barrier();
 #pragma unroll
-        for (uint32_t j = 0; j < 8; j++)
+        for (uint32_t j = 0; j < R; j++)
             if (pos[j] != 0xffffffffu) sb[c2[pos[j] >> 16] + (pos[j] & 0xffffu)] = rec[j];
         lds_barrier();
         uint4 *dst = reinterpret_cast<uint4 *>(r2 + size_t(q) * kSegChunk);
         const uint4 *src = reinterpret_cast<const uint4 *>(sb);
-        for (uint32_t j = tid; j * 4 < total; j += 1024) dst[j] = src[j];
+        for (uint32_t j = tid; j * 4 < total; j += T) dst[j] = src[j];
         // (the next chunk rewrites spp / sob / c2 only after the barriers
         // that every reader of this chunk's values has passed)
         if (!SKE_SEG_D_PIPE && qn < nq) {
@@ -2365,11 +2400,13 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             if (seg) {
                 S.s = si % P.nsub;
                 S.nruns = (A.ntiles + kSegRunTiles - 1) / kSegRunTiles;
-                hipLaunchKernelGGL(k_seg_c1, dim3(std::min(S.nruns, unsigned(cus) * 2)), dim3(1024), 0, st, A, S);
+                hipLaunchKernelGGL(k_seg_c1<SKE_SEG_C1T>, dim3(std::min(S.nruns, unsigned(cus) * SegC1<SKE_SEG_C1T>::BPC)),
+                                   dim3(SKE_SEG_C1T), 0, st, A, S);
                 if (hook) hook(hook_user, 2, 1, st);
                 if (hook) hook(hook_user, 3, 0, st);
                 hipLaunchKernelGGL(k_seg_scan, dim3(S.nb1), dim3(1024), 0, st, S);
-                hipLaunchKernelGGL(k_seg_d, dim3(unsigned(cus) * 2), dim3(1024), 0, st, S);
+                hipLaunchKernelGGL(k_seg_d<SKE_SEG_DT>, dim3(unsigned(cus) * SegD<SKE_SEG_DT>::BPC), dim3(SKE_SEG_DT),
+                                   0, st, S);
                 if (hook) hook(hook_user, 3, 1, st);
             } else if (flist) {
                 const unsigned gc =

@@ -9,6 +9,7 @@ is already on the device.
 from __future__ import annotations
 
 import ctypes as C
+import gc
 
 import numpy as np
 
@@ -16,6 +17,21 @@ from ._lib import Context, GenParams, SKE_MEM_DEVICE
 from . import synthetic
 
 PASS_KINDS = 9  # SKE_PASS_KINDS (include/sketch.h)
+
+
+class _no_gc:
+    """Collect cyclic garbage now, then keep the collector off until exit
+    (around a stream capture: see SketchEngine.capture)."""
+
+    def __enter__(self):
+        gc.collect()
+        self.was = gc.isenabled()
+        gc.disable()
+
+    def __exit__(self, *exc):
+        if self.was:
+            gc.enable()
+        return False
 
 
 class DeviceBuffer:
@@ -249,19 +265,26 @@ class SketchEngine:
     # ---- HIP graphs: record enqueue-only calls once, replay many times
     def capture(self, fn) -> "Graph":
         """Record the device work `fn()` enqueues on the context stream (only
-        *_async calls) into an uploaded executable graph."""
-        self.ctx.call("ske_capture_begin")
-        try:
-            fn()
-        except BaseException:
-            # end the capture (the stream must leave capture mode) and drop
-            # the partial graph; the recording call's error is the one raised
+        *_async calls) into an uploaded executable graph.
+
+        Python's cyclic garbage collector is run before and held off during
+        the recording: a collection inside it could finalise an unreachable
+        Context or device buffer (ske_close / hipFree / hipStreamSynchronize),
+        which a thread-local stream capture forbids -- the capture would be
+        invalidated and this recording fail."""
+        with _no_gc():
+            self.ctx.call("ske_capture_begin")
+            try:
+                fn()
+            except BaseException:
+                # end the capture (the stream must leave capture mode) and drop
+                # the partial graph; the recording call's error is the one raised
+                g = C.c_void_p()
+                if self.ctx.lib.ske_capture_end(self.ctx.ptr, C.byref(g)) == 0 and g.value:
+                    self.ctx.lib.ske_graph_free(self.ctx.ptr, g)
+                raise
             g = C.c_void_p()
-            if self.ctx.lib.ske_capture_end(self.ctx.ptr, C.byref(g)) == 0 and g.value:
-                self.ctx.lib.ske_graph_free(self.ctx.ptr, g)
-            raise
-        g = C.c_void_p()
-        self.ctx.call("ske_capture_end", C.byref(g))
+            self.ctx.call("ske_capture_end", C.byref(g))
         return Graph(self.ctx, g.value)
 
     def capture_branched(self, steps, main, side) -> "Graph":

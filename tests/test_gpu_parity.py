@@ -504,6 +504,51 @@ def test_graph_replay_equals_eager(engine):
         assert np.array_equal(o.to_host(np.uint8, b.n), a)
 
 
+def test_capture_survives_cyclic_garbage(engine):
+    """An unreachable Context in a reference cycle (a test's or a caller's
+    engine) must not be finalised inside a stream capture: ske_close's
+    hipStreamSynchronize / hipFree there invalidate a thread-local capture
+    (round 6: a full-size test's graph recording failed right after a test
+    whose engines were left to the cyclic collector).  With the collector
+    forced to run on every allocation, the recording still succeeds and the
+    replay equals the eager run."""
+    import gc
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import DeviceBuffer, SketchEngine
+    w = synthetic.WORKLOADS["c2"]
+    engine.reserve(0, w.bf_error, w.bf_capacity)
+    p = engine.gen_params(w)
+    engine.preload(0, p, w.n_members)
+    engine.hll_reserve(w.n_keys)
+    bs = [engine.swipe_batch(p, j * 100_000, 100_000) for j in range(2)]
+    outs = [DeviceBuffer(engine.ctx, b.n) for b in bs]
+    for b, o in zip(bs, outs):
+        engine.swipes_async(0, b, o)
+    engine.sync()
+    answers = [o.to_host(np.uint8, b.n) for b, o in zip(bs, outs)]
+    regs = engine.registers_all(w.n_keys).copy()
+    gc.collect()
+    old = gc.get_threshold()
+    try:
+        for _ in range(3):  # unreachable engines in cycles, left to the collector
+            other = SketchEngine(0)
+            other.hll_reserve(8)
+            cyc = [other]
+            cyc.append(cyc)
+            del other, cyc
+        gc.set_threshold(1)  # a collection at (almost) every allocation
+        g = engine.capture(lambda: [engine.swipes_async(0, b, o) for b, o in zip(bs, outs)])
+    finally:
+        gc.set_threshold(*old)
+    gc.collect()
+    g.launch()
+    engine.sync()
+    g.free()
+    assert np.array_equal(engine.registers_all(w.n_keys), regs)  # the replay raises nothing new
+    for a, b, o in zip(answers, bs, outs):
+        assert np.array_equal(o.to_host(np.uint8, b.n), a)
+
+
 @pytest.mark.parametrize("variant", [-1, 2, 3])
 def test_two_streams_equal_one_stream(engine, variant):
     """Launches alternating over two HIP streams (overlapping K1 kernels; the
