@@ -69,7 +69,7 @@ MALL_BYTES = 256 << 20  # Infinity Cache: a slab this small stays on chip
 METRIC = "swipes/sec (fused BF.EXISTS+PFADD) at 1/2/4/8 GPUs; % of HBM peak"
 PASS_NAMES = ["k1", "k_part_a", "k_part_b", "k_part_c", "k_seg_d", "k_seg_e", "feed_h2d", "feed_d2h", "feed_call"]
 K1_PASSES = 6  # PASS_NAMES[:6] are K1 kernels; the rest the stages of a host-fed call
-PMC_ROUNDS = ["r05", "r04", "r03", "r02"]  # newest committed PMC summaries first
+PMC_ROUNDS = ["r06", "r05", "r04", "r03", "r02"]  # newest committed PMC summaries first
 VERIFY_KEYS = 64
 # swipes per GPU and step where it differs from the workload's own
 # step_swipes: C3 since round 5 takes 2^27 (its 1B-swipe stream in 8 steps;

@@ -1,12 +1,12 @@
-"""Per-kernel PMC summaries of the round-5 default C3 step (partitioned K1 +
-segmented PFADD) from tools/gpu_pmc_r05.sh's passes, named by bench.py's pass
+"""Per-kernel PMC summaries of the default C3 step (partitioned K1 +
+segmented PFADD) from tools/gpu_pmc_seg.sh's passes, named by bench.py's pass
 kinds: k_part_a, k_part_b, k_part_c (the segmented C1, k_seg_c1), k_seg_d
 (k_seg_scan + k_seg_d, per sub-batch), k_seg_e (window pass E1 + E2 + merge
 M, per step).  Warm-up dispatches are skipped (2 steps of NSUB sub-batches;
 env NSUB, default 4: 2^27 swipes in sub-batches of 2^25).  Every summary
 records the swipes one launch covers (env STEP_SWIPES / NSUB; the window pass:
 a step), so bench.py applies it only to launches of that size.
-usage: NSUB=4 STEP_SWIPES=134217728 python tools/r05_pmc_seg.py <pmc_root> <out_prefix>
+usage: NSUB=4 STEP_SWIPES=134217728 python tools/pmc_seg.py <pmc_root> <out_prefix>
 """
 import json
 import os
@@ -19,8 +19,9 @@ root, prefix = sys.argv[1], sys.argv[2]
 NSUB = int(os.environ.get("NSUB", "4"))
 STEP = int(os.environ.get("STEP_SWIPES", str(1 << 27)))
 SKIP_SUB, SKIP_STEP = 2 * NSUB, 2
+ROUND6 = os.environ.get("SEG_D_TEMPLATE", "1") == "1"  # round 6: k_seg_d<T> (round 5: k_seg_d(SegArgs))
 plan = {"k_part_a": (["k_part_a3"], SKIP_SUB), "k_part_b": (["k_part_b"], SKIP_SUB),
-        "k_part_c": (["k_seg_c1"], SKIP_SUB), "k_seg_d": (["k_seg_scan", "k_seg_d("], SKIP_SUB),
+        "k_part_c": (["k_seg_c1"], SKIP_SUB), "k_seg_d": (["k_seg_scan", "k_seg_d<" if ROUND6 else "k_seg_d("], SKIP_SUB),
         "k_seg_e": (["k_seg_e<1, false>", "k_seg_e<1, true>", "k_seg_m<1>"], SKIP_STEP)}
 for name, (kernels, skip) in plan.items():
     parts = {k: summarise(root, k, skip) for k in kernels}
