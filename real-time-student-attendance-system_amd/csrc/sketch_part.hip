@@ -71,13 +71,25 @@ constexpr uint32_t kPbBlock = 1024;
 #define SKE_PC_BLOCKS_PER_CU 8
 #endif
 constexpr uint32_t kPcBlock = 256;            // k_part_c (fail bytes)
-constexpr uint32_t kPcFlBlock = SKE_PC_BLOCK;  // k_part_c_fl (fail lists)
 constexpr uint32_t kPSliceMask = kPSliceBits - 1;
 constexpr uint32_t kPSliceBytes = kPSliceBits / 8;  // 64 KiB
 constexpr uint32_t kPSub = 1u << 26;                // swipes per sub-batch (passes A-B-C), at most
 constexpr uint32_t kPbGroup = 8;                    // tiles a pass-B wave reads at once
 constexpr uint32_t kPbLanes = 64 / kPbGroup;        // lanes per tile run
 constexpr uint32_t kPTileLog = 10;                  // swipes per tile = 1 << kPTileLog
+// swipes per tile of the fail-list chains (one link, k = 11: C3 / C5's
+// filter): 1024, or 1536 (longer (pair, tile) runs for pass B)
+#ifndef SKE_TILE_FL
+#define SKE_TILE_FL 1024
+#endif
+constexpr uint32_t kTileFl = SKE_TILE_FL;
+static_assert(kTileFl == 1024 || kTileFl == 1536, "fail-list tiles of 1024 or 1536 swipes");
+// pass B's 16-B pieces per lane and run of the fail-list chains: a (pair,
+// tile) run of ~74 records (1024-swipe tiles) or ~111 (1536) from the line
+// holding its start (runs longer than 32 R - 31 records finish in a tail loop)
+constexpr int kPbRFl = kTileFl == 1024 ? 4 : 6;
+// pass C (fail lists): threads per block, kTileFl / kPcFlT swipes each per tile
+constexpr uint32_t kPcFlT = kTileFl == 1024 ? SKE_PC_BLOCK : 768;
 
 struct PartLink {
     const uint8_t *bf;
@@ -193,7 +205,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t part_rsrc(const void *p, uint3
 // tile's atomics (from offsets loaded at that tile's start); 2 -- at the
 // previous tile's start, from offsets loaded a tile earlier
 #ifndef SKE_PA_AHEAD
-#define SKE_PA_AHEAD 2
+#define SKE_PA_AHEAD (kTileFl == 1024 ? 2 : 1)  // (1536-swipe tiles: 2 would spill)
 #endif
 typedef uint32_t part_u32x4 __attribute__((ext_vector_type(4)));
 template <int BIT, class T> __device__ __forceinline__ T nt_ld(const T *p) {
@@ -415,17 +427,22 @@ constexpr uint32_t kOORa = 0x80000000u;  // a buffer offset past every range: lo
 // place in the group's region in a register; every run starts on a 16-B
 // piece (padded to 4 records in LDS and in the region), so the copy-out stays
 // one 16-B store per piece, to the place an LDS map gives the piece's unit.
-template <int KM, uint32_t kCnt, bool GL = false>
+template <int KM, uint32_t kCnt, bool GL = false, uint32_t TILE = 1024>
 __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two blocks per CU
     constexpr uint32_t kT = 512;
-    constexpr uint32_t kU = 1024 / kT, kTile = 1024;
+    constexpr uint32_t kU = TILE / kT, kTile = TILE;
     constexpr uint32_t kPer = kCnt / kT;  // counters per thread: kPer / 2 whole pairs
     // (the sink's records land past the copy-out; GL: a unit's run padded to 4)
     constexpr uint32_t kRecWords = kTile * KM + (GL ? 4 * (kCnt / 2) : 0);
     constexpr uint32_t kCo = (kRecWords / 4 + kT - 1) / kT;  // 16-B copy-out pieces per thread
     constexpr uint32_t kMap = GL ? kRecWords / 4 : 1;        // GL: a piece's place - its LDS place
-    static_assert(kCnt % (2 * kT) == 0 && 4u * kRecWords < 65536u,
-                  "whole pairs per thread; a rank * 4 below bit 16; starts fit 16 bits");
+    // counter bias: counter c starts at c << kSB, so an atomic's return value
+    // >> kRS (= kSB - 2) is its byte offset 4 c as long as 4 * rank stays below
+    // bit kRS (1024-swipe tiles: 18 / 16; 1536: 19 / 17)
+    constexpr uint32_t kSB = 4u * kRecWords < 65536u ? 18 : 19, kRS = kSB - 2;
+    static_assert(kCnt % (2 * kT) == 0 && 4u * kRecWords < (1u << kRS) && kRecWords < 65536u &&
+                      (2 * kCnt - 1) < (1u << (32 - kSB)) && kTile % kT == 0 && kTile <= 2048,
+                  "whole pairs per thread; a rank * 4 below bit kRS; starts fit 16 bits; 11-bit swipe field");
     // one LDS object, counters first: it sits at LDS address 0, so a probe's
     // counter address is its slice field shifted and added to the parity's
     // base (v_bfe + v_lshl_add: two VALU per probe)
@@ -443,7 +460,7 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t nunits = A.nunits;
     const uint32_t sink = 2 * nunits;  // the sink pair's first slice
-    for (uint32_t c = tid; c < 2 * kCnt; c += kT) cnt[c] = c << 18;
+    for (uint32_t c = tid; c < 2 * kCnt; c += kT) cnt[c] = c << kSB;
     lds_barrier();
     // Every global load and store below is issued by every wave the same
     // number of times (buffer operations; a lane or a whole call with nothing
@@ -572,7 +589,7 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
 #pragma unroll
         for (uint32_t j = 0; j < kPer; j++) {
             const uint32_t c = cb + tid * kPer + j;
-            v[j] = (cnt[c] - (c << 18)) >> 2;
+            v[j] = (cnt[c] - (c << kSB)) >> 2;
         }
 #pragma unroll
         for (uint32_t j = 0; j < kPer; j += 2) s += GL ? (v[j] + v[j + 1] + 3) & ~3u : v[j] + v[j + 1];
@@ -599,8 +616,8 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
             }
             __builtin_amdgcn_raw_buffer_store_b32(W, roff, un < nunits ? (un * A.off_stride + t) * 4 : kOORa, 0, 0);
             if (g == sink) stot = run;
-            cnt[c] = 4 * run - (c << 18);
-            cnt[c + 1] = 4 * (run + v[j]) - ((c + 1) << 18);
+            cnt[c] = 4 * run - (c << kSB);
+            cnt[c + 1] = 4 * (run + v[j]) - ((c + 1) << kSB);
             run += GL ? (n2 + 3) & ~3u : n2;
         }
         lds_barrier();
@@ -609,11 +626,11 @@ __global__ void __launch_bounds__(512, 4) k_part_a3(const PartArgs A) {  // two 
 #pragma unroll
             for (int q = 0; q < KM; q++) {
                 const uint32_t r = rp[u][q];
-                *reinterpret_cast<uint32_t *>(srecb + (r + *reinterpret_cast<const uint32_t *>(cntb + (r >> 16)))) =
+                *reinterpret_cast<uint32_t *>(srecb + (r + *reinterpret_cast<const uint32_t *>(cntb + (r >> kRS)))) =
                     rv[u][q];
             }
         const uint32_t nb = (cb ^ kCnt);
-        for (uint32_t g = tid; g <= sink + 1; g += kT) cnt[nb + g] = (nb + g) << 18;
+        for (uint32_t g = tid; g <= sink + 1; g += kT) cnt[nb + g] = (nb + g) << kSB;
         lds_barrier();
         const uint32_t total = stot;
         // a fixed number of 16-B pieces per thread (those past the tile's
@@ -735,8 +752,11 @@ hipError_t set_pb_stamp_buffer(void *p) {
 #endif
 // GL (FL only): the group layout -- a run's start is its place in the (tile
 // group, unit) region, or (bit 31 of its run word) in the tile's overflow row
-template <int SP, int R = 2 * SP, bool FL = false, bool GL = false>  // R: 16-byte pieces per lane and run (runs of SP slices)
+// TILE: swipes per tile (FL: kTileFl; the others 1024); a k_part_a3 record's
+// swipe field is its bits 20..30
+template <int SP, int R = 2 * SP, bool FL = false, bool GL = false, uint32_t TILE = 1024>  // R: 16-byte pieces per lane and run (runs of SP slices)
 __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const PartArgs A) {
+    static_assert(FL || TILE == 1024, "tiles of other than 1024 swipes are the fail-list chains'");
     static_assert(!GL || FL, "the group layout is pass A3's");
     PB_STAMP(0);
     const uint32_t tmask = (1u << kPTileLog) - 1;
@@ -942,7 +962,7 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                 okm |= part_bit(img32[o >> 5], rr) << j;
             }
             uint32_t fm = vm & ~okm;
-            const uint32_t tbase = (tg + k) << kPTileLog;
+            const uint32_t tbase = (tg + k) * TILE;
             const uint32_t cnt = __builtin_popcount(fm);
             // the record a lane's next failing probe sits in, by a select
             // tree on its index bits (no compare chain)
@@ -979,7 +999,7 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                 while (fm) {
                     const uint32_t j = __builtin_ctz(fm);
                     fm &= fm - 1;
-                    const uint32_t at = (pick(j) >> 20) & tmask;  // k_part_a3's swipe field
+                    const uint32_t at = (pick(j) >> 20) & 0x7ffu;  // k_part_a3's swipe field
                     if (pos < kPbLanes) q[k * kPbLanes + pos] = at;
                     else __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail, fail_at(tbase + at), 0, 0);  // overflow
                     pos++;
@@ -1026,7 +1046,7 @@ __global__ void __launch_bounds__(kPbBlock, SP == 1 ? 8 : 4) k_part_b(const Part
                                                     : ((rr & kPSliceMask) | ((rr >> kPTileLog) & kPSliceBits));
                     if (!((img[o >> 3] >> (o & 7)) & 1))
                         __builtin_amdgcn_raw_buffer_store_b8(uint8_t(1), rfail,
-                                                             fail_at(tbase + ((rr >> (FL ? 20 : kPSliceLog)) & tmask)), 0, 0);
+                                                             fail_at(tbase + (FL ? (rr >> 20) & 0x7ffu : (rr >> kPSliceLog) & tmask)), 0, 0);
                 }
             }
             bc = b1;
@@ -1124,13 +1144,14 @@ __global__ void __launch_bounds__(kPcBlock) k_part_c(const PartArgs A) {
 // slower, 0.409 -> 0.436 ms, round 4: the line traffic, not the CAS count,
 // holds this pass.)  U swipes per thread per tile, kPcFlBlock * U = 1024
 // (1024 x 1 since round 4; see SKE_PC_BLOCK).
-template <int U>
-__global__ void __launch_bounds__(kPcFlBlock) k_part_c_fl(const PartArgs A) {
-    static_assert(kPcFlBlock * U == 1024, "one 1024-swipe tile per sub-step");
+template <uint32_t BT, int U, uint32_t TILE>
+__global__ void __launch_bounds__(BT) k_part_c_fl(const PartArgs A) {
+    static_assert(BT * U == TILE, "one tile per sub-step");
+    constexpr uint32_t kPcFlBlock = BT;
     constexpr uint32_t kRun = kPbGroup;  // tiles per block iteration
-    __shared__ uint16_t mark[kRun * 1024];
+    __shared__ uint16_t mark[kRun * TILE];
     const uint32_t tid = threadIdx.x;
-    for (uint32_t j = tid; j < kRun * 1024; j += kPcFlBlock) mark[j] = 0;
+    for (uint32_t j = tid; j < kRun * TILE; j += kPcFlBlock) mark[j] = 0;
     uint32_t gt0, gt1;
     part_group(A.ntiles, blockIdx.x % kPGroups, gt0, gt1);
     const uint32_t nblk = gridDim.x / kPGroups;
@@ -1142,7 +1163,7 @@ __global__ void __launch_bounds__(kPcFlBlock) k_part_c_fl(const PartArgs A) {
     auto load = [&](uint32_t t, uint32_t tend, In &in) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t i = t * 1024 + uint32_t(u) * kPcFlBlock + tid;
+            const uint32_t i = t * TILE + uint32_t(u) * kPcFlBlock + tid;
             const bool act = t < tend && i < A.n;
             in.sl[u] = act ? nt_ld<16>(A.slot + i) : 0u;
             in.hv[u] = act ? nt_ld<16>(A.hllw + i) : 0xff000000u;  // (top byte: pass B's overflow flag)
@@ -1169,12 +1190,12 @@ __global__ void __launch_bounds__(kPcFlBlock) k_part_c_fl(const PartArgs A) {
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const uint32_t base = ((p0 + uint32_t(j) * kPcFlBlock + tid) % kRun) * 1024;
+                const uint32_t base = ((p0 + uint32_t(j) * kPcFlBlock + tid) % kRun) * TILE;
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
                     const uint32_t lo = e[j][c] & 0xffffu, hi = e[j][c] >> 16;
-                    if (ok[j] && lo != 0xffffu) mark[base + (lo & 1023u)] = ep;
-                    if (ok[j] && hi != 0xffffu) mark[base + (hi & 1023u)] = ep;
+                    if (ok[j] && lo < TILE) mark[base + lo] = ep;  // (0xffff: no entry)
+                    if (ok[j] && hi < TILE) mark[base + hi] = ep;
                 }
             }
         }
@@ -1182,13 +1203,13 @@ __global__ void __launch_bounds__(kPcFlBlock) k_part_c_fl(const PartArgs A) {
         for (uint32_t t = r0; t < r1; t++) {
             In nxt;
             load(t + 1, r1, nxt);
-            const uint16_t *mk = mark + (t - r0) * 1024;
+            const uint16_t *mk = mark + (t - r0) * TILE;
             bool valid[U];
             uint32_t *w[U];
             uint32_t rank[U], sh[U], cw[U], seen[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const uint32_t i = t * 1024 + uint32_t(u) * kPcFlBlock + tid;
+                const uint32_t i = t * TILE + uint32_t(u) * kPcFlBlock + tid;
                 valid[u] = i < A.n && cur.fb[u] == 0 && mk[uint32_t(u) * kPcFlBlock + tid] != ep;
                 w[u] = nullptr;
                 rank[u] = sh[u] = 0;
@@ -1217,7 +1238,7 @@ __global__ void __launch_bounds__(kPcFlBlock) k_part_c_fl(const PartArgs A) {
             if (A.out) {
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    const uint32_t i = t * 1024 + uint32_t(u) * kPcFlBlock + tid;
+                    const uint32_t i = t * TILE + uint32_t(u) * kPcFlBlock + tid;
                     if (i < A.n) nt_st<16>(A.out + i, uint8_t(valid[u]));
                 }
             }
@@ -1268,7 +1289,7 @@ __global__ void __launch_bounds__(kPcFlBlock) k_part_c_fl(const PartArgs A) {
 //                   its records in place (pre-check load + CAS, as pass C).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSegRunTiles = kPbGroup;                 // tiles per level-1 run
-constexpr uint32_t kSegRunSw = kSegRunTiles << kPTileLog;  // 8192 swipes
+constexpr uint32_t kSegRunSw = kSegRunTiles * kTileFl;    // 8192 swipes (12 288 with 1536-swipe tiles)
 constexpr uint32_t kSegMaxB1 = 512;                         // level-1 buckets
 constexpr uint32_t kSegMaxWpb = 512;                        // windows per bucket
 constexpr uint32_t kSegChunk = 8192;                        // records per level-2 chunk
@@ -1334,16 +1355,18 @@ __device__ __forceinline__ uint32_t seg_last_le(const uint32_t *a, uint32_t n, u
     return lo;
 }
 
-// C1's block: T threads, U = 8192 / T swipes of a run each (1024 x 8 at two
-// blocks per CU, or 512 x 16 at three: three runs in flight per CU)
+// C1's block: T threads, U = kSegRunSw / T swipes of a run each (1024 x 8 at
+// two blocks per CU, or 512 x 16 at three: three runs in flight per CU; with
+// 1536-swipe tiles 768 x 16 at two)
 #ifndef SKE_SEG_C1T
-#define SKE_SEG_C1T 512
+#define SKE_SEG_C1T (kTileFl == 1024 ? 512 : 768)
 #endif
 template <uint32_t T> struct SegC1 {
     static constexpr uint32_t U = kSegRunSw / T;       // swipes per thread per run
-    static constexpr uint32_t PT = 1024 / T;           // swipes per thread per tile
-    static constexpr uint32_t BPC = T == 1024 ? 2 : 3;  // blocks per CU
+    static constexpr uint32_t PT = kTileFl / T;        // swipes per thread per tile
+    static constexpr uint32_t BPC = T == 512 ? 3 : 2;  // blocks per CU
     static constexpr uint32_t WPE = BPC * (T / 64) / 4;
+    static_assert(kTileFl % T == 0, "whole tile slices per thread");
 };
 template <uint32_t T>
 __global__ void __launch_bounds__(T, SegC1<T>::WPE) k_seg_c1(const PartArgs A, const SegArgs S) {
@@ -1367,7 +1390,7 @@ __global__ void __launch_bounds__(T, SegC1<T>::WPE) k_seg_c1(const PartArgs A, c
         uint32_t sl[U], hv[U];
 #pragma unroll
         for (uint32_t u = 0; u < U; u++) {  // swipe u: tile u / PT, its (u % PT)-th T-thread slice
-            const uint32_t i = (t0 + u / PT) * 1024 + (u % PT) * T + tid;
+            const uint32_t i = (t0 + u / PT) * kTileFl + (u % PT) * T + tid;
             const bool act = t0 + u / PT < t1 && i < A.n;
             sl[u] = act ? nt_ld<16>(A.slot + i) : 0u;
             hv[u] = act ? nt_ld<16>(A.hllw + i) : 0xff000000u;
@@ -1387,12 +1410,12 @@ __global__ void __launch_bounds__(T, SegC1<T>::WPE) k_seg_c1(const PartArgs A, c
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const uint32_t base = ((p0 + uint32_t(j) * T + tid) % kSegRunTiles) * 1024;
+                const uint32_t base = ((p0 + uint32_t(j) * T + tid) % kSegRunTiles) * kTileFl;
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
                     const uint32_t lo = e[j][c] & 0xffffu, hi = e[j][c] >> 16;
-                    if (ok[j] && lo != 0xffffu) mark[base + (lo & 1023u)] = ep;
-                    if (ok[j] && hi != 0xffffu) mark[base + (hi & 1023u)] = ep;
+                    if (ok[j] && lo < kTileFl) mark[base + lo] = ep;  // (0xffff: no entry)
+                    if (ok[j] && hi < kTileFl) mark[base + hi] = ep;
                 }
             }
         }
@@ -1400,8 +1423,8 @@ __global__ void __launch_bounds__(T, SegC1<T>::WPE) k_seg_c1(const PartArgs A, c
         uint32_t rec[U], pos[U];
 #pragma unroll
         for (uint32_t u = 0; u < U; u++) {
-            const uint32_t lt = (u / PT) * 1024 + (u % PT) * T + tid;  // the swipe's place in the run
-            const uint32_t i = t0 * 1024 + lt;
+            const uint32_t lt = (u / PT) * kTileFl + (u % PT) * T + tid;  // the swipe's place in the run
+            const uint32_t i = t0 * kTileFl + lt;
             const bool act = t0 + u / PT < t1 && i < A.n;
             const bool valid = act && (hv[u] >> 24) == 0 && mark[lt] != ep;
             if (A.out && act) nt_st<16>(A.out + i, uint8_t(valid));
@@ -2064,11 +2087,13 @@ static uint32_t part_km(uint32_t ksum) {
 }
 
 // records per tile, rounded so tiles start on 128-B lines
-static uint32_t part_stride(uint32_t ksum) { return ((ksum << kPTileLog) + 31) & ~31u; }
+static uint32_t part_stride(uint32_t ksum, uint32_t tile) { return ((ksum * tile) + 31) & ~31u; }
 
 // the fail-list instantiation: one link of k = 11 (C3/C5's filter), slice
 // pairs (the sink pair must fit k_part_a3<11, 2048>'s counters)
 static bool part_flist(const PartArgs &A) { return A.nlinks == 1 && A.ksum == 11 && A.nslices <= 2046; }
+// swipes per tile: kTileFl for the fail-list chains, 1024 for the others
+static uint32_t part_tile(const PartArgs &A) { return part_flist(A) ? kTileFl : kPaBlock; }
 
 static bool part_plan(const ChainDev &ch, PartArgs *A) {
     if (ch.nlinks < 1 || ch.nlinks > kPMaxLinks) return false;
@@ -2093,7 +2118,7 @@ static bool part_plan(const ChainDev &ch, PartArgs *A) {
     A->nslices = slices;
     A->ksum = ksum;
     A->nunits = (slices + 1) / 2;
-    A->stride = part_stride(ksum);
+    A->stride = part_stride(ksum, part_tile(*A));
     return true;
 }
 
@@ -2112,7 +2137,7 @@ bool part_supported(const ChainDev &ch) {
 // written by two tiles, partial-line writes.
 static bool part_glayout(PartArgs *A, const SegOpts &so, uint32_t ntiles_max) {
     A->gcap = A->govf = 0;
-    if (so.rec_groups != 1 || !part_flist(*A) || A->nunits >= 512) return false;
+    if (so.rec_groups != 1 || !part_flist(*A) || A->nunits >= 512 || kTileFl != 1024) return false;
     const double d = double(A->link[0].d);
     const double share = std::min(d, double(2 * kPSliceBits)) / d;  // of the largest unit
     const double mu = 8.0 * 1024 * A->ksum * share;
@@ -2131,7 +2156,8 @@ static bool part_glayout(PartArgs *A, const SegOpts &so, uint32_t ntiles_max) {
 // fail lists of one-link chains)
 static hipError_t part_scratch(PartArgs *A, uint64_t n, uint32_t sub, const SegOpts &so, Scratch *scr) {
     const uint32_t m = n < sub ? uint32_t(n) : sub;
-    const uint32_t ntiles_max = (m + kPaBlock - 1) / kPaBlock;
+    const uint32_t tile = part_tile(*A);
+    const uint32_t ntiles_max = (m + tile - 1) / tile;
     const uint32_t fstride = (m + 255) & ~255u;
     A->off_stride = (ntiles_max + 15) & ~15u;
     hipError_t e = hipSuccess;
@@ -2160,10 +2186,11 @@ constexpr uint32_t kPSubDefault = 1u << 25;
 static uint32_t part_sub(uint32_t sub_opt, const PartArgs &A) {
     const uint64_t tiles = ((uint64_t(1) << 31) - 1) / (uint64_t(A.stride) * 4);
     const uint64_t span = SKE_PB_SPLIT == 1 ? tiles : (tiles - 8) * kPGroups;  // tiles a sub-batch may have
-    const uint32_t cap = uint32_t(std::min<uint64_t>(kPSub, span / 8 * 8 * kPaBlock));
+    const uint32_t tile = part_tile(A);
+    const uint32_t cap = uint32_t(std::min<uint64_t>(kPSub / tile * tile, span / 8 * 8 * tile));
     uint32_t sub = sub_opt ? sub_opt : std::min(cap, kPSubDefault);
-    sub = (sub + kPaBlock - 1) / kPaBlock * kPaBlock;
-    return sub < kPaBlock ? kPaBlock : (sub > cap ? cap : sub);
+    sub = (sub + tile - 1) / tile * tile;
+    return sub < tile ? tile : (sub > cap ? cap : sub);
 }
 
 // the scratch before the first launch (so a graph recorded later holds it)
@@ -2301,6 +2328,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
     if (nmax == 0) return hipSuccess;
     hipError_t e = part_scratch(&A, nmax, sub, so, scr);
     if (e != hipSuccess) return e;
+    const uint32_t tile = part_tile(A);
     A.regs = regs;
     A.nslots = nslots;
     A.err = err;
@@ -2316,14 +2344,14 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
         // fixed-width ids: a sub-batch's byte offsets (swipe * width) stay 32-bit
         uint32_t subj = sub;
         if (!B.offs && B.fixed_w) {
-            const uint64_t cap = (0xffffff00ull / B.fixed_w) / kPaBlock * kPaBlock;
-            subj = cap < sub ? uint32_t(cap < kPaBlock ? kPaBlock : cap) : sub;
+            const uint64_t cap = (0xffffff00ull / B.fixed_w) / tile * tile;
+            subj = cap < sub ? uint32_t(cap < tile ? tile : cap) : sub;
         }
         // sub-batches of even size (a 17.6 M batch as 2 x 8.8 M, not 16 M +
         // 1.6 M: a small last sub-batch cannot fill the chip)
         if (B.n > subj) {
             const uint64_t ns = (B.n + subj - 1) / subj;
-            subj = uint32_t(((B.n + ns - 1) / ns + kPaBlock - 1) / kPaBlock * kPaBlock);
+            subj = uint32_t(((B.n + ns - 1) / ns + tile - 1) / tile * tile);
         }
         // the segmented PFADD (k_seg_*) for this batch, or pass C per sub-batch
         SegPlan P;
@@ -2369,7 +2397,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             const uint32_t ms = B.n - s0 < subj ? uint32_t(B.n - s0) : subj;
             A.fixed_w = B.fixed_w;
             A.n = ms;
-            A.ntiles = (ms + kPaBlock - 1) / kPaBlock;
+            A.ntiles = (ms + tile - 1) / tile;
             A.bytes = B.offs ? B.bytes : B.bytes + s0 * B.fixed_w;
             A.offs = B.offs ? B.offs + s0 : nullptr;
             A.slot = B.slot + s0;
@@ -2378,9 +2406,9 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             if (A.gcap)  // the group layout (C3/C5 by default)
                 hipLaunchKernelGGL((k_part_a3<11, 1024, true>), dim3(g2), dim3(512), 0, st, A);
             else if (flist && A.nunits < 512)  // C3/C5: 152 pairs, two counters per thread
-                hipLaunchKernelGGL((k_part_a3<11, 1024>), dim3(g2), dim3(512), 0, st, A);
+                hipLaunchKernelGGL((k_part_a3<11, 1024, false, kTileFl>), dim3(g2), dim3(512), 0, st, A);
             else if (flist)
-                hipLaunchKernelGGL((k_part_a3<11, 2048>), dim3(g2), dim3(512), 0, st, A);
+                hipLaunchKernelGGL((k_part_a3<11, 2048, false, kTileFl>), dim3(g2), dim3(512), 0, st, A);
             else if (km <= 11)
                 hipLaunchKernelGGL(k_part_a<11>, dim3(ga), dim3(kPaBlock), 0, st, A);
             else
@@ -2390,7 +2418,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             if (A.gcap)
                 hipLaunchKernelGGL((k_part_b<2, 4, true, true>), dim3(gb), dim3(kPbBlock), 0, st, A);
             else if (flist)
-                hipLaunchKernelGGL((k_part_b<2, 4, true>), dim3(gb), dim3(kPbBlock), 0, st, A);
+                hipLaunchKernelGGL((k_part_b<2, kPbRFl, true, false, kTileFl>), dim3(gb), dim3(kPbBlock), 0, st, A);
             else if (pairs)
                 hipLaunchKernelGGL(k_part_b<2>, dim3(gb), dim3(kPbBlock), 0, st, A);
             else
@@ -2410,9 +2438,9 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
                 if (hook) hook(hook_user, 3, 1, st);
             } else if (flist) {
                 const unsigned gc =
-                    (part_grid(ms, 1024 * kPbGroup, unsigned(cus) * SKE_PC_BLOCKS_PER_CU) + kPGroups - 1) /
+                    (part_grid(ms, kTileFl * kPbGroup, unsigned(cus) * SKE_PC_BLOCKS_PER_CU) + kPGroups - 1) /
                     kPGroups * kPGroups;
-                hipLaunchKernelGGL(k_part_c_fl<1024 / kPcFlBlock>, dim3(gc), dim3(kPcFlBlock), 0, st, A);
+                hipLaunchKernelGGL((k_part_c_fl<kPcFlT, kTileFl / kPcFlT, kTileFl>), dim3(gc), dim3(kPcFlT), 0, st, A);
             } else {
                 const unsigned gc = (part_grid(ms, kPcBlock * 2, unsigned(cus) * 8) + kPGroups - 1) / kPGroups * kPGroups;
                 hipLaunchKernelGGL(k_part_c<2>, dim3(gc), dim3(kPcBlock), 0, st, A);
