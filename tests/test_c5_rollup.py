@@ -91,5 +91,32 @@ def test_c5_campus_year_rollup(engine, orc):
     slab = torch.as_tensor(_Slab(), device="cuda")
     want = torch.amax(slab, dim=0).cpu().numpy()
     assert np.array_equal(engine.registers(nk), want)
+    # the same queries device-resident end to end (round 6: plans on the GPU,
+    # counts kept there, top / bottom-3 by torch.topk, PFMERGE over a device
+    # source list) equal the host-staged ones above
+    import rtsas_amd
+    from rtsas_amd.distributed import KeyMap, ShardedSketch
+    from rtsas_amd.processor import rank_top_bottom_dev
+    client = rtsas_amd.SketchClient(context=engine.ctx)
+    sk = ShardedSketch(client, 0, 1)
+    km = KeyMap(names, 1)
+    assert km.identity
+    kp = sk.plan_keys(km, np.arange(nk))
+    cdev = sk.pfcount_each_planned(kp)
+    assert cdev.is_cuda and np.array_equal(cdev.cpu().numpy(), counts)
+    assert rank_top_bottom_dev(cdev, 3) == (head, tail)  # names are in index order
+    plan = sk.plan(km, [np.arange(0, days), 7 * days + np.arange(days)])
+    assert sk.rollup_planned(plan, device=True).cpu().numpy().astype(np.uint64).tolist() == out.tolist()
+    engine.ctx.call("ske_hll_clear", nk)
+    campus, row = sk.pfmerge_planned(kp, nk)
+    assert np.array_equal(row.cpu().numpy()[0], want) and campus == orc.hll_count_regs(want)
+    # a device source list is range-checked on the device
+    bad = torch.tensor([0, nk + 5, 3], dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    with pytest.raises(rtsas_amd.SketchLibError):
+        engine.ctx.call("ske_hll_pfmerge_dev", nk, C.c_void_p(bad.data_ptr()), 3)
+    with pytest.raises(rtsas_amd.SketchLibError):
+        engine.ctx.call("ske_hll_pfcount_each", C.c_void_p(bad.data_ptr()), 3,
+                        C.c_void_p(torch.zeros(3, dtype=torch.int64, device="cuda").data_ptr()), 1)
     for b in batches:
         b.free()
