@@ -8,7 +8,7 @@ Zipf(1.1)-over-lectures x uniform-over-days stream of 8-digit ids with 10 %
 invalid swipes, and the HLL keys this rank owns (distributed.KeyMap:
 MurmurHash64A(key name) mod world over the 100k README-form key names; all
 of them at N = 1, ~12.5k per rank at N = 8).  One step = one K1 call over
-one resident batch of 2^27 swipes per GPU (C3's 1B-swipe stream in 8 steps;
+one resident batch of 2^28 swipes per GPU (C3's 1B-swipe stream in 4 steps;
 answers written, PFADD of the valid ones): the partitioned K1 in even
 sub-batches of 2^25 swipes (sketch_part.hip: hash + probe records,
 LDS-slice probes, answers + the segmented PFADD's records and level-2 sort),
@@ -72,10 +72,12 @@ K1_PASSES = 6  # PASS_NAMES[:6] are K1 kernels; the rest the stages of a host-fe
 PMC_ROUNDS = ["r06", "r05", "r04", "r03", "r02"]  # newest committed PMC summaries first
 VERIFY_KEYS = 64
 # swipes per GPU and step where it differs from the workload's own
-# step_swipes: C3 since round 5 takes 2^27 (its 1B-swipe stream in 8 steps;
-# the segmented PFADD streams each key window of the slab once per step, so
-# the step is sized to several register updates per slab line -- DESIGN.md §3)
-BENCH_STEP = {"c3": 1 << 27}
+# step_swipes: C3 takes 2^28 since round 6 (its 1B-swipe stream in 4 steps;
+# 2^27 in round 5, 16 M before).  The segmented PFADD streams each key window
+# of the slab once per step, ~0.64 ms whatever the step, so the step is sized
+# to many register updates per slab line: per 2^27 swipes the window pass
+# costs 0.85 ms at a 2^27 step and 0.53 ms at 2^28
+BENCH_STEP = {"c3": 1 << 28}
 
 
 def parse(argv=None):
@@ -519,7 +521,7 @@ def rollup_bench(run, dist, reps=3):
 def stream_1b(run, n_all, warm_pt, total=1 << 30):
     """north_star's workload as a whole: the 1B-event stream
     from a zeroed slab -- ceil(2^30 / n_all) steps of this run's batches
-    (0, 1, ...; 8 steps of 2^27 at N = 1, the whole stream on every rank's
+    (0, 1, ...; 4 steps of 2^28 at N = 1, the whole stream on every rank's
     share at N > 1), timed like the headline (barrier + synchronize on both
     sides, max over ranks), then the same cold stream replayed with a HIP
     event pair around every kernel for the per-pass split.  `warm_pt`: the

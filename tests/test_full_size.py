@@ -281,22 +281,23 @@ def test_c3_bench_shard_one_gpu(engine, orc):
     assert np.array_equal(got, regs)
 
 
-@pytest.mark.parametrize("world", [1, 8])
-def test_c3_bench_step_128m_segmented(engine, orc, world):
-    """C3 at bench.py's default step since round 5 (2^27 swipes per GPU: a
-    1B-swipe C3 stream in 8 steps), on one GPU's keys at N = 1 (100k Zipf
-    lecture-day keys, a 1.6 GB slab) and at N = 8 (synthetic.shard(c3, 8):
-    12.5k keys, 205 MB).  The auto choice takes the segmented PFADD at this
-    density (asserted through the pass timing kinds); every answer and every
-    register bit-exact vs the oracle (its multi-threaded per-event loop,
-    identical results to the sequential one).  N = 1 in the default
-    sub-batches (4 of 2^25 swipes), N = 8 in sub-batches of 2^24 (8)."""
+@pytest.mark.parametrize("world,n", [(1, 1 << 27), (8, 1 << 27), (1, 1 << 28)])
+def test_c3_bench_step_128m_segmented(engine, orc, world, n):
+    """C3 at bench.py's default steps: 2^27 swipes per GPU (round 5: a
+    1B-swipe C3 stream in 8 steps) and 2^28 (round 6: in 4 steps, 8
+    sub-batches feeding one window pass), on one GPU's keys at N = 1 (100k
+    Zipf lecture-day keys, a 1.6 GB slab) and at N = 8
+    (synthetic.shard(c3, 8): 12.5k keys, 205 MB).  The auto choice takes the
+    segmented PFADD at this density (asserted through the pass timing kinds);
+    every answer and every register bit-exact vs the oracle (its
+    multi-threaded per-event loop, identical results to the sequential one).
+    N = 1 in the default sub-batches (2^25 swipes), N = 8 in sub-batches of
+    2^24."""
     import os
     from rtsas_amd import synthetic
     from rtsas_amd.engine import DeviceBuffer
     w = synthetic.shard(synthetic.WORKLOADS["c3"], world)
     p = _setup(engine, w)
-    n = 1 << 27
     sub = 0 if world == 1 else 1 << 24
     engine.set_option("part_sub", sub)
     b = engine.swipe_batch(p, 0, n)
@@ -306,7 +307,7 @@ def test_c3_bench_step_128m_segmented(engine, orc, world):
     engine.swipes(0, b, out)
     pt = engine.pass_times(reset=True)
     engine.set_option("pass_timing", 0)
-    nsub = 4 if sub == 0 else 8
+    nsub = n // ((1 << 25) if sub == 0 else sub)
     assert pt[5][1] == 1 and pt[4][1] == nsub, pt  # one window pass, nsub sub-batches
     chain = orc.Chain(w.bf_capacity, w.bf_error)
     mb = engine.members_batch(p, 0, w.n_members)
