@@ -197,9 +197,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t part_rsrc(const void *p, uint3
 // 0.25 ms; bits 8 and 16 neutral to slightly slower; bit 32 makes pass C
 // 0.39 -> 0.59 ms (the raising CAS no longer finds its line near).  Default 7.
 // (Round 4, final kernels: 15 and 23 within 0.1 % of 7, profiles/r04_ab_nt.txt.)
-// Bit 64 (pass B's records) was always on before round 5.
+// Bit 64 (pass B's records) was always on before round 5 (default 71).
+// Round 6, the segmented PFADD at 2^28-swipe steps (profiles/r06_ab_nt.txt,
+// three sessions, N = 1 and the 8-way shard): pass B's record loads without
+// `nt` and the copy-out with it -- pass B 0.39 -> 0.37 ms per 2^25 sub-batch --
+// and C1's streams (bit 16) with it -- C1 0.116 -> 0.099: default 21 (1 | 4 |
+// 16), step 9.2 -> 8.9 ms; without bit 4, or with bit 64, pass B is back at 0.38+.
 #ifndef SKE_NT
-#define SKE_NT 71
+#define SKE_NT 21
 #endif
 // pass A3's id prefetch distance: 1 -- a tile's ids load after the previous
 // tile's atomics (from offsets loaded at that tile's start); 2 -- at the
