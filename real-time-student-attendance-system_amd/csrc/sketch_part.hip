@@ -222,6 +222,18 @@ template <int BIT, class T> __device__ __forceinline__ void nt_st(T *p, T v) {
     else *p = v;
 }
 template <int BIT> __device__ __forceinline__ constexpr int nt_aux() { return (SKE_NT & BIT) ? 2 : 0; }
+// The segmented PFADD's streams (SKE_NT2 bits): 1 C1's level-1 record
+// copy-out, 2 D's level-1 record loads, 4 D's level-2 record copy-out, 8 the
+// window pass's record loads, 16 its register-image loads (LDS-DMA), 32 its
+// line write-back.  Default 0 (round 5's policies).
+#ifndef SKE_NT2
+#define SKE_NT2 0
+#endif
+template <int BIT> __device__ __forceinline__ constexpr int nt2_aux() { return (SKE_NT2 & BIT) ? 2 : 0; }
+template <int BIT, class T> __device__ __forceinline__ void nt2_st(T *p, T v) {
+    if constexpr ((SKE_NT2 & BIT) != 0) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 
 struct PartId {
     uint32_t b, len;
@@ -1459,9 +1471,9 @@ __global__ void __launch_bounds__(T, SegC1<T>::WPE) k_seg_c1(const PartArgs A, c
         for (uint32_t u = 0; u < U; u++)
             if (pos[u] != 0xffffffffu) srec[cnt[pos[u] >> 16] + (pos[u] & 0xffffu)] = rec[u];
         lds_barrier();
-        uint4 *dst = reinterpret_cast<uint4 *>(S.r1 + size_t(r) * kSegRunSw);
-        const uint4 *src = reinterpret_cast<const uint4 *>(srec);
-        for (uint32_t j = tid; j * 4 < total; j += T) dst[j] = src[j];
+        part_u32x4 *dst = reinterpret_cast<part_u32x4 *>(S.r1 + size_t(r) * kSegRunSw);
+        const part_u32x4 *src = reinterpret_cast<const part_u32x4 *>(srec);
+        for (uint32_t j = tid; j * 4 < total; j += T) nt2_st<1>(dst + j, src[j]);
         // (the next run rewrites cnt, marks and srec only behind barriers
         // that every reader of this run's values has passed)
     }
@@ -1640,7 +1652,7 @@ __global__ void __launch_bounds__(T, SegD<T>::WPE) k_seg_d(const SegArgs S) {
 #pragma unroll
             for (uint32_t j = 0; j < R; j++) {
                 const uint32_t p = w0 + j * T + tid;
-                rec[j] = __builtin_amdgcn_raw_buffer_load_b32(rr1, p < w1 ? (sob[k[j]] + p) * 4 : kOOR, 0, 0);
+                rec[j] = __builtin_amdgcn_raw_buffer_load_b32(rr1, p < w1 ? (sob[k[j]] + p) * 4 : kOOR, 0, nt2_aux<2>());
             }
         } else {
             // (a sparse bucket's chunk over more runs than LDS stages: the
@@ -1683,9 +1695,9 @@ __global__ void __launch_bounds__(T, SegD<T>::WPE) k_seg_d(const SegArgs S) {
         for (uint32_t j = 0; j < R; j++)
             if (pos[j] != 0xffffffffu) sb[c2[pos[j] >> 16] + (pos[j] & 0xffffu)] = rec[j];
         lds_barrier();
-        uint4 *dst = reinterpret_cast<uint4 *>(r2 + size_t(q) * kSegChunk);
-        const uint4 *src = reinterpret_cast<const uint4 *>(sb);
-        for (uint32_t j = tid; j * 4 < total; j += T) dst[j] = src[j];
+        part_u32x4 *dst = reinterpret_cast<part_u32x4 *>(r2 + size_t(q) * kSegChunk);
+        const part_u32x4 *src = reinterpret_cast<const part_u32x4 *>(sb);
+        for (uint32_t j = tid; j * 4 < total; j += T) nt2_st<4>(dst + j, src[j]);
         // (the next chunk rewrites spp / sob / c2 only after the barriers
         // that every reader of this chunk's values has passed)
         if (!SKE_SEG_D_PIPE && qn < nq) {
@@ -1845,7 +1857,7 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
             const uint32_t piece = i * (T / 64) + wave;  // 1 KiB pieces
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 r, (__attribute__((address_space(3))) void *)(win + piece * 1024), 16,
-                int(piece * 1024 + lane * 16), 0, 0, 0);
+                int(piece * 1024 + lane * 16), 0, 0, nt2_aux<16>());
         }
     };
     // run x of window column w2 of the bucket staged in buffer pb
@@ -1987,7 +1999,7 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
                             const uint32_t f = r0 + c * 64 + lane;
                             if (f < f_hi) {
                                 while (rp[j + 1] <= f) j++;
-                                rec[c] = __builtin_amdgcn_raw_buffer_load_b32(rr2, (rb[j] + (f - rp[j])) * 4, 0, 0);
+                                rec[c] = __builtin_amdgcn_raw_buffer_load_b32(rr2, (rb[j] + (f - rp[j])) * 4, 0, nt2_aux<8>());
                             }
                         }
                     }
@@ -2037,7 +2049,7 @@ __global__ void __launch_bounds__(SegE<KLOG>::T, SegE<KLOG>::WPS) k_seg_e(const 
             for (uint32_t i = 0; i < NPC; i++) {
                 const uint32_t j = i * T + tid;
                 if (j < npc && dirty[j >> 3])
-                    reinterpret_cast<part_u32x4 *>(g)[j] = reinterpret_cast<const part_u32x4 *>(win)[j];
+                    nt2_st<32>(reinterpret_cast<part_u32x4 *>(g) + j, reinterpret_cast<const part_u32x4 *>(win)[j]);
             }
         }
         lds_barrier();  // win, dirty and hdr are rewritten by the next item
