@@ -201,10 +201,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t part_rsrc(const void *p, uint3
 // Round 6, the segmented PFADD at 2^28-swipe steps (profiles/r06_ab_nt.txt,
 // three sessions, N = 1 and the 8-way shard): pass B's record loads without
 // `nt` and the copy-out with it -- pass B 0.39 -> 0.37 ms per 2^25 sub-batch --
-// and C1's streams (bit 16) with it -- C1 0.116 -> 0.099: default 21 (1 | 4 |
-// 16), step 9.2 -> 8.9 ms; without bit 4, or with bit 64, pass B is back at 0.38+.
+// and C1's streams (bit 16) with it -- C1 0.116 -> 0.099 -- and pass A's HLL
+// words (bit 8) with it (pass B 0.370 -> 0.364): default 29 (1 | 4 | 8 | 16),
+// step 9.2 -> 8.85-8.9 ms; without bit 4, or with bit 64, pass B is back at
+// 0.38+; bit 2 (pass A's ids) costs pass B 0.01.
 #ifndef SKE_NT
-#define SKE_NT 21
+#define SKE_NT 29
 #endif
 // pass A3's id prefetch distance: 1 -- a tile's ids load after the previous
 // tile's atomics (from offsets loaded at that tile's start); 2 -- at the
