@@ -1342,7 +1342,27 @@ struct SegArgs {
     uint4 *mlist;     // cut windows (window, first copy, slices)
     uint8_t *copies;  // [ccap][window bytes] LDS copies of cut windows' slices
     uint32_t ccap;    // copies (and queue entries) available
+    // the arena form (SKE_SEG_ARENA): level-1 records in chunk slots of r1
+    uint32_t *fill;   // [nsub][nb1 + 1] records reserved per bucket; [s][nb1] = chunk slots taken
+    uint32_t *ctab;   // [nb1][kmaxc] chunk c of bucket h: its slot + 1 (0: not yet placed)
+    uint32_t kmaxc;   // chunks a bucket can have in a sub-batch
+    uint32_t kstat;   // chunk c < kstat of bucket h sits in slot h * kstat + c; later chunks take
+                      // slots nb1 * kstat + (counter), named in ctab
 };
+
+// The arena form of C1 -> D (SKE_SEG_ARENA 1).  C1 reserves each bucket's
+// records of a run with one atomic add on the bucket's fill count (issued
+// before the run's scan and placement, which hide its latency), so a
+// bucket's records are one contiguous sequence of the sub-batch; the sequence
+// lives in 8 192-record chunks.  The first kstat chunks of bucket h have the
+// fixed slots h * kstat + c of r1 (about twice a bucket's mean); a later
+// chunk of a heavy bucket takes a slot from a counter, claimed by the run
+// whose reservation holds the chunk's first record, which publishes it in
+// ctab before it waits for any other.  D then reads whole chunks: no scan
+// pass S, no run tables, no gather.
+#ifndef SKE_SEG_ARENA
+#define SKE_SEG_ARENA 0
+#endif
 
 // Exclusive prefix of one value per thread over the block (blockDim a
 // multiple of 64); every thread also gets the total.  `ws`: blockDim / 64
@@ -1374,6 +1394,47 @@ __device__ __forceinline__ uint32_t seg_last_le(const uint32_t *a, uint32_t n, u
     return lo;
 }
 
+// Arena: the slots of the (at most two) chunks that bucket h's cv records
+// of a run, from sequence index base on, fall in, packed as slot0 | slot1 <<
+// 14 | (chunk0 & 1) << 28.  A fixed chunk (c < kstat) needs nothing; a
+// counted chunk whose first record is in this reservation takes its slot
+// here and publishes it; one begun by an earlier reservation is waited for
+// (its owner took its fill index before this one did, so it is resident and
+// publishes without waiting on anything).  A wait that never ends sets error
+// bit 4 (reported as the call's error) after ~1 s.
+static_assert(kSegChunk == 8192, "the arena's chunk arithmetic");
+__device__ __forceinline__ uint32_t seg_arena_slot(const SegArgs &S, unsigned int *err, uint32_t h, uint32_t c,
+                                                   bool own) {
+    if (c < S.kstat) return h * S.kstat + c;
+    uint32_t *ct = S.ctab + size_t(h) * S.kmaxc + c;
+    if (own) {
+        const uint32_t d = atomicAdd(S.fill + size_t(S.s) * (S.nb1 + 1) + S.nb1, 1u);
+        __hip_atomic_store(ct, d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return S.nb1 * S.kstat + d;
+    }
+    uint32_t v = 0;
+    for (uint32_t it = 0; it < (1u << 22); it++) {
+        v = __hip_atomic_load(ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v) break;
+        __builtin_amdgcn_s_sleep(8);
+    }
+    if (!v) {
+        atomicOr(err, 4u);
+        v = 1;
+    }
+    return S.nb1 * S.kstat + v - 1;
+}
+__device__ __forceinline__ uint32_t seg_arena_slots(const SegArgs &S, unsigned int *err, uint32_t h, uint32_t cv,
+                                                    uint32_t base) {
+    const uint32_t c0 = base >> 13, c1 = (base + cv - 1) >> 13;  // cv <= 8192: c1 <= c0 + 1
+    // (chunk c1 > c0 starts inside this reservation: it is ours, published
+    // before we wait for c0)
+    const uint32_t s1 = c1 != c0 ? seg_arena_slot(S, err, h, c1, true) : 0u;
+    __asm__ volatile("" ::: "memory");
+    const uint32_t s0 = seg_arena_slot(S, err, h, c0, (base & (kSegChunk - 1)) == 0);
+    return s0 | ((c1 != c0 ? s1 : s0) << 14) | ((c0 & 1u) << 28);
+}
+
 // C1's block: T threads, U = kSegRunSw / T swipes of a run each (1024 x 8 at
 // two blocks per CU, or 512 x 16 at three: three runs in flight per CU; with
 // 1536-swipe tiles 768 x 16 at two)
@@ -1390,9 +1451,10 @@ template <uint32_t T> struct SegC1 {
 template <uint32_t T>
 __global__ void __launch_bounds__(T, SegC1<T>::WPE) k_seg_c1(const PartArgs A, const SegArgs S) {
     constexpr uint32_t U = SegC1<T>::U, PT = SegC1<T>::PT;
-    __shared__ uint16_t mark[kSegRunSw];
+    __shared__ __attribute__((aligned(16))) uint16_t mark[kSegRunSw];
     __shared__ __attribute__((aligned(16))) uint32_t srec[kSegRunSw];
     __shared__ uint32_t cnt[kSegMaxB1 + 1];
+    __shared__ uint32_t slt[SKE_SEG_ARENA ? kSegMaxB1 : 1];
     __shared__ uint32_t ws[T / 64];
     const uint32_t tid = threadIdx.x;
     for (uint32_t j = tid; j < kSegRunSw; j += T) mark[j] = 0;
@@ -1462,20 +1524,75 @@ __global__ void __launch_bounds__(T, SegC1<T>::WPE) k_seg_c1(const PartArgs A, c
         }
         lds_barrier();
         uint32_t total;
-        const uint32_t ex = seg_scan(tid < S.nb1 ? cnt[tid] : 0u, ws, total);
+        const uint32_t cv = tid < S.nb1 ? cnt[tid] : 0u;
+        // (arena: the bucket's reservation, its result first used after the placement)
+        // (a buffer atomic: its address is one VGPR, rebuilt from tid, so no
+        // 64-bit pointer is kept live -- and spilled -- across the run)
+        uint32_t abase = 0;
+        if (SKE_SEG_ARENA && cv)
+            abase = uint32_t(__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(
+                int(cv), part_rsrc(S.fill, S.nsub * (S.nb1 + 1) * 4), int((S.s * (S.nb1 + 1) + tid) * 4), 0, 0));
+        const uint32_t ex = seg_scan(cv, ws, total);
         if (tid < S.nb1) {
             cnt[tid] = ex;
-            S.o1[size_t(tid) * kSegMaxRuns + r] = ex;
+            if (!SKE_SEG_ARENA) S.o1[size_t(tid) * kSegMaxRuns + r] = ex;
         }
-        if (tid == 0) S.o1[size_t(S.nb1) * kSegMaxRuns + r] = total;  // [nb1] = the run's total
+        if (!SKE_SEG_ARENA && tid == 0) S.o1[size_t(S.nb1) * kSegMaxRuns + r] = total;  // [nb1] = the run's total
         lds_barrier();
 #pragma unroll
         for (uint32_t u = 0; u < U; u++)
-            if (pos[u] != 0xffffffffu) srec[cnt[pos[u] >> 16] + (pos[u] & 0xffffu)] = rec[u];
-        lds_barrier();
-        part_u32x4 *dst = reinterpret_cast<part_u32x4 *>(S.r1 + size_t(r) * kSegRunSw);
-        const part_u32x4 *src = reinterpret_cast<const part_u32x4 *>(srec);
-        for (uint32_t j = tid; j * 4 < total; j += T) nt2_st<1>(dst + j, src[j]);
+            if (pos[u] != 0xffffffffu) {
+                const uint32_t b = pos[u] >> 16, at = cnt[b] + (pos[u] & 0xffffu);
+                srec[at] = rec[u];
+                // (arena: the record's bucket, tagged so that no run's epoch
+                // (<= kSegMaxRuns < 0x8000) ever equals it)
+                if (SKE_SEG_ARENA) mark[at] = uint16_t(0x8000u | b);
+            }
+        if (SKE_SEG_ARENA) {
+            // the run's reservations (after the placement, so that no record
+            // registers are live across them); record j of the run (bucket h)
+            // is then the bucket's sequence index i = j + (base - start of h
+            // in the run), in the bucket's first or second chunk of this
+            // reservation (told apart by i's chunk parity)
+            const uint32_t aslot = cv ? seg_arena_slots(S, A.err, tid, cv, abase) : 0u;
+            lds_barrier();  // the placement's reads of cnt are done
+            if (tid < S.nb1) {
+                cnt[tid] = abase - ex;
+                slt[tid] = aslot;
+            }
+            lds_barrier();
+            // four records per thread: one 16-B store (dword-aligned) when
+            // they share a bucket and a chunk -- most of a run's ~57-record
+            // segments -- else one store each
+            typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+            auto slot_of = [](uint32_t i, uint32_t v) {
+                return ((i >> 13) & 1u) == (v >> 28) ? (v & 0x3fffu) : ((v >> 14) & 0x3fffu);
+            };
+            for (uint32_t g = tid; g * 4 < total; g += T) {
+                const uint32_t j = g * 4;
+                const part_u32x4 v = reinterpret_cast<const part_u32x4 *>(srec)[g];
+                const uint2 mk = reinterpret_cast<const uint2 *>(mark)[g];
+                const uint32_t m[4] = {mk.x & 0xffffu, mk.x >> 16, mk.y & 0xffffu, mk.y >> 16};
+                const uint32_t h0 = m[0] & (kSegMaxB1 - 1), i0 = j + cnt[h0];
+                if (j + 4 <= total && m[3] == m[0] && (i0 & (kSegChunk - 1)) <= kSegChunk - 4) {
+                    *reinterpret_cast<u32x4a *>(S.r1 + size_t(slot_of(i0, slt[h0])) * kSegChunk +
+                                                (i0 & (kSegChunk - 1))) = u32x4a{v.x, v.y, v.z, v.w};
+                } else {
+#pragma unroll
+                    for (uint32_t e = 0; e < 4; e++) {
+                        if (j + e >= total) break;
+                        const uint32_t h = m[e] & (kSegMaxB1 - 1), i = j + e + cnt[h];
+                        S.r1[size_t(slot_of(i, slt[h])) * kSegChunk + (i & (kSegChunk - 1))] = v[e];
+                    }
+                }
+            }
+            lds_barrier();  // cnt, slt and marks are rewritten by the next run
+        } else {
+            lds_barrier();
+            part_u32x4 *dst = reinterpret_cast<part_u32x4 *>(S.r1 + size_t(r) * kSegRunSw);
+            const part_u32x4 *src = reinterpret_cast<const part_u32x4 *>(srec);
+            for (uint32_t j = tid; j * 4 < total; j += T) nt2_st<1>(dst + j, src[j]);
+        }
         // (the next run rewrites cnt, marks and srec only behind barriers
         // that every reader of this run's values has passed)
     }
@@ -1708,6 +1825,101 @@ __global__ void __launch_bounds__(T, SegD<T>::WPE) k_seg_d(const SegArgs S) {
         }
         q = qn;
         cur = nx;
+    }
+}
+
+// D of the arena form: one block per chunk of the sub-batch (grid-stride, in
+// bucket order), its slot fixed or from ctab, its records read whole (16-B loads), then
+// the same window sort and outputs as k_seg_d (o2 / r2 row q = the bucket's
+// first chunk + chunk, so E is unchanged).  It clears the chunk's ctab entry
+// for the next sub-batch.
+template <uint32_t T> struct SegDA {
+    static constexpr uint32_t R = kSegChunk / T;        // records per thread
+    static constexpr uint32_t BPC = T == 1024 ? 2 : 3;  // blocks per CU (80 VGPRs; LDS ~39 KiB each)
+    static constexpr uint32_t WPE = BPC * (T / 64) / 4;
+};
+template <uint32_t T>
+__global__ void __launch_bounds__(T, SegDA<T>::WPE) k_seg_da(const SegArgs S) {
+    constexpr uint32_t R = SegDA<T>::R;
+    static_assert(R % 4 == 0 && kSegMaxWpb <= T && kSegMaxB1 <= T, "D geometry");
+    __shared__ uint32_t tot[kSegMaxB1], cbl[kSegMaxB1 + 1];
+    __shared__ uint32_t c2[kSegMaxWpb + 1];
+    __shared__ __attribute__((aligned(16))) uint32_t sb[kSegChunk];
+    __shared__ uint32_t ws[T / 64];
+    const uint32_t tid = threadIdx.x, wpb = 1u << S.wlog;
+    const uint32_t *fl = S.fill + size_t(S.s) * (S.nb1 + 1);
+    uint32_t t = 0;
+    if (tid < S.nb1) {
+        t = fl[tid];
+        tot[tid] = t;
+    }
+    uint32_t nq;
+    const uint32_t cbase = seg_scan(tid < S.nb1 ? (t + kSegChunk - 1) / kSegChunk : 0u, ws, nq);
+    if (tid < S.nb1) {
+        cbl[tid] = cbase;
+        if (blockIdx.x == 0) S.cb[size_t(S.s) * (S.nb1 + 1) + tid] = cbase;
+    }
+    if (tid == 0 && blockIdx.x == 0) S.cb[size_t(S.s) * (S.nb1 + 1) + S.nb1] = nq;
+    lds_barrier();
+    uint32_t *r2 = S.r2 + size_t(S.s) * S.maxch * kSegChunk;
+    uint32_t *o2 = S.o2 + size_t(S.s) * S.maxch * (wpb + 1);
+    // chunk q of the sub-batch (bucket order, dealt round robin): bucket h,
+    // its chunk c, in a fixed slot or (c >= kstat) the counted one ctab names
+    const uint32_t nstat = S.nb1 * S.kstat, nslot = nstat + fl[S.nb1];
+    const __amdgpu_buffer_rsrc_t rr1 = part_rsrc(S.r1, nslot * kSegChunk * 4);
+    for (uint32_t q = blockIdx.x; q < nq; q += gridDim.x) {
+        const uint32_t h = __builtin_amdgcn_readfirstlane(seg_last_le(cbl, S.nb1, q));  // (empty buckets share
+        const uint32_t c = q - cbl[h];                                                   // the next one's base)
+        uint32_t p = h * S.kstat + c;
+        if (c >= S.kstat) {
+            p = nstat + __builtin_amdgcn_readfirstlane(S.ctab[size_t(h) * S.kmaxc + c]) - 1;
+            lds_barrier();  // every lane has read the entry
+            if (tid == 0) S.ctab[size_t(h) * S.kmaxc + c] = 0;
+        }
+        const uint32_t w0 = c * kSegChunk, th = tot[h];
+        const uint32_t n = th - w0 < kSegChunk ? th - w0 : kSegChunk;
+        uint32_t rec[R];
+#pragma unroll
+        for (uint32_t k = 0; k < R / 4; k++) {
+            const uint32_t x = (k * T + tid) * 4;  // the piece's first record in the chunk
+            const part_u32x4 v = __builtin_bit_cast(
+                part_u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr1, x < n ? (p * kSegChunk + x) * 4 : kOOR, 0,
+                                                                  nt2_aux<2>()));
+            rec[4 * k] = v.x;
+            rec[4 * k + 1] = v.y;
+            rec[4 * k + 2] = v.z;
+            rec[4 * k + 3] = v.w;
+        }
+        for (uint32_t j = tid; j <= wpb; j += T) c2[j] = 0;
+        lds_barrier();
+        uint32_t pos[R];
+#pragma unroll
+        for (uint32_t j = 0; j < R; j++) {
+            pos[j] = 0xffffffffu;
+            if ((j / 4 * T + tid) * 4 + j % 4 < n) {
+                const uint32_t w2 = (rec[j] >> (kSegRecShift + S.klog)) & (wpb - 1);
+                pos[j] = (w2 << 16) | atomicAdd(&c2[w2], 1u);
+            }
+        }
+        lds_barrier();
+        uint32_t total;
+        const uint32_t ex = seg_scan(tid < wpb ? c2[tid] : 0u, ws, total);
+        if (tid < wpb) {
+            c2[tid] = ex;
+            o2[size_t(q) * (wpb + 1) + tid] = ex;
+        }
+        if (tid == 0) o2[size_t(q) * (wpb + 1) + wpb] = total;
+        lds_barrier();
+#pragma unroll
+        for (uint32_t j = 0; j < R; j++)
+            if (pos[j] != 0xffffffffu) sb[c2[pos[j] >> 16] + (pos[j] & 0xffffu)] = rec[j];
+        lds_barrier();
+        part_u32x4 *dst = reinterpret_cast<part_u32x4 *>(r2 + size_t(q) * kSegChunk);
+        const part_u32x4 *src = reinterpret_cast<const part_u32x4 *>(sb);
+        for (uint32_t j = tid; j * 4 < total; j += T) nt2_st<4>(dst + j, src[j]);
+        // (the next chunk rewrites c2 before its first barrier: the readers
+        // of this chunk's c2 passed the barrier before the copy-out; sb is
+        // rewritten only after two more barriers)
     }
 }
 
@@ -2286,10 +2498,24 @@ static hipError_t seg_scratch(const SegPlan &P, uint32_t sub, uint64_t n, Scratc
     const uint64_t m = n < sub ? n : sub;
     const uint64_t mg = std::min<uint64_t>(n, uint64_t(P.nsub) * sub);  // swipes of one window pass
     hipError_t e = hipSuccess;
-    S->r1 = (uint32_t *)scratch_get(scr, 32, size_t((m + kSegRunSw - 1) / kSegRunSw) * kSegRunSw * 4, &e);
-    if (e == hipSuccess) S->o1 = (uint32_t *)scratch_get(scr, 33, size_t(P.nb1 + 1) * kSegMaxRuns * 4, &e);
-    if (e == hipSuccess) S->p1 = (uint32_t *)scratch_get(scr, 34, size_t(P.nb1) * (kSegMaxRuns + 1) * 4, &e);
-    if (e == hipSuccess) S->cst = (uint32_t *)scratch_get(scr, 35, size_t(P.nb1) * (kSegMaxRuns + 1) * 4, &e);
+    if (SKE_SEG_ARENA) {
+        // chunk slots: about twice a bucket's mean fixed per bucket, and as
+        // many counted ones as the sub-batch could ever need (every bucket's
+        // last chunk may be partial); slot numbers < 2^14 (k_seg_c1's packing)
+        const uint64_t ch = (m + kSegChunk - 1) / kSegChunk, dyn = ch + P.nb1;
+        uint64_t kst = 2 * ((ch + P.nb1 - 1) / P.nb1) + 2;
+        kst = std::min<uint64_t>(kst, ((1u << 14) - 1 - dyn) / P.nb1);
+        S->kstat = uint32_t(kst);
+        S->kmaxc = uint32_t(ch + 1);
+        S->r1 = (uint32_t *)scratch_get(scr, 32, size_t(P.nb1 * kst + dyn) * kSegChunk * 4, &e);
+        if (e == hipSuccess) S->fill = (uint32_t *)scratch_get(scr, 40, size_t(P.nsub) * (P.nb1 + 1) * 4, &e);
+        if (e == hipSuccess) S->ctab = (uint32_t *)scratch_get_zeroed(scr, 41, size_t(P.nb1) * S->kmaxc * 4, &e);
+    } else {
+        S->r1 = (uint32_t *)scratch_get(scr, 32, size_t((m + kSegRunSw - 1) / kSegRunSw) * kSegRunSw * 4, &e);
+        if (e == hipSuccess) S->o1 = (uint32_t *)scratch_get(scr, 33, size_t(P.nb1 + 1) * kSegMaxRuns * 4, &e);
+        if (e == hipSuccess) S->p1 = (uint32_t *)scratch_get(scr, 34, size_t(P.nb1) * (kSegMaxRuns + 1) * 4, &e);
+        if (e == hipSuccess) S->cst = (uint32_t *)scratch_get(scr, 35, size_t(P.nb1) * (kSegMaxRuns + 1) * 4, &e);
+    }
     if (e == hipSuccess)
         S->r2 = (uint32_t *)scratch_get(scr, 36, size_t(P.nsub) * P.maxch * kSegChunk * 4, &e);
     if (e == hipSuccess)
@@ -2447,13 +2673,22 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             if (seg) {
                 S.s = si % P.nsub;
                 S.nruns = (A.ntiles + kSegRunTiles - 1) / kSegRunTiles;
+                if (SKE_SEG_ARENA && S.s == 0) {  // the group's fill counts
+                    e = hipMemsetAsync(S.fill, 0, size_t(P.nsub) * (P.nb1 + 1) * 4, st);
+                    if (e != hipSuccess) return e;
+                }
                 hipLaunchKernelGGL(k_seg_c1<SKE_SEG_C1T>, dim3(std::min(S.nruns, unsigned(cus) * SegC1<SKE_SEG_C1T>::BPC)),
                                    dim3(SKE_SEG_C1T), 0, st, A, S);
                 if (hook) hook(hook_user, 2, 1, st);
                 if (hook) hook(hook_user, 3, 0, st);
-                hipLaunchKernelGGL(k_seg_scan, dim3(S.nb1), dim3(1024), 0, st, S);
-                hipLaunchKernelGGL(k_seg_d<SKE_SEG_DT>, dim3(unsigned(cus) * SegD<SKE_SEG_DT>::BPC), dim3(SKE_SEG_DT),
-                                   0, st, S);
+                if (SKE_SEG_ARENA) {
+                    hipLaunchKernelGGL(k_seg_da<SKE_SEG_DT>, dim3(unsigned(cus) * SegDA<SKE_SEG_DT>::BPC),
+                                       dim3(SKE_SEG_DT), 0, st, S);
+                } else {
+                    hipLaunchKernelGGL(k_seg_scan, dim3(S.nb1), dim3(1024), 0, st, S);
+                    hipLaunchKernelGGL(k_seg_d<SKE_SEG_DT>, dim3(unsigned(cus) * SegD<SKE_SEG_DT>::BPC),
+                                       dim3(SKE_SEG_DT), 0, st, S);
+                }
                 if (hook) hook(hook_user, 3, 1, st);
             } else if (flist) {
                 const unsigned gc =

@@ -23,6 +23,8 @@ ROUND6 = os.environ.get("SEG_D_TEMPLATE", "1") == "1"  # round 6: k_seg_d<T> (ro
 plan = {"k_part_a": (["k_part_a3"], SKIP_SUB), "k_part_b": (["k_part_b"], SKIP_SUB),
         "k_part_c": (["k_seg_c1"], SKIP_SUB), "k_seg_d": (["k_seg_scan", "k_seg_d<" if ROUND6 else "k_seg_d("], SKIP_SUB),
         "k_seg_e": (["k_seg_e<1, false>", "k_seg_e<1, true>", "k_seg_m<1>"], SKIP_STEP)}
+if os.environ.get("SEG_ARENA") == "1":  # the arena form: D alone (k_seg_da), no scan pass
+    plan["k_seg_d"] = (["k_seg_da<"], SKIP_SUB)
 for name, (kernels, skip) in plan.items():
     parts = {k: summarise(root, k, skip) for k in kernels}
     mean = {}
