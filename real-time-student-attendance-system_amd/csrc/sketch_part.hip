@@ -1291,14 +1291,19 @@ __global__ void __launch_bounds__(BT) k_part_c_fl(const PartArgs A) {
 //                   and for each valid swipe one 4-byte record
 //                   (slot-in-bucket << 20 | register << 6 | rank),
 //                   counting-sorted in LDS by level-1 bucket (slot >> s1,
-//                   <= 512 buckets) and written as the run's block of
+//                   <= 512 buckets).  Arena form (default): each bucket's
+//                   records of the run reserved in the bucket's contiguous
+//                   sequence of the sub-batch (one atomic add) and stored
+//                   into its 8192-record chunk slots.  Run-table form
+//                   (SKE_SEG_ARENA 0): written as the run's block of
 //                   records; o1[bucket][run] = the bucket's start in it.
-//   S  (k_seg_scan) per bucket: prefix of its run lengths over the runs,
-//                   and the run holding the first record of each of its
-//                   8192-record level-2 chunks.
-//   D  (k_seg_d)    per chunk: its records gathered from the runs,
-//                   counting-sorted in LDS by window (2^klog keys) within
-//                   the bucket; o2[chunk][window] = the window's start.
+//   S  (k_seg_scan) run-table form only: per bucket, prefix of its run
+//                   lengths over the runs, and the run holding the first
+//                   record of each of its 8192-record level-2 chunks.
+//   D  (k_seg_da /  per chunk: its records (arena: read whole; run-table
+//       k_seg_d)    form: gathered from the runs), counting-sorted in LDS
+//                   by window (2^klog keys) within the bucket;
+//                   o2[chunk][window] = the window's start.
 //   E  (k_seg_e)    per window, once per call (after every sub-batch's C1,
 //                   S, D): its records' runs over every chunk of its bucket;
 //                   with at least dense_min records the window's registers
@@ -1343,7 +1348,8 @@ struct SegArgs {
     uint8_t *copies;  // [ccap][window bytes] LDS copies of cut windows' slices
     uint32_t ccap;    // copies (and queue entries) available
     // the arena form (SKE_SEG_ARENA): level-1 records in chunk slots of r1
-    uint32_t *fill;   // [nsub][nb1 + 1] records reserved per bucket; [s][nb1] = chunk slots taken
+    uint32_t *fill;   // [nsub][nb1 + 1] (x kSegFillStride words) records reserved per bucket; [s][nb1] =
+                      // counted chunk slots taken
     uint32_t *ctab;   // [nb1][kmaxc] chunk c of bucket h: its slot + 1 (0: not yet placed)
     uint32_t kmaxc;   // chunks a bucket can have in a sub-batch
     uint32_t kstat;   // chunk c < kstat of bucket h sits in slot h * kstat + c; later chunks take
@@ -1360,8 +1366,12 @@ struct SegArgs {
 // whose reservation holds the chunk's first record, which publishes it in
 // ctab before it waits for any other.  D then reads whole chunks: no scan
 // pass S, no run tables, no gather.
+// Measured at the 2^28 default step (profiles/r06_ab_seg_arena.txt): C1 +
+// D 0.195 -> 0.178 ms per 2^25 sub-batch at N = 1 (C1 0.100 -> 0.119, S + D
+// 0.095 -> 0.059), 0.193 -> 0.174 at the 8-way shard; step 8.87 -> 8.73 ms.
+// 0: round 6's run-table form (k_seg_scan + k_seg_d).
 #ifndef SKE_SEG_ARENA
-#define SKE_SEG_ARENA 0
+#define SKE_SEG_ARENA 1
 #endif
 
 // Exclusive prefix of one value per thread over the block (blockDim a
@@ -1403,12 +1413,21 @@ __device__ __forceinline__ uint32_t seg_last_le(const uint32_t *a, uint32_t n, u
 // publishes without waiting on anything).  A wait that never ends sets error
 // bit 4 (reported as the call's error) after ~1 s.
 static_assert(kSegChunk == 8192, "the arena's chunk arithmetic");
+// fill counts 256 B apart: every run adds to every bucket's, and counters
+// packed in a few lines would queue on the few memory channels holding them
+#ifndef SKE_SEG_FILL_STRIDE
+#define SKE_SEG_FILL_STRIDE 64
+#endif
+constexpr uint32_t kSegFillStride = SKE_SEG_FILL_STRIDE;
+__device__ __forceinline__ uint32_t seg_fill_at(const SegArgs &S, uint32_t h) {
+    return (S.s * (S.nb1 + 1) + h) * kSegFillStride;
+}
 __device__ __forceinline__ uint32_t seg_arena_slot(const SegArgs &S, unsigned int *err, uint32_t h, uint32_t c,
                                                    bool own) {
     if (c < S.kstat) return h * S.kstat + c;
     uint32_t *ct = S.ctab + size_t(h) * S.kmaxc + c;
     if (own) {
-        const uint32_t d = atomicAdd(S.fill + size_t(S.s) * (S.nb1 + 1) + S.nb1, 1u);
+        const uint32_t d = atomicAdd(S.fill + seg_fill_at(S, S.nb1), 1u);
         __hip_atomic_store(ct, d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return S.nb1 * S.kstat + d;
     }
@@ -1531,7 +1550,7 @@ __global__ void __launch_bounds__(T, SegC1<T>::WPE) k_seg_c1(const PartArgs A, c
         uint32_t abase = 0;
         if (SKE_SEG_ARENA && cv)
             abase = uint32_t(__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(
-                int(cv), part_rsrc(S.fill, S.nsub * (S.nb1 + 1) * 4), int((S.s * (S.nb1 + 1) + tid) * 4), 0, 0));
+                int(cv), part_rsrc(S.fill, S.nsub * (S.nb1 + 1) * kSegFillStride * 4), int(seg_fill_at(S, tid) * 4), 0, 0));
         const uint32_t ex = seg_scan(cv, ws, total);
         if (tid < S.nb1) {
             cnt[tid] = ex;
@@ -1847,10 +1866,10 @@ __global__ void __launch_bounds__(T, SegDA<T>::WPE) k_seg_da(const SegArgs S) {
     __shared__ __attribute__((aligned(16))) uint32_t sb[kSegChunk];
     __shared__ uint32_t ws[T / 64];
     const uint32_t tid = threadIdx.x, wpb = 1u << S.wlog;
-    const uint32_t *fl = S.fill + size_t(S.s) * (S.nb1 + 1);
+    const uint32_t *fl = S.fill + seg_fill_at(S, 0);
     uint32_t t = 0;
     if (tid < S.nb1) {
-        t = fl[tid];
+        t = fl[tid * kSegFillStride];
         tot[tid] = t;
     }
     uint32_t nq;
@@ -1865,7 +1884,7 @@ __global__ void __launch_bounds__(T, SegDA<T>::WPE) k_seg_da(const SegArgs S) {
     uint32_t *o2 = S.o2 + size_t(S.s) * S.maxch * (wpb + 1);
     // chunk q of the sub-batch (bucket order, dealt round robin): bucket h,
     // its chunk c, in a fixed slot or (c >= kstat) the counted one ctab names
-    const uint32_t nstat = S.nb1 * S.kstat, nslot = nstat + fl[S.nb1];
+    const uint32_t nstat = S.nb1 * S.kstat, nslot = nstat + fl[S.nb1 * kSegFillStride];
     const __amdgpu_buffer_rsrc_t rr1 = part_rsrc(S.r1, nslot * kSegChunk * 4);
     for (uint32_t q = blockIdx.x; q < nq; q += gridDim.x) {
         const uint32_t h = __builtin_amdgcn_readfirstlane(seg_last_le(cbl, S.nb1, q));  // (empty buckets share
@@ -2508,7 +2527,8 @@ static hipError_t seg_scratch(const SegPlan &P, uint32_t sub, uint64_t n, Scratc
         S->kstat = uint32_t(kst);
         S->kmaxc = uint32_t(ch + 1);
         S->r1 = (uint32_t *)scratch_get(scr, 32, size_t(P.nb1 * kst + dyn) * kSegChunk * 4, &e);
-        if (e == hipSuccess) S->fill = (uint32_t *)scratch_get(scr, 40, size_t(P.nsub) * (P.nb1 + 1) * 4, &e);
+        if (e == hipSuccess)
+            S->fill = (uint32_t *)scratch_get(scr, 40, size_t(P.nsub) * (P.nb1 + 1) * kSegFillStride * 4, &e);
         if (e == hipSuccess) S->ctab = (uint32_t *)scratch_get_zeroed(scr, 41, size_t(P.nb1) * S->kmaxc * 4, &e);
     } else {
         S->r1 = (uint32_t *)scratch_get(scr, 32, size_t((m + kSegRunSw - 1) / kSegRunSw) * kSegRunSw * 4, &e);
@@ -2674,7 +2694,7 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
                 S.s = si % P.nsub;
                 S.nruns = (A.ntiles + kSegRunTiles - 1) / kSegRunTiles;
                 if (SKE_SEG_ARENA && S.s == 0) {  // the group's fill counts
-                    e = hipMemsetAsync(S.fill, 0, size_t(P.nsub) * (P.nb1 + 1) * 4, st);
+                    e = hipMemsetAsync(S.fill, 0, size_t(P.nsub) * (P.nb1 + 1) * kSegFillStride * 4, st);
                     if (e != hipSuccess) return e;
                 }
                 hipLaunchKernelGGL(k_seg_c1<SKE_SEG_C1T>, dim3(std::min(S.nruns, unsigned(cus) * SegC1<SKE_SEG_C1T>::BPC)),

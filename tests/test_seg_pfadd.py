@@ -1,4 +1,4 @@
-"""The segmented PFADD (sketch_part.hip k_seg_c1 / k_seg_scan / k_seg_d /
+"""The segmented PFADD (sketch_part.hip k_seg_c1 / k_seg_da (or k_seg_scan + k_seg_d) /
 k_seg_e): pass C of the one-link partitioned K1 when a batch's register
 updates are dense in the slab -- valid swipes' (register, rank) records
 bucketed by key, each window of keys staged in LDS, raised there and its

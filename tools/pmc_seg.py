@@ -1,7 +1,7 @@
 """Per-kernel PMC summaries of the default C3 step (partitioned K1 +
 segmented PFADD) from tools/gpu_pmc_seg.sh's passes, named by bench.py's pass
 kinds: k_part_a, k_part_b, k_part_c (the segmented C1, k_seg_c1), k_seg_d
-(k_seg_scan + k_seg_d, per sub-batch), k_seg_e (window pass E1 + E2 + merge
+(k_seg_da per sub-batch; SEG_ARENA=0: k_seg_scan + k_seg_d), k_seg_e (window pass E1 + E2 + merge
 M, per step).  Warm-up dispatches are skipped (2 steps of NSUB sub-batches;
 env NSUB, default 4: 2^27 swipes in sub-batches of 2^25).  Every summary
 records the swipes one launch covers (env STEP_SWIPES / NSUB; the window pass:
@@ -23,7 +23,7 @@ ROUND6 = os.environ.get("SEG_D_TEMPLATE", "1") == "1"  # round 6: k_seg_d<T> (ro
 plan = {"k_part_a": (["k_part_a3"], SKIP_SUB), "k_part_b": (["k_part_b"], SKIP_SUB),
         "k_part_c": (["k_seg_c1"], SKIP_SUB), "k_seg_d": (["k_seg_scan", "k_seg_d<" if ROUND6 else "k_seg_d("], SKIP_SUB),
         "k_seg_e": (["k_seg_e<1, false>", "k_seg_e<1, true>", "k_seg_m<1>"], SKIP_STEP)}
-if os.environ.get("SEG_ARENA") == "1":  # the arena form: D alone (k_seg_da), no scan pass
+if os.environ.get("SEG_ARENA", "1") == "1":  # the arena form (default): D alone (k_seg_da), no scan pass
     plan["k_seg_d"] = (["k_seg_da<"], SKIP_SUB)
 for name, (kernels, skip) in plan.items():
     parts = {k: summarise(root, k, skip) for k in kernels}
