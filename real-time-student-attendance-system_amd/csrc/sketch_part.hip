@@ -1367,8 +1367,8 @@ struct SegArgs {
 // ctab before it waits for any other.  D then reads whole chunks: no scan
 // pass S, no run tables, no gather.
 // Measured at the 2^28 default step (profiles/r06_ab_seg_arena.txt): C1 +
-// D 0.195 -> 0.178 ms per 2^25 sub-batch at N = 1 (C1 0.100 -> 0.119, S + D
-// 0.095 -> 0.059), 0.193 -> 0.174 at the 8-way shard; step 8.87 -> 8.73 ms.
+// D 0.195 -> 0.169 ms per 2^25 sub-batch at N = 1 (C1 0.100 -> 0.110, S + D
+// 0.095 -> 0.059), 0.193 -> 0.172 at the 8-way shard; step 8.87 -> 8.63 ms.
 // 0: round 6's run-table form (k_seg_scan + k_seg_d).
 #ifndef SKE_SEG_ARENA
 #define SKE_SEG_ARENA 1
@@ -1544,17 +1544,32 @@ __global__ void __launch_bounds__(T, SegC1<T>::WPE) k_seg_c1(const PartArgs A, c
         lds_barrier();
         uint32_t total;
         const uint32_t cv = tid < S.nb1 ? cnt[tid] : 0u;
-        // (arena: the bucket's reservation, its result first used after the placement)
-        // (a buffer atomic: its address is one VGPR, rebuilt from tid, so no
-        // 64-bit pointer is kept live -- and spilled -- across the run)
+        // Arena: each bucket's reservation is rounded up to 4 records, so every
+        // reservation starts 16-B aligned; the pad holds records of rank 0 (a
+        // real record's rank is >= 1), which D skips.  The reservation is a
+        // buffer atomic issued here and first waited for after the placement
+        // (its address is one VGPR rebuilt from tid: no 64-bit pointer is kept
+        // live -- and spilled -- across the run).
+        const uint32_t cvp = SKE_SEG_ARENA ? (cv + 3) & ~3u : cv;
         uint32_t abase = 0;
         if (SKE_SEG_ARENA && cv)
             abase = uint32_t(__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(
-                int(cv), part_rsrc(S.fill, S.nsub * (S.nb1 + 1) * kSegFillStride * 4), int(seg_fill_at(S, tid) * 4), 0, 0));
-        const uint32_t ex = seg_scan(cv, ws, total);
+                int(cvp), part_rsrc(S.fill, S.nsub * (S.nb1 + 1) * kSegFillStride * 4), int(seg_fill_at(S, tid) * 4), 0,
+                0));
+        // one scan for both run layouts (arena: the padded prefix in the high
+        // half; both totals stay below 2^16)
+        uint32_t tot2;
+        const uint32_t ex2 = seg_scan(SKE_SEG_ARENA ? (cvp << 16) | cv : cv, ws, tot2);
+        const uint32_t ex = SKE_SEG_ARENA ? ex2 & 0xffffu : ex2, exp = ex2 >> 16;
+        total = SKE_SEG_ARENA ? tot2 & 0xffffu : tot2;
+        // (the padded layout when it fits the run's LDS, else the unpadded one:
+        // block-uniform)
+        const bool padded = SKE_SEG_ARENA && (tot2 >> 16) <= kSegRunSw;
         if (tid < S.nb1) {
-            cnt[tid] = ex;
+            cnt[tid] = padded ? exp : ex;
             if (!SKE_SEG_ARENA) S.o1[size_t(tid) * kSegMaxRuns + r] = ex;
+            if (padded)
+                for (uint32_t k = cv; k < cvp; k++) srec[exp + k] = 0u;
         }
         if (!SKE_SEG_ARENA && tid == 0) S.o1[size_t(S.nb1) * kSegMaxRuns + r] = total;  // [nb1] = the run's total
         lds_barrier();
@@ -1568,42 +1583,57 @@ __global__ void __launch_bounds__(T, SegC1<T>::WPE) k_seg_c1(const PartArgs A, c
                 if (SKE_SEG_ARENA) mark[at] = uint16_t(0x8000u | b);
             }
         if (SKE_SEG_ARENA) {
-            // the run's reservations (after the placement, so that no record
+            // the run's chunk slots (after the placement, so that no record
             // registers are live across them); record j of the run (bucket h)
             // is then the bucket's sequence index i = j + (base - start of h
             // in the run), in the bucket's first or second chunk of this
             // reservation (told apart by i's chunk parity)
-            const uint32_t aslot = cv ? seg_arena_slots(S, A.err, tid, cv, abase) : 0u;
+            const uint32_t aslot = cv ? seg_arena_slots(S, A.err, tid, cvp, abase) : 0u;
             lds_barrier();  // the placement's reads of cnt are done
             if (tid < S.nb1) {
-                cnt[tid] = abase - ex;
+                cnt[tid] = abase - (padded ? exp : ex);
                 slt[tid] = aslot;
             }
             lds_barrier();
-            // four records per thread: one 16-B store (dword-aligned) when
-            // they share a bucket and a chunk -- most of a run's ~57-record
-            // segments -- else one store each
-            typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
             auto slot_of = [](uint32_t i, uint32_t v) {
                 return ((i >> 13) & 1u) == (v >> 28) ? (v & 0x3fffu) : ((v >> 14) & 0x3fffu);
             };
-            for (uint32_t g = tid; g * 4 < total; g += T) {
-                const uint32_t j = g * 4;
-                const part_u32x4 v = reinterpret_cast<const part_u32x4 *>(srec)[g];
-                const uint2 mk = reinterpret_cast<const uint2 *>(mark)[g];
-                const uint32_t m[4] = {mk.x & 0xffffu, mk.x >> 16, mk.y & 0xffffu, mk.y >> 16};
-                const uint32_t h0 = m[0] & (kSegMaxB1 - 1), i0 = j + cnt[h0];
-                if (j + 4 <= total && m[3] == m[0] && (i0 & (kSegChunk - 1)) <= kSegChunk - 4) {
-                    *reinterpret_cast<u32x4a *>(S.r1 + size_t(slot_of(i0, slt[h0])) * kSegChunk +
-                                                (i0 & (kSegChunk - 1))) = u32x4a{v.x, v.y, v.z, v.w};
-                } else {
+            if (padded) {
+                // every 4-record group lies in one bucket and one chunk, 16-B
+                // aligned at both ends (a group's first record is never a pad)
+                const uint32_t ng = (tot2 >> 16) / 4;
+                for (uint32_t g = tid; g < ng; g += T) {
+                    const uint32_t h = mark[4 * g] & (kSegMaxB1 - 1), i = 4 * g + cnt[h];
+                    nt2_st<1>(reinterpret_cast<part_u32x4 *>(S.r1 + size_t(slot_of(i, slt[h])) * kSegChunk +
+                                                             (i & (kSegChunk - 1))),
+                              reinterpret_cast<const part_u32x4 *>(srec)[g]);
+                }
+            } else {
+                // (a run too full for its pads in LDS) four records per
+                // thread: one 16-B store when they share a bucket and a chunk,
+                // else one store each; each bucket's pad stored by its thread
+                typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+                for (uint32_t g = tid; g * 4 < total; g += T) {
+                    const uint32_t j = g * 4;
+                    const part_u32x4 v = reinterpret_cast<const part_u32x4 *>(srec)[g];
+                    const uint2 mk = reinterpret_cast<const uint2 *>(mark)[g];
+                    const uint32_t m[4] = {mk.x & 0xffffu, mk.x >> 16, mk.y & 0xffffu, mk.y >> 16};
+                    const uint32_t h0 = m[0] & (kSegMaxB1 - 1), i0 = j + cnt[h0];
+                    if (j + 4 <= total && m[3] == m[0] && (i0 & (kSegChunk - 1)) <= kSegChunk - 4) {
+                        *reinterpret_cast<u32x4a *>(S.r1 + size_t(slot_of(i0, slt[h0])) * kSegChunk +
+                                                    (i0 & (kSegChunk - 1))) = u32x4a{v.x, v.y, v.z, v.w};
+                    } else {
 #pragma unroll
-                    for (uint32_t e = 0; e < 4; e++) {
-                        if (j + e >= total) break;
-                        const uint32_t h = m[e] & (kSegMaxB1 - 1), i = j + e + cnt[h];
-                        S.r1[size_t(slot_of(i, slt[h])) * kSegChunk + (i & (kSegChunk - 1))] = v[e];
+                        for (uint32_t e = 0; e < 4; e++) {
+                            if (j + e >= total) break;
+                            const uint32_t h = m[e] & (kSegMaxB1 - 1), i = j + e + cnt[h];
+                            S.r1[size_t(slot_of(i, slt[h])) * kSegChunk + (i & (kSegChunk - 1))] = v[e];
+                        }
                     }
                 }
+                if (tid < S.nb1)
+                    for (uint32_t k = cv; k < cvp; k++)
+                        S.r1[size_t(slot_of(abase + k, aslot)) * kSegChunk + ((abase + k) & (kSegChunk - 1))] = 0u;
             }
             lds_barrier();  // cnt, slt and marks are rewritten by the next run
         } else {
@@ -1915,7 +1945,7 @@ __global__ void __launch_bounds__(T, SegDA<T>::WPE) k_seg_da(const SegArgs S) {
 #pragma unroll
         for (uint32_t j = 0; j < R; j++) {
             pos[j] = 0xffffffffu;
-            if ((j / 4 * T + tid) * 4 + j % 4 < n) {
+            if ((j / 4 * T + tid) * 4 + j % 4 < n && (rec[j] & 63u) != 0) {  // (rank 0: a C1 pad)
                 const uint32_t w2 = (rec[j] >> (kSegRecShift + S.klog)) & (wpb - 1);
                 pos[j] = (w2 << 16) | atomicAdd(&c2[w2], 1u);
             }

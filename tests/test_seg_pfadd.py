@@ -114,6 +114,32 @@ def test_seg_key_counts(engine, orc, nkeys, n, klog):
     assert np.array_equal(engine.registers_all(w.n_keys), regs)
 
 
+@pytest.mark.parametrize("nkeys,klog", [(4097, 1), (20_000, 3), (300, 0)])
+def test_seg_all_valid_runs(engine, orc, nkeys, klog):
+    """Every swipe valid (no invalid ids): a full C1 run holds 8192 records,
+    so the arena form's 4-record pads no longer fit its LDS and it takes the
+    unpadded layout, storing each bucket's pad itself (k_seg_c1)."""
+    from rtsas_amd import synthetic
+    from rtsas_amd.engine import DeviceBuffer
+    w = synthetic.WORKLOADS["c3"]
+    w = synthetic.Workload(**{**w.__dict__, "n_members": 100_000, "n_keys": nkeys, "invalid_frac": 0.0,
+                              "zipf_lectures": 0, "zipf_days": 0})
+    engine.reserve(0, w.bf_error, w.bf_capacity)
+    p = engine.gen_params(w)
+    engine.preload(0, p, w.n_members)
+    engine.hll_reserve(w.n_keys)
+    engine.set_option("hll_seg", 1)
+    engine.set_option("seg_klog", klog)
+    n = 900_001
+    b = engine.swipe_batch(p, 0, n)
+    out = DeviceBuffer(engine.ctx, n)
+    engine.swipes(0, b, out)
+    _, regs, answers = _oracle(orc, engine, w, p, [b])
+    assert answers[0].all()
+    assert np.array_equal(out.to_host(np.uint8, n), answers[0])
+    assert np.array_equal(engine.registers_all(w.n_keys), regs)
+
+
 def _rand_items(rng, n, maxlen, minlen=0):
     lens = rng.integers(minlen, maxlen + 1, n)
     return [rng.integers(0, 256, int(l), dtype=np.uint8).tobytes() for l in lens]
