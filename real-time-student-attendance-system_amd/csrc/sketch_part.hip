@@ -1579,8 +1579,9 @@ __global__ void __launch_bounds__(T, SegC1<T>::WPE) k_seg_c1(const PartArgs A, c
                 const uint32_t b = pos[u] >> 16, at = cnt[b] + (pos[u] & 0xffffu);
                 srec[at] = rec[u];
                 // (arena: the record's bucket, tagged so that no run's epoch
-                // (<= kSegMaxRuns < 0x8000) ever equals it)
-                if (SKE_SEG_ARENA) mark[at] = uint16_t(0x8000u | b);
+                // (<= kSegMaxRuns < 0x8000) ever equals it; the padded layout
+                // reads it at group starts only)
+                if (SKE_SEG_ARENA && (!padded || (at & 3u) == 0)) mark[at] = uint16_t(0x8000u | b);
             }
         if (SKE_SEG_ARENA) {
             // the run's chunk slots (after the placement, so that no record
