@@ -185,7 +185,6 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
 struct Scratch;  // growable device scratch, owned by the context
 constexpr int kScratchSlots = 48;
 void *scratch_get(Scratch *s, int slot, size_t bytes, hipError_t *err);
-void *scratch_get_zeroed(Scratch *s, int slot, size_t bytes, hipError_t *err);  // fresh slots zeroed
 void scratch_set_recording(Scratch *s, bool on);  // slots handed out now get pinned
 void scratch_unpin(Scratch *s);                    // every graph freed: slots may grow
 

@@ -58,23 +58,6 @@ void *scratch_get(Scratch *s, int slot, size_t bytes, hipError_t *err) {
     return s->p[slot];
 }
 
-// scratch_get, and a slot (re)allocated by this call is zeroed before it is
-// returned (never during a capture: a recorded slot cannot grow)
-void *scratch_get_zeroed(Scratch *s, int slot, size_t bytes, hipError_t *err) {
-    void *const old = s->p[slot];
-    const size_t oc = s->cap[slot];
-    void *p = scratch_get(s, slot, bytes, err);
-    if (p && (p != old || s->cap[slot] != oc)) {
-        hipError_t e = hipMemset(p, 0, s->cap[slot]);
-        if (e == hipSuccess) e = hipDeviceSynchronize();
-        if (e != hipSuccess) {
-            *err = e;
-            return nullptr;
-        }
-    }
-    return p;
-}
-
 void scratch_free_all(Scratch *s) {
     for (int i = 0; i < kScratchSlots; i++)
         if (s->p[i]) (void)hipFree(s->p[i]);

@@ -2560,7 +2560,7 @@ static hipError_t seg_scratch(const SegPlan &P, uint32_t sub, uint64_t n, Scratc
         S->r1 = (uint32_t *)scratch_get(scr, 32, size_t(P.nb1 * kst + dyn) * kSegChunk * 4, &e);
         if (e == hipSuccess)
             S->fill = (uint32_t *)scratch_get(scr, 40, size_t(P.nsub) * (P.nb1 + 1) * kSegFillStride * 4, &e);
-        if (e == hipSuccess) S->ctab = (uint32_t *)scratch_get_zeroed(scr, 41, size_t(P.nb1) * S->kmaxc * 4, &e);
+        if (e == hipSuccess) S->ctab = (uint32_t *)scratch_get(scr, 41, size_t(P.nb1) * S->kmaxc * 4, &e);
     } else {
         S->r1 = (uint32_t *)scratch_get(scr, 32, size_t((m + kSegRunSw - 1) / kSegRunSw) * kSegRunSw * 4, &e);
         if (e == hipSuccess) S->o1 = (uint32_t *)scratch_get(scr, 33, size_t(P.nb1 + 1) * kSegMaxRuns * 4, &e);
@@ -2724,8 +2724,12 @@ hipError_t launch_swipes_part(const ChainDev &ch, const PartBatch *bt, uint32_t 
             if (seg) {
                 S.s = si % P.nsub;
                 S.nruns = (A.ntiles + kSegRunTiles - 1) / kSegRunTiles;
-                if (SKE_SEG_ARENA && S.s == 0) {  // the group's fill counts
+                if (SKE_SEG_ARENA && S.s == 0) {
+                    // the group's fill counts, and the chunk table (D clears
+                    // what C1 published, so this only matters for a fresh
+                    // buffer or a call that stopped between C1 and D)
                     e = hipMemsetAsync(S.fill, 0, size_t(P.nsub) * (P.nb1 + 1) * kSegFillStride * 4, st);
+                    if (e == hipSuccess) e = hipMemsetAsync(S.ctab, 0, size_t(P.nb1) * S.kmaxc * 4, st);
                     if (e != hipSuccess) return e;
                 }
                 hipLaunchKernelGGL(k_seg_c1<SKE_SEG_C1T>, dim3(std::min(S.nruns, unsigned(cus) * SegC1<SKE_SEG_C1T>::BPC)),
