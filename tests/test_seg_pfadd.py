@@ -154,7 +154,10 @@ def _pack(items):
 
 def test_seg_ragged_ids_hot_key(engine, orc):
     """0..40-byte ids (pass A's generic hash), one key taking 60 % of the
-    swipes (a bucket whose runs fill whole chunks), C3's one-link filter."""
+    swipes (a bucket whose runs fill whole chunks), C3's one-link filter.
+    In the arena form the hot key's bucket holds ~12 chunks against kstat = 6
+    fixed slots per bucket (16 buckets, 22 chunks): its later chunks take
+    counted slots through the chunk table."""
     import ctypes as C
     from rtsas_amd.engine import DeviceBatch, DeviceBuffer
     rng = np.random.default_rng(5)
